@@ -1,0 +1,215 @@
+"""Benchmark: converged power-flow scenarios/s on the 123-bus feeder (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Workload = BASELINE config 2: synthetic 123-bus feeder (seed 123), a batch of
+4096 seeded load/DER scenarios per GPU (weak scaling; scenario ids are global,
+rank r solves ids [r*4096, (r+1)*4096)).  One step = one pass of the hot path
+over that batch: libfreedm_pf's tiled DPF kernel (all sweeps, fused loss/Vmin/
+Vmax) plus the deterministic batch aggregate, inputs resident in HBM.  After
+the K timed steps the per-GPU aggregates are combined once by an RCCL
+all-reduce (the only collective of the path).  value = converged scenarios of
+all ranks / max-over-ranks wall time of the timed region.
+
+Also reported: the roofline of the dominant kernel (algorithmic bytes per
+SURVEY.md 8(d) / its HIP-event time), and the CPU oracle (oracle/ref_dpf.c,
+a scalar port) timed on the host's cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SCEN_PER_GPU = 4096
+FEEDER_NODES, FEEDER_SEED, SCEN_SEED = 123, 123, 4096
+
+
+def bytes_alg_per_scenario(nb: int, nn: int) -> int:
+    """S in (48 B per branch) + V out (48 B per node) + iters,
+    loss, Vmin, Vmax (28 B); state-resident model (state stays in LDS)."""
+    return 48 * nb + 48 * nn + 28
+
+
+def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
+    from oracle import oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    from freedm_amd import scenario_loads
+    pq = scenario_loads(feeder, np.arange(chunk), seed=SCEN_SEED)
+    n_conv = 0
+    n_done = 0
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        r = O.dpf_batch(feeder.Dl, feeder.Z, pq, nthreads=threads, want_full=False)
+        n_conv += int((r["status"] == 0).sum())
+        n_done += chunk
+        passes += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n_conv / dt, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} passes x {chunk} scenarios of the config-2 batch (123-bus, seed {SCEN_SEED}), "
+                      f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _pmc_traffic():
+    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3
+    --pmc summary (profiles/pmc_traffic.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        if d.get("workload") == f"{FEEDER_NODES}-bus x {SCEN_PER_GPU}":
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scenarios", type=int, default=SCEN_PER_GPU, help="scenarios per GPU per step")
+    ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
+
+    feeder = synthetic_feeder(FEEDER_NODES, FEEDER_SEED)
+    pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile)
+    B = args.scenarios
+    pf.reserve(B)
+    ids = np.arange(rank * B, (rank + 1) * B)
+    d_pq = torch.from_numpy(scenario_loads(feeder, ids, seed=SCEN_SEED)).to(dev)
+    out = {"iters": torch.zeros(B, dtype=torch.int32, device=dev),
+           "status": torch.zeros(B, dtype=torch.int8, device=dev),
+           "loss": torch.zeros(B, dtype=torch.float64, device=dev),
+           "vmin": torch.zeros(B, dtype=torch.float64, device=dev),
+           "vmax": torch.zeros(B, dtype=torch.float64, device=dev),
+           "v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
+           "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
+    stream = torch.cuda.current_stream(dev)
+    agg_all = torch.zeros((max(args.steps, 1) + args.warmup, 8), dtype=torch.float64, device=dev)
+    agg_ptr = [agg_all[i] for i in range(agg_all.shape[0])]
+    solve, aggregate = pf.bind_device(d_pq, out, stream=stream)
+
+    def step(i, ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        solve()                      # the DPF kernel: all sweeps + fused loss / Vmin / Vmax
+        if ev1 is not None:
+            ev1.record(stream)
+        aggregate(agg_ptr[i])        # deterministic batch aggregate (8 doubles per step)
+
+    for i in range(args.warmup):
+        step(args.steps + i)
+    torch.cuda.synchronize(dev)
+    conv_per_step = int((out["status"] == 0).sum().item())
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, *evs[i])
+    a = agg_all[:args.steps]
+    total = torch.cat([a[:, 0].sum().view(1), a[:, 1].min().view(1), a[:, 2].max().view(1), a[:, 3:].sum(0)])
+    if world > 1:
+        # the one collective: combine the per-GPU study aggregates over RCCL/xGMI
+        mm = torch.stack([total[1], -total[2]])
+        dist.all_reduce(total, op=dist.ReduceOp.SUM)
+        dist.all_reduce(mm, op=dist.ReduceOp.MIN)
+        total[1], total[2] = mm[0], -mm[1]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    tot = total.cpu().numpy()
+    n_conv_all = float(tot[3])
+    value = n_conv_all / elapsed
+    nb, nn = pf.info["nb"], pf.nn
+    bpa = bytes_alg_per_scenario(nb, nn)
+    achieved = bpa * B / avg_kern_s / 1e9
+    traffic = _pmc_traffic()
+
+    if rank == 0:
+        res = {
+            "metric": "converged power-flow scenarios/sec, 123-bus feeder",
+            "value": value,
+            "unit": "scenarios/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64 (complex fp64)",
+            "data": "synthetic (seeded 123-bus radial feeder + seeded load/PV scenarios)",
+            "config": {"workload": f"BASELINE config 2: 123-bus feeder, {B} scenarios per GPU per step",
+                       "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
+                       "tile": pf.info["tile"], "parallelism": f"scenario shards x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "dpf_tiled_kernel" if pf.kernel == "tiled" else "dpf_generic_kernel",
+                         "bytes_alg_per_scenario": bpa, "kernel_ms": avg_kern_s * 1e3},
+            "aggregate": {"loss_sum_kw": float(tot[0]), "vmin": float(tot[1]), "vmax": float(tot[2]),
+                          "n_conv": int(tot[3]), "n_nonconv": int(tot[4]), "n_over": int(tot[5]),
+                          "n_under": int(tot[6]), "n_scen": int(tot[7])},
+            "converged_per_step_rank0": conv_per_step,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(feeder, seconds=args.cpu_seconds)
+            res["speedup_vs_cpu"] = value / res["cpu_baseline"]["value"]
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

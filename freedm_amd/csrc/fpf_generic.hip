@@ -1,0 +1,209 @@
+// fpf_generic.hip -- the generic batched DPF kernel for gfx950.
+//
+// One lane per scenario; every lane runs the reference's sweep program
+// (DPF_return7.cpp:102-218) verbatim from the feeder's op lists, so it is exact
+// for ANY feeder that passes the index checks (including the malformed orders
+// the tiled kernel refuses).  Per-scenario state (Sld, V, IL, Ib) is streamed
+// through HBM in a scenario-fastest SoA layout -- slot k, field f of scenario s
+// at base[(2k+f)*ld + s] -- so consecutive lanes touch consecutive doubles.
+// The op lists are wave-uniform (scalar loads); lanes diverge only at their own
+// convergence break (a converged lane stops updating, like the reference).
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fpf {
+
+namespace {
+
+struct Slots {
+    double *base;
+    size_t ld;
+    int s;
+    __device__ __forceinline__ cx ld_(int slot) const {
+        return mk(base[(size_t)(2 * slot) * ld + s], base[(size_t)(2 * slot + 1) * ld + s]);
+    }
+    __device__ __forceinline__ void st(int slot, cx v) const {
+        base[(size_t)(2 * slot) * ld + s] = v.re;
+        base[(size_t)(2 * slot + 1) * ld + s] = v.im;
+    }
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
+                                                          const double *__restrict__ pq,
+                                                          double *__restrict__ scr, size_t ld,
+                                                          OutDev o) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const int nl = f.nl, nn = f.nn;
+    const Slots Sld{scr, ld, s};
+    const Slots V{scr + (size_t)nl * 6 * ld, ld, s};
+    const Slots IL{scr + (size_t)nl * 12 * ld, ld, s};
+    const Slots Ib{scr + (size_t)(2 * nl + nn) * 6 * ld, ld, s};
+    const cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+
+    // Sld = (P + jQ) / (bkva/3)   DPF_return7.cpp:46-50
+    for (int j = 0; j < nl; ++j)
+        for (int p = 0; p < 3; ++p) {
+            const cx sl = mk(pq[((size_t)(2 * p) * nl + j) * B + s], pq[((size_t)(2 * p + 1) * nl + j) * B + s]);
+            Sld.st(j * 3 + p, cdiv(sl, mk(f.s3, 0.0)));
+            V.st(j * 3 + p, v0[p]);                                  // :92-96
+        }
+
+    cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    int iters = 0, status = 1;
+    for (int it = 0; it < f.mxitr; ++it) {
+        // load currents  :106-130
+        for (int k = 0; k < nn * 3; ++k) IL.st(k, mk(0, 0));
+        for (int q = 0; q < f.n_il; ++q) {
+            const IlOp op = f.il_ops[q];
+            for (int p = 0; p < 3; ++p)
+                IL.st((op.ndr - 1) * 3 + p, load_current(Sld.ld_(op.row * 3 + p), V.ld_(op.ndr * 3 + p)));
+        }
+        // backward sweep  :134-160
+        for (int k = 0; k < (nn - 1) * 3; ++k) Ib.st(k, mk(0, 0));
+        cx ibl[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+        for (int q = 0; q < f.n_bw; ++q) {
+            const BwOp op = f.bw_ops[q];
+            if (op.kind == 1) {
+                for (int p = 0; p < 3; ++p) Ib.st(op.idx * 3 + p, cadd(Ib.ld_(op.idx * 3 + p), ibl[p]));
+                for (int p = 0; p < 3; ++p) ibl[p] = mk(0, 0);
+            } else {
+                for (int p = 0; p < 3; ++p) {
+                    const cx x = cadd(cadd(Ib.ld_(op.idx * 3 + p), ibl[p]), IL.ld_(op.idx * 3 + p));
+                    Ib.st(op.idx * 3 + p, x);
+                    ibl[p] = x;
+                }
+            }
+        }
+        // forward sweep  :163-195
+        for (int q = 0; q < f.n_fw; ++q) {
+            const FwOp op = f.fw_ops[q];
+            const double *t = f.tz + 18 * (size_t)q;
+            const cx b0 = Ib.ld_(op.ib * 3 + 0), b1 = Ib.ld_(op.ib * 3 + 1), b2 = Ib.ld_(op.ib * 3 + 2);
+            for (int p = 0; p < 3; ++p) {
+                const cx sv = op.src < 0 ? v0[p] : V.ld_(op.src * 3 + p);
+                cx rv = csub(sv, drop_col(t, b0, b1, b2, p));
+                if (op.mask & (1 << p)) rv = mk(0, 0);
+                V.st(op.dst * 3 + p, rv);
+            }
+        }
+        // convergence  :199-210
+        double errmx = 0;
+        for (int p = 0; p < 3; ++p) {
+            const cx d = csub(Ib.ld_(p), ibo[p]);
+            const double df = hypot(d.re, d.im);
+            if (p == 0 || df > errmx) errmx = df;
+        }
+        for (int p = 0; p < 3; ++p) ibo[p] = Ib.ld_(p);
+        iters = it + 1;
+        if (errmx < f.eps) { status = 0; break; }
+    }
+
+    // post-processing (:222-253) fused with the VVC reductions
+    // (loss VoltVarCtrl.cpp:1152-1161, V_abc_list.cpp:7-81, Vmin/Vmax :1201-1207)
+    double acc1[3] = {0, 0, 0}, acc2[3] = {0, 0, 0}, pb0[3] = {0, 0, 0};
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int cnt[3] = {0, 0, 0};
+    for (int k = 0; k < nn; ++k) {
+        for (int p = 0; p < 3; ++p) {
+            const cx v = V.ld_(k * 3 + p);
+            const cx ib = Ib.ld_((k == 0 ? 0 : k - 1) * 3 + p);
+            const cx il = IL.ld_((k == 0 ? nn - 1 : k - 1) * 3 + p);
+            const cx sv = cmul(v, mk(f.s3, 0.0));
+            const cx sb = cmul(sv, cconj(ib));
+            const cx sl = cmul(sv, cconj(il));
+            const double mag = hypot(v.re, v.im);
+            const size_t o6 = ((size_t)(2 * p) * nn + k) * B + s, o6i = o6 + (size_t)nn * B;
+            if (o.vpolar) { o.vpolar[o6] = mag; o.vpolar[o6i] = polar_angle(v, p); }
+            if (o.pqb) { o.pqb[o6] = sb.re; o.pqb[o6i] = sb.im; }
+            if (o.pql) { o.pql[o6] = sl.re; o.pql[o6i] = sl.im; }
+            if (o.v_re) o.v_re[((size_t)p * nn + k) * B + s] = v.re;
+            if (o.v_im) o.v_im[((size_t)p * nn + k) * B + s] = v.im;
+            if (k & 1) acc2[p] += sl.re; else acc1[p] += sl.re;
+            if (k == 0) pb0[p] = sb.re;
+            if (mag != 0 && cnt[p] < f.K[p]) {
+                mn[p] = fmin(mn[p], mag);
+                mx[p] = fmax(mx[p], mag);
+                ++cnt[p];
+            }
+        }
+    }
+    double x[3], pmin[3], pmax[3];
+    for (int p = 0; p < 3; ++p) {
+        x[p] = pb0[p] - (acc1[p] + acc2[p]);
+        pmin[p] = cnt[p] < f.K[p] ? fmin(mn[p], 0.0) : mn[p];
+        pmax[p] = cnt[p] < f.K[p] ? fmax(mx[p], 0.0) : mx[p];
+    }
+    const double loss = ((0.0 + x[0]) + x[2]) + (0.0 + x[1]);
+    double vmin = pmin[0], vmax = pmax[0];
+    for (int p = 1; p < 3; ++p) {
+        if (pmin[p] < vmin) vmin = pmin[p];
+        if (pmax[p] > vmax) vmax = pmax[p];
+    }
+    if (o.iters) o.iters[s] = iters;
+    if (o.status) o.status[s] = (int8_t)status;
+    if (o.loss) o.loss[s] = loss;
+    if (o.vmin) o.vmin[s] = vmin;
+    if (o.vmax) o.vmax[s] = vmax;
+}
+
+hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
+                          size_t ld, const OutDev &o, hipStream_t st) {
+    const int block = 256;
+    const int grid = (n_scen + block - 1) / block;
+    hipLaunchKernelGGL(dpf_generic_kernel, dim3(grid), dim3(block), 0, st, f, n_scen, pq, scratch, ld, o);
+    return hipGetLastError();
+}
+
+// Deterministic batch aggregate (fixed thread->scenario map and fixed tree):
+// [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over, n_under, n_scen]
+__global__ __launch_bounds__(1024) void dpf_aggregate_kernel(int B, const int8_t *__restrict__ status,
+                                                             const double *__restrict__ loss,
+                                                             const double *__restrict__ vmin,
+                                                             const double *__restrict__ vmax,
+                                                             double lb_v, double ub_v, double *agg) {
+    __shared__ double sh[8][1024];
+    const int t = threadIdx.x;
+    double ls = 0, mn = INFINITY, mx = -INFINITY, nc = 0, nnc = 0, no = 0, nu = 0;
+    for (int s = t; s < B; s += blockDim.x) {
+        if (status[s] == 0) {
+            ls += loss[s];
+            mn = fmin(mn, vmin[s]);
+            mx = fmax(mx, vmax[s]);
+            nc += 1;
+            if (vmax[s] > ub_v) no += 1;
+            if (vmin[s] < lb_v) nu += 1;
+        } else {
+            nnc += 1;
+        }
+    }
+    sh[0][t] = ls; sh[1][t] = mn; sh[2][t] = mx; sh[3][t] = nc;
+    sh[4][t] = nnc; sh[5][t] = no; sh[6][t] = nu;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            sh[0][t] += sh[0][t + w];
+            sh[1][t] = fmin(sh[1][t], sh[1][t + w]);
+            sh[2][t] = fmax(sh[2][t], sh[2][t + w]);
+            for (int q = 3; q < 7; ++q) sh[q][t] += sh[q][t + w];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        for (int q = 0; q < 7; ++q) agg[q] = sh[q][0];
+        agg[7] = (double)B;
+    }
+}
+
+hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss, const double *vmin,
+                            const double *vmax, double lb_v, double ub_v, double *d_agg, hipStream_t st) {
+    hipLaunchKernelGGL(dpf_aggregate_kernel, dim3(1), dim3(1024), 0, st, n_scen, status, loss, vmin, vmax,
+                       lb_v, ub_v, d_agg);
+    return hipGetLastError();
+}
+
+}  // namespace fpf

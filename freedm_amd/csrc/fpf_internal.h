@@ -1,0 +1,91 @@
+// fpf_internal.h -- tables shared by the host side (fpf_api.cpp) and the gfx950
+// kernels (fpf_kernels.hip).  Everything the kernels read about a feeder is
+// precomputed once by fpf_feeder_create and lives in device memory.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fpf {
+
+// One forward-sweep update V(dst) = V(src) - lng * (Ib(ib) . Zl(code)), then
+// phase p zeroed when bit p of mask is set (DPF_return7.cpp:163-195).
+// src < 0 means the constant V0 (the special first branch, :168).
+struct FwOp {
+    int32_t dst, src, ib, code, mask, pad;
+};
+
+// Backward-sweep op (DPF_return7.cpp:136-160), executed in list order:
+//   kind 0 (branch)    : Ib[idx] = (Ib[idx] + Ibl) + IL[idx];  Ibl = Ib[idx]
+//   kind 1 (separator) : Ib[idx] = Ib[idx] + Ibl;              Ibl = 0
+struct BwOp {
+    int32_t kind, idx;
+};
+
+// Load-current op (DPF_return7.cpp:107-130): IL[ndr-1] = conj(Sld[row]/V[ndr]).
+struct IlOp {
+    int32_t row, ndr;
+};
+
+// Per-node table of the tiled kernel (well-formed feeders only): node k >= 1
+// owns exactly one branch row; the forward op writing V(k) and the load
+// current IL(k-1) both belong to that row.
+struct NodeOp {
+    int32_t fw;      // index of the node's forward op (its TEMP block in FeederDev.tz)
+    int32_t row;     // Dl row whose rbus == k (loads of the node)
+    int32_t code;    // 0-based line code
+    int32_t mask;    // phase-zeroing bits (0 for the special first branch)
+    int32_t tap;     // tap-accumulator slot, -1 if no separator targets k
+};
+
+// Sequential-stage program of the tiled kernel (one entry per Dl row).
+//   backward, reverse row order: node >= 1 -> branch of that node, tap1 = its
+//            tap-accumulator slot + 1 (0 = none); node == 0 -> separator adding
+//            Ibl into accumulator tap1 - 1
+//   forward, row order: V(dst) = V(src) - drop(dst), phases in `mask` zeroed;
+//            src == 0 reads the constant V0 kept in slot 0
+struct SeqBw { int16_t node, tap1; };
+struct SeqFw { int16_t dst; uint16_t src_mask; };   // src = low 13 bits, mask = top 3
+
+struct FeederDev {
+    // sizes
+    int32_t nl, nn, ncode;
+    int32_t n_il, n_bw, n_fw;
+    int32_t K[3];            // Lnum_p + 1 (V_abc_list.cpp:12-17)
+    int32_t n_taps, mxitr;
+    // constants
+    double V0[6];            // re/im per phase (DPF_return7.cpp:84-89)
+    double s3;               // bkva / 3
+    double eps;
+    double lb_v, ub_v;
+    // device tables
+    const double *tz;        // [n_fw][3][3] complex interleaved: TEMP(L,a) of each
+                             // forward op = cx(lng,0)*cx(1,0)*(Z(L,a)/Zb)
+    const IlOp *il_ops;
+    const BwOp *bw_ops;
+    const FwOp *fw_ops;
+    const NodeOp *node_ops;  // [nn] (index 0 unused) -- tiled only
+    const SeqBw *seq_bw;     // tiled only
+    const SeqFw *seq_fw;     // tiled only
+    int32_t n_seq_bw, n_seq_fw;
+};
+
+// Device views of the caller's output buffers ([col][row][B], scenario fastest).
+struct OutDev {
+    double *vpolar, *pqb, *pql, *v_re, *v_im;
+    int32_t *iters;
+    int8_t *status;
+    double *loss, *vmin, *vmax;
+};
+
+// launchers (fpf_kernels.hip)
+hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
+                          size_t ld, const OutDev &o, hipStream_t st);
+hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
+                        int tile, hipStream_t st);
+hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss,
+                            const double *vmin, const double *vmax, double lb_v, double ub_v,
+                            double *d_agg, hipStream_t st);
+size_t tiled_lds_bytes(const FeederDev &f, int tile);
+int tiled_max_tile(const FeederDev &f);
+
+}  // namespace fpf

@@ -1,0 +1,79 @@
+// fpf_math.hpp -- complex-fp64 arithmetic with the reference's operation order
+// (SURVEY.md 8(a) A9), for host precomputation and gfx950 device code alike.
+// The library is compiled with -ffp-contract=off: the reference is ISO C++98
+// built without FMA contraction, and bit-exact V needs the same roundings.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#pragma clang fp contract(off)
+
+namespace fpf {
+
+struct cx {
+    double re, im;
+};
+
+__host__ __device__ __forceinline__ cx mk(double r, double i) { cx z; z.re = r; z.im = i; return z; }
+__host__ __device__ __forceinline__ cx cadd(cx a, cx b) { return mk(a.re + b.re, a.im + b.im); }
+__host__ __device__ __forceinline__ cx csub(cx a, cx b) { return mk(a.re - b.re, a.im - b.im); }
+// GCC's inline expansion of std::complex<double> * std::complex<double>
+__host__ __device__ __forceinline__ cx cmul(cx x, cx y) {
+    return mk(x.re * y.re - x.im * y.im, x.re * y.im + x.im * y.re);
+}
+__host__ __device__ __forceinline__ cx cconj(cx a) { return mk(a.re, -a.im); }
+
+// libgcc __divdc3 (Smith's method): what GCC emits for std::complex<double> '/'
+__host__ __device__ __forceinline__ cx cdiv(cx x, cx y) {
+    const double a = x.re, b = x.im, c = y.re, d = y.im;
+    cx r;
+    if (fabs(c) < fabs(d)) {
+        const double ratio = c / d;
+        const double denom = (c * ratio) + d;
+        r.re = ((a * ratio) + b) / denom;
+        r.im = ((b * ratio) - a) / denom;
+    } else {
+        const double ratio = d / c;
+        const double denom = (d * ratio) + c;
+        r.re = ((b * ratio) + a) / denom;
+        r.im = (b - (a * ratio)) / denom;
+    }
+    return r;
+}
+
+// Load current of one phase, DPF_return7.cpp:117-125:
+//   abs(v) == 0 ? 0 : conj(S / v)
+__host__ __device__ __forceinline__ cx load_current(cx s, cx v) {
+    if (v.re == 0.0 && v.im == 0.0) return mk(0.0, 0.0);
+    return cconj(cdiv(s, v));
+}
+
+// TEMP(L,a) = ALPHA * Zt(L,a) with ALPHA = cx(lng,0)*cx(1,0) (Armadillo folds the
+// scalar lng into the gemm alpha).  Feeder-static, so the host precomputes it.
+__host__ __device__ __forceinline__ cx zgemm_temp(double lng, cx z) {
+    const cx alpha = cmul(mk(lng, 0.0), mk(1.0, 0.0));
+    return cmul(alpha, z);
+}
+
+// Column a of lng * (Ib(1x3) * Zt(3x3)) in reference-BLAS ZGEMM order:
+//   C(1,a) = ((0 + TEMP(0,a)*Ib0) + TEMP(1,a)*Ib1) + TEMP(2,a)*Ib2
+// t points at the op's 9 interleaved TEMP values, t[2*(L*3+a)] = Re TEMP(L,a).
+__host__ __device__ __forceinline__ cx drop_col(const double *t, const cx ib0, const cx ib1,
+                                                const cx ib2, int a) {
+    cx c = mk(0.0, 0.0);
+    c = cadd(c, cmul(mk(t[2 * (0 * 3 + a)], t[2 * (0 * 3 + a) + 1]), ib0));
+    c = cadd(c, cmul(mk(t[2 * (1 * 3 + a)], t[2 * (1 * 3 + a) + 1]), ib1));
+    c = cadd(c, cmul(mk(t[2 * (2 * 3 + a)], t[2 * (2 * 3 + a) + 1]), ib2));
+    return c;
+}
+
+// Vpolar angle, DPF_return7.cpp:232-235
+[[maybe_unused]] static __host__ __device__ __noinline__ double polar_angle(cx v, int phase) {
+    double ang = (180.0 / 3.14159265358979323846) * atan(v.im / v.re);
+    if (!isfinite(ang)) ang = 0.0;
+    if (phase == 1) ang = ang - 180;
+    if (phase == 2) ang = ang + 180;
+    return ang;
+}
+
+}  // namespace fpf

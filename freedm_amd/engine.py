@@ -1,0 +1,238 @@
+"""Host-side mirror of the reference's power-flow interface over the C ABI.
+
+    PowerFlow(feeder)            one fpf_ctx + fpf_feeder (device tables uploaded once)
+      .solve(pq)                 host numpy batch  -> fpf_solve_batch
+      .solve_device(pq, out)     device buffers    -> fpf_solve_batch_device (async)
+    DPF_return7(Dl, Z)           the reference call (Broker/src/vvc/DPF_return7.cpp:8),
+                                 a 1-scenario batch returning a VPQ record
+                                 (fun_return.h:43-51); raises on non-convergence
+                                 like the reference's Armadillo logic_error.
+
+Every solve runs on the GPU through libfreedm_pf; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .feeder import Feeder
+
+__all__ = ["PowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError"]
+
+
+class DPFError(RuntimeError):
+    """A libfreedm_pf error (FPF_ERR_*)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"fpf error {code}: {msg}")
+        self.code = code
+
+
+class NonConvergedError(DPFError):
+    """DPF_return7 did not converge in mxitr sweeps.  The reference throws a
+    std::logic_error (size mismatch, DPF_return7.cpp:100-101,242) at this point."""
+
+
+def _ptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())      # torch tensor on the device
+
+
+class _Ctx:
+    _by_dev: dict = {}
+
+    def __init__(self, device: int):
+        L = _lib.load()
+        h = C.c_void_p()
+        rc = L.fpf_ctx_create(device, C.byref(h))
+        if rc:
+            raise DPFError(rc, f"fpf_ctx_create(device={device}) failed (no HIP device?)")
+        self.h = h
+        self.device = device
+
+    @classmethod
+    def get(cls, device: int) -> "_Ctx":
+        if device not in cls._by_dev:
+            cls._by_dev[device] = _Ctx(device)
+        return cls._by_dev[device]
+
+    def err(self) -> str:
+        return _lib.load().fpf_last_error(self.h).decode()
+
+
+@dataclass
+class VPQ:
+    """Result record of DPF_return7 (fun_return.h:43-51)."""
+    Vpolar: np.ndarray   # Nn x 6
+    PQb: np.ndarray      # Nn x 6
+    PQL: np.ndarray      # Nn x 6
+    Qset_a: np.ndarray   # Dl.col(7)
+    Qset_b: np.ndarray   # Dl.col(9)
+    Qset_c: np.ndarray   # Dl.col(11)
+    V: np.ndarray        # Nn x 3 complex (not in the reference record; row order of Vpolar)
+    iters: int
+    loss: float
+    vmin: float
+    vmax: float
+
+
+class PowerFlow:
+    """Batched DPF_return7 on one GPU for one feeder."""
+
+    def __init__(self, feeder: Feeder, device: int = 0, kernel: str = "auto", tile: int = 0, **opts):
+        L = _lib.load()
+        self.feeder = feeder
+        self.ctx = _Ctx.get(device)
+        o = _lib.default_opts(kernel=kernel, tile=tile, **opts)
+        self.opts = o
+        dl = np.asfortranarray(feeder.Dl, dtype=np.float64)
+        Z = np.asarray(feeder.Z, dtype=np.complex128)
+        zbuf = np.zeros(max(2 * Z.size, 2))
+        zbuf[0:2 * Z.size:2] = Z.real.ravel(order="F")
+        zbuf[1:2 * Z.size:2] = Z.imag.ravel(order="F")
+        h = C.c_void_p()
+        rc = L.fpf_feeder_create(self.ctx.h, dl.ctypes.data_as(_lib._dp), dl.shape[0], dl.shape[1],
+                                 zbuf.ctypes.data_as(_lib._dp), Z.shape[0], Z.shape[1], C.byref(o), C.byref(h))
+        if rc:
+            raise DPFError(rc, self.ctx.err())
+        self.h = h
+        info = _lib.FpfFeederInfo()
+        L.fpf_feeder_get_info(h, C.byref(info))
+        self.info = info.as_dict()
+        self.nl, self.nn = self.info["nl"], self.info["nn"]
+        self.kernel = {1: "generic", 2: "tiled"}[self.info["kernel"]]
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                _lib.load().fpf_feeder_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def reserve(self, n_scen: int) -> None:
+        rc = _lib.load().fpf_feeder_reserve(self.h, int(n_scen))
+        if rc:
+            raise DPFError(rc, self.ctx.err())
+
+    # ------------------------------------------------------------------ host batch
+    def solve(self, pq: np.ndarray, full: bool = True) -> dict:
+        """Solve B scenarios.  pq: [6][Nl][B] float64 (P1 Q1 P2 Q2 P3 Q3 of each
+        Dl row, scenario fastest).  Returns per-scenario arrays ([col][row][B])
+        and the batch aggregate."""
+        L = _lib.load()
+        pq = np.ascontiguousarray(pq, dtype=np.float64)
+        if pq.ndim != 3 or pq.shape[:2] != (6, self.nl):
+            raise ValueError(f"pq must be [6][{self.nl}][B]")
+        B = pq.shape[2]
+        nn = self.nn
+        r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
+             "vmin": np.zeros(B), "vmax": np.zeros(B)}
+        if full:
+            r.update(Vpolar=np.zeros((6, nn, B)), PQb=np.zeros((6, nn, B)), PQL=np.zeros((6, nn, B)),
+                     V_re=np.zeros((3, nn, B)), V_im=np.zeros((3, nn, B)))
+        out = _lib.FpfOutputs(_ptr(r.get("Vpolar")), _ptr(r.get("PQb")), _ptr(r.get("PQL")), _ptr(r.get("V_re")),
+                              _ptr(r.get("V_im")), _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]),
+                              _ptr(r["vmin"]), _ptr(r["vmax"]))
+        agg = _lib.FpfAggregate()
+        rc = L.fpf_solve_batch(self.h, B, pq.ctypes.data_as(_lib._dp), C.byref(out), C.byref(agg))
+        if rc < 0:
+            raise DPFError(rc, self.ctx.err())
+        r["n_nonconv"] = rc
+        r["aggregate"] = agg.as_dict()
+        return r
+
+    # ------------------------------------------------------------------ device batch
+    def solve_device(self, pq, out: dict, agg=None, stream=None) -> None:
+        """Enqueue a solve on device buffers (torch tensors or raw pointers).
+        pq: [6][Nl][B] float64 on the device; out: dict with any of
+        vpolar/pqb/pql/v_re/v_im/iters/status/loss/vmin/vmax; agg: 8 float64."""
+        L = _lib.load()
+        B = int(pq.shape[2])
+        g = out.get
+        o = _lib.FpfOutputs(_ptr(g("vpolar")), _ptr(g("pqb")), _ptr(g("pql")), _ptr(g("v_re")), _ptr(g("v_im")),
+                            _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")))
+        st = None
+        if stream is not None:
+            st = stream if isinstance(stream, int) else int(stream.cuda_stream)
+        rc = L.fpf_solve_batch_device(self.h, B, _ptr(pq), C.byref(o), _ptr(agg), st)
+        if rc < 0:
+            raise DPFError(rc, self.ctx.err())
+
+    def bind_device(self, pq, out: dict, agg=None, stream=None):
+        """Pre-bind the ctypes arguments of a device solve (and optional aggregate)
+        and return (solve, aggregate) zero-argument callables -- the per-call host
+        cost is then one foreign call each."""
+        L = _lib.load()
+        B = int(pq.shape[2])
+        g = out.get
+        o = _lib.FpfOutputs(_ptr(g("vpolar")), _ptr(g("pqb")), _ptr(g("pql")), _ptr(g("v_re")), _ptr(g("v_im")),
+                            _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")))
+        st = C.c_void_p(None if stream is None else (stream if isinstance(stream, int) else int(stream.cuda_stream)))
+        h, pq_p, o_ref = self.h, C.c_void_p(_ptr(pq)), C.byref(o)
+        fs, fa = L.fpf_solve_batch_device, L.fpf_aggregate_device
+        keep = (o,)
+
+        def solve():
+            rc = fs(h, B, pq_p, o_ref, None, st)
+            if rc < 0:
+                raise DPFError(rc, self.ctx.err())
+
+        def aggregate(dst):
+            rc = fa(h, B, C.c_void_p(_ptr(out["status"])), C.c_void_p(_ptr(out["loss"])), C.c_void_p(_ptr(out["vmin"])),
+                    C.c_void_p(_ptr(out["vmax"])), C.c_void_p(_ptr(dst)), st)
+            if rc < 0:
+                raise DPFError(rc, self.ctx.err())
+        solve._keep = keep
+        return solve, aggregate
+
+    def aggregate_device(self, out: dict, agg, n_scen: int | None = None, stream=None) -> None:
+        """Enqueue the deterministic batch aggregate of per-scenario device outputs."""
+        L = _lib.load()
+        B = int(out["loss"].shape[0]) if n_scen is None else int(n_scen)
+        st = None
+        if stream is not None:
+            st = stream if isinstance(stream, int) else int(stream.cuda_stream)
+        rc = L.fpf_aggregate_device(self.h, B, _ptr(out["status"]), _ptr(out["loss"]), _ptr(out["vmin"]),
+                                    _ptr(out["vmax"]), _ptr(agg), st)
+        if rc < 0:
+            raise DPFError(rc, self.ctx.err())
+
+    # ------------------------------------------------------------------ reference call
+    def dpf_return7(self, Dl: np.ndarray) -> VPQ:
+        Dl = np.asarray(Dl, dtype=np.float64)
+        if Dl.shape[0] != self.nl:
+            raise ValueError("Dl rows differ from the feeder's")
+        pq = np.ascontiguousarray(Dl[:, 6:12].T)[:, :, None]
+        r = self.solve(pq, full=True)
+        if r["status"][0] != 0:
+            raise NonConvergedError(1, f"DPF did not converge in {int(r['iters'][0])} sweeps")
+        V = (r["V_re"][:, :, 0] + 1j * r["V_im"][:, :, 0]).T
+        return VPQ(Vpolar=r["Vpolar"][:, :, 0].T.copy(), PQb=r["PQb"][:, :, 0].T.copy(),
+                   PQL=r["PQL"][:, :, 0].T.copy(), Qset_a=Dl[:, 7:8].copy(), Qset_b=Dl[:, 9:10].copy(),
+                   Qset_c=Dl[:, 11:12].copy(), V=V, iters=int(r["iters"][0]), loss=float(r["loss"][0]),
+                   vmin=float(r["vmin"][0]), vmax=float(r["vmax"][0]))
+
+
+_pf_cache: dict = {}
+
+
+def DPF_return7(Dl: np.ndarray, Z: np.ndarray, device: int = 0) -> VPQ:
+    """Drop-in for `VPQ DPF_return7(arma::mat Dl, arma::cx_mat Z)`.
+
+    The feeder topology (columns 0..5) and Z are uploaded once and cached; the
+    loads (columns 6..11) travel per call."""
+    Dl = np.asarray(Dl, dtype=np.float64)
+    Z = np.asarray(Z, dtype=np.complex128)
+    key = (device, Dl.shape, Dl[:, :6].tobytes(), Z.tobytes())
+    pf = _pf_cache.get(key)
+    if pf is None:
+        pf = PowerFlow(Feeder(Dl, Z), device=device)
+        _pf_cache[key] = pf
+    return pf.dpf_return7(Dl)

@@ -1,0 +1,169 @@
+/*
+ * freedm_pf.h -- C ABI of libfreedm_pf, the MI355X (gfx950) batched distribution
+ * power-flow engine that replaces the FREEDM DGI Broker's VVC power-flow call.
+ *
+ * Reference interface replaced (vmuthuk2/FREEDM, paths relative to the repo):
+ *   VPQ DPF_return7(arma::mat Dl, arma::cx_mat Z)
+ *       declared Broker/src/vvc/fun_return.h:53, defined DPF_return7.cpp:8-263
+ *       called   Broker/src/vvc/VoltVarCtrl.cpp:1141, 1379, 1466, 1600, 1687
+ *   struct VPQ {Vpolar, PQb, PQL, Ib, IL, Qset_a/b/c}   fun_return.h:43-51
+ *   plus the reductions VVC takes from each solve:
+ *       loss        VoltVarCtrl.cpp:1152-1161
+ *       Vmin/Vmax   VoltVarCtrl.cpp:1201-1207 with V_abc_list.cpp:7-81 and
+ *                   Lnum_a/b/c of form_Yabc.cpp:46-58
+ *
+ * One fpf_solve_batch call evaluates B scenarios of one feeder: scenario s is
+ * DPF_return7 on the feeder's Dl with columns 6..11 replaced by pq[.][.][s].
+ * B = 1 with pq = Dl.colptr(6) is exactly one DPF_return7 call.
+ *
+ * Compiles as C89 and as C++98 -pedantic (the Broker builds with -std=c++98,
+ * Broker/CMakeLists.txt:55): C linkage, <stddef.h> types only.
+ *
+ * Layout conventions
+ *   Dl    : Nl x ncols (ncols >= 12) float64, column-major  (= arma::mat::memptr())
+ *   Z     : z_rows x z_cols complex128, column-major, interleaved (re, im)
+ *           (= reinterpret_cast<const double*>(arma::cx_mat::memptr()))
+ *   pq    : [6][Nl][B] float64, scenario fastest; field order P1 Q1 P2 Q2 P3 Q3
+ *           (= Dl columns 6..11).  For B = 1 this is Dl.colptr(6).
+ *   per-scenario matrix outputs: [col][row][B], scenario fastest; for B = 1 each
+ *           is the column-major Nn x 6 (or Nn x 3) Armadillo matrix of the VPQ field.
+ *   Row k of every Nn-row output is node k (row 0 = substation), which is the
+ *   Vpolar/PQb/PQL row order of DPF_return7.cpp:236-252.
+ *
+ * Error convention (no exceptions cross the ABI; the reference threw instead):
+ *   return >= 0 : number of scenarios with status FPF_NONCONVERGED (results of
+ *                 all scenarios are written; status[] says which)
+ *   return <  0 : FPF_ERR_* ; fpf_last_error(ctx) has the message
+ *
+ * Threading: one fpf_ctx per host thread; calls on one ctx are not re-entrant.
+ * fpf_solve_batch blocks until results are in host memory (the reference call
+ * was synchronous on the Broker's io_service thread, CBroker.cpp:582-612).
+ */
+#ifndef FREEDM_PF_H
+#define FREEDM_PF_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FPF_ABI_VERSION 1
+
+/* return codes */
+#define FPF_OK               0
+#define FPF_ERR_ARG         -1   /* NULL / inconsistent argument                          */
+#define FPF_ERR_TOPOLOGY    -2   /* Dl/Z index out of range: the reference's Armadillo     */
+                                 /* bounds check throws std::logic_error here             */
+#define FPF_ERR_HIP         -3   /* HIP runtime failure                                    */
+#define FPF_ERR_NOMEM       -4
+#define FPF_ERR_UNSUPPORTED -5   /* requested kernel cannot run this feeder               */
+
+/* per-scenario status */
+#define FPF_CONVERGED        0
+#define FPF_NONCONVERGED     1   /* no errmx < eps within mxitr sweeps; the reference     */
+                                 /* throws (DPF_return7.cpp:100-101,242); we return the   */
+                                 /* state after the last sweep                            */
+
+/* kernel selection */
+#define FPF_KERNEL_AUTO      0   /* tiled if the feeder is well formed, else generic      */
+#define FPF_KERNEL_GENERIC   1   /* one lane per scenario, state streamed through HBM     */
+#define FPF_KERNEL_TILED     2   /* one workgroup per scenario tile, state in LDS         */
+
+typedef struct fpf_ctx fpf_ctx;
+typedef struct fpf_feeder fpf_feeder;
+
+typedef struct fpf_opts {
+    double bkva;       /* 1000         DPF_return7.cpp:11  */
+    double bkv;        /* 12.47        :12                 */
+    double vo_kv;      /* 12.47*1.015  :13                 */
+    double eps;        /* 0.0001       :14                 */
+    int    mxitr;      /* 20           :15                 */
+    int    kernel;     /* FPF_KERNEL_*                     */
+    double lb_v;       /* 0.96  load_system_data.cpp:23 (hosting counters) */
+    double ub_v;       /* 1.05  load_system_data.cpp:24                    */
+    int    tile;       /* scenarios per workgroup for the tiled kernel, 0 = auto */
+    int    reserved[7];
+} fpf_opts;
+
+typedef struct fpf_feeder_info {
+    int nl;            /* rows of Dl                                  */
+    int ncols;
+    int nn;            /* cnt_nodes (DPF_return7.cpp:37)              */
+    int nb;            /* rows with ln != 0                           */
+    int n_codes;       /* line codes = max(z_rows/3, 1)               */
+    int n_sep;         /* separator rows (ln == 0)                    */
+    int n_taps;        /* distinct separator targets                  */
+    int well_formed;   /* 1 if the tiled kernel can run it            */
+    int lnum[3];       /* Lnum_a/b/c (form_Yabc.cpp:46-58)            */
+    int depth;         /* longest root-to-leaf chain                  */
+    int kernel;        /* kernel AUTO resolves to                     */
+    int tile;          /* scenarios per workgroup (tiled)             */
+    int reserved[4];
+} fpf_feeder_info;
+
+/* Per-scenario outputs; every pointer may be NULL (= not produced). */
+typedef struct fpf_outputs {
+    double      *vpolar;   /* [6][Nn][B]  |Va| angA |Vb| angB |Vc| angC (deg)  */
+    double      *pqb;      /* [6][Nn][B]  branch P/Q (kW, kVAr)                */
+    double      *pql;      /* [6][Nn][B]  load P/Q                             */
+    double      *v_re;     /* [3][Nn][B]  complex node voltage (p.u.)          */
+    double      *v_im;     /* [3][Nn][B]                                       */
+    int         *iters;    /* [B] sweeps executed                              */
+    signed char *status;   /* [B] FPF_CONVERGED / FPF_NONCONVERGED             */
+    double      *loss;     /* [B] kW   (VoltVarCtrl.cpp:1152-1161)             */
+    double      *vmin;     /* [B] p.u. (VoltVarCtrl.cpp:1201-1207)             */
+    double      *vmax;     /* [B] p.u.                                         */
+} fpf_outputs;
+
+/* Batch aggregate (the hosting-study reduction).  Also the payload of the
+ * cross-GPU all-reduce: fields 0 (sum) and 3..7 (sum), 1 (min), 2 (max). */
+typedef struct fpf_aggregate {
+    double loss_sum;   /* over converged scenarios                     */
+    double vmin;       /* min over converged scenarios                 */
+    double vmax;       /* max over converged scenarios                 */
+    double n_conv;
+    double n_nonconv;
+    double n_over;     /* converged with vmax > ub_v                   */
+    double n_under;    /* converged with vmin < lb_v                   */
+    double n_scen;
+} fpf_aggregate;
+
+int         fpf_abi_version(void);
+void        fpf_opts_default(fpf_opts *opts);
+
+int         fpf_ctx_create(int device, fpf_ctx **out);
+void        fpf_ctx_destroy(fpf_ctx *ctx);
+const char *fpf_last_error(const fpf_ctx *ctx);
+
+/* Validate and upload a feeder (topology tables, Z/Zb, V0 live on the device). */
+int         fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int ncols,
+                              const double *z, int z_rows, int z_cols,
+                              const fpf_opts *opts, fpf_feeder **out);
+void        fpf_feeder_destroy(fpf_feeder *feeder);
+int         fpf_feeder_get_info(const fpf_feeder *feeder, fpf_feeder_info *info);
+/* Pre-size device scratch for batches up to max_scen (no allocation later). */
+int         fpf_feeder_reserve(fpf_feeder *feeder, int max_scen);
+
+/* Host-memory batch: copies in, solves, copies out; blocks.  agg may be NULL. */
+int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
+                            const fpf_outputs *out, fpf_aggregate *agg);
+
+/* Device-memory batch: every pointer (pq, out fields, d_agg) is device memory;
+ * enqueued on `stream` (a hipStream_t; NULL = the ctx's stream) and returns
+ * without synchronising.  d_agg (8 doubles, fpf_aggregate layout) may be NULL.
+ * Returns FPF_OK or an error (the non-converged count is in d_agg / status). */
+int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
+                                   const fpf_outputs *d_out, double *d_agg, void *stream);
+
+/* Device-memory batch aggregate over per-scenario results (deterministic
+ * reduction); same layout as fpf_aggregate.  Lets a caller aggregate several
+ * batches, or time the solve kernel alone. */
+int         fpf_aggregate_device(fpf_feeder *feeder, int n_scen, const signed char *d_status,
+                                 const double *d_loss, const double *d_vmin, const double *d_vmax,
+                                 double *d_agg, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FREEDM_PF_H */

@@ -1,0 +1,560 @@
+/*
+ * ref_dpf.c -- TEST INFRASTRUCTURE ONLY: the CPU parity oracle and CPU baseline.
+ * Never linked into, loaded by, or called from the product path (freedm_amd/).
+ *
+ * Scalar C99 restatement of Broker/src/vvc/DPF_return7.cpp:8-263 (DPF_return7)
+ * and of the VVC reductions on its result (VoltVarCtrl.cpp:1152-1161,1201-1207;
+ * V_abc_list.cpp:7-81; form_Yabc.cpp:8-58).  "Parity unpinned": see ref_dpf.h.
+ *
+ * Operation-order contract.  Build with
+ * -ffp-contract=off: the reference is C++98 (ISO mode => no FMA contraction).
+ *   * complex x complex : GCC inline expansion  (ac-bd, ad+bc)
+ *   * complex / complex : libgcc __divdc3 (Smith's method), which GCC emits for
+ *                         std::complex<double> division; also used for the
+ *                         Armadillo "cx_mat / double" forms (DPF_return7.cpp:50,71),
+ *                         whose scalar is promoted to cx_double(k, 0)
+ *   * 1x3 * 3x3 complex : Armadillo glue_times sends a complex row-vector product
+ *                         with a folded scalar (lng) to gemm -> BLAS zgemm; we use
+ *                         the reference-BLAS ZGEMM loop order:
+ *                         TEMP = ALPHA*B(L,J); C(I,J) = C(I,J) + TEMP*A(I,L)
+ *                         (the BLAS the reference links is unpinned, A9)
+ *   * |z|               : std::abs -> hypot
+ *   * sum()/accu()      : Armadillo arrayops::accumulate (two interleaved accumulators)
+ */
+#include "ref_dpf.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { double re, im; } cx;
+
+static inline cx mk(double r, double i) { cx z; z.re = r; z.im = i; return z; }
+static inline cx cadd(cx a, cx b) { return mk(a.re + b.re, a.im + b.im); }
+static inline cx csub(cx a, cx b) { return mk(a.re - b.re, a.im - b.im); }
+static inline cx cmul(cx x, cx y) { return mk(x.re * y.re - x.im * y.im, x.re * y.im + x.im * y.re); }
+static inline cx cconj(cx a) { return mk(a.re, -a.im); }
+
+/* libgcc2.c __divdc3, Smith's method (finite operands) */
+static cx cdiv(cx x, cx y)
+{
+    double a = x.re, b = x.im, c = y.re, d = y.im, ratio, denom;
+    cx r;
+    if (fabs(c) < fabs(d)) {
+        ratio = c / d;
+        denom = (c * ratio) + d;
+        r.re = ((a * ratio) + b) / denom;
+        r.im = ((b * ratio) - a) / denom;
+    } else {
+        ratio = d / c;
+        denom = (d * ratio) + c;
+        r.re = ((b * ratio) + a) / denom;
+        r.im = (b - (a * ratio)) / denom;
+    }
+    return r;
+}
+
+/* Armadillo accumulate(): acc1 takes even positions, acc2 odd ones */
+static double arma_accu(const double *x, int n, int stride)
+{
+    double acc1 = 0.0, acc2 = 0.0;
+    int j;
+    for (j = 1; j < n; j += 2) {
+        acc1 += x[(j - 1) * stride];
+        acc2 += x[j * stride];
+    }
+    if ((j - 1) < n) acc1 += x[(j - 1) * stride];
+    return acc1 + acc2;
+}
+
+#define DL(i, j) dl[(size_t)(i) + (size_t)(j) * (size_t)nl]
+
+void ref_opts_default(ref_opts *o)
+{
+    o->bkva = 1000;          /* DPF_return7.cpp:11 */
+    o->bkv = 12.47;          /* :12 */
+    o->vo_kv = 12.47 * 1.015; /* :13 */
+    o->eps = 0.0001;         /* :14 */
+    o->mxitr = 20;           /* :15 */
+}
+
+int ref_count_nodes(const double *dl, int nl, int ncols)
+{
+    int i, cnt = 0;
+    if (!dl || nl < 1 || ncols < 12) return REF_BAD_INPUT;
+    for (i = 0; i < nl; ++i) {
+        double ln = DL(i, 0);
+        if (!(fabs(ln) < 2147483647.0)) return REF_BAD_INPUT; /* (int) of NaN/huge is UB */
+        if ((int)ln != 0) cnt++;
+    }
+    return cnt + 1; /* :37 */
+}
+
+/* int(x) conversion, valid when finite and inside int range */
+static int to_int(double x, int *ok)
+{
+    if (!(fabs(x) < 2147483647.0)) { *ok = 0; return 0; }
+    return (int)x;
+}
+/* implicit double -> uword conversion used as an Armadillo index (< bound) */
+static int to_uword(double x, int bound, int *ok)
+{
+    if (!(x > -1.0) || !(x < (double)bound)) { *ok = 0; return 0; }
+    return (int)x;
+}
+static void want(int cond, int *ok) { if (!cond) *ok = 0; }
+
+int ref_check(const double *dl, int nl, int ncols, int z_rows, int z_cols)
+{
+    int ok = 1, i, m, nn, ncode;
+    nn = ref_count_nodes(dl, nl, ncols);
+    if (nn < 0) return REF_BAD_INPUT;
+    if (z_cols < 3 && z_rows >= 3) return REF_BAD_INPUT;   /* Z(span, span(0,2)) :59 */
+    ncode = z_rows / 3 > 0 ? z_rows / 3 : 1;               /* Zl starts as zeros(3,3) :68 */
+    /* load currents :107-130 */
+    for (i = 0; i < nl; ++i) {
+        if (DL(i, 0) > 0) {
+            int ndr = to_int(DL(i, 2), &ok);
+            want(ndr >= 0 && ndr < nl, &ok);            /* V(ndr) */
+            want(ndr - 1 >= 0 && ndr - 1 < nn, &ok);    /* IL(ndr-1, a) */
+        }
+    }
+    /* backward sweep :136-160 */
+    want(nn - 1 >= 1, &ok);
+    for (m = nl - 1; m >= 0; --m) {
+        if (DL(m, 0) == 0) {
+            int node;
+            want(m + 1 < nl, &ok);                        /* sbus(m + 1, 0) */
+            if (m + 1 >= nl) break;
+            node = to_int(DL(m + 1, 1), &ok);
+            want(node - 1 >= 0 && node - 1 < nn - 1, &ok);
+        } else {
+            int ndr = to_int(DL(m, 2), &ok);
+            want(ndr - 1 >= 0 && ndr - 1 < nn - 1, &ok);
+        }
+    }
+    /* forward sweep :163-195 */
+    {
+        int lcd1 = to_int(DL(0, 3), &ok);
+        want(lcd1 >= 1 && lcd1 <= ncode, &ok);
+        want(nl >= 2, &ok);                               /* V(1, 0) */
+    }
+    for (m = 1; m < nl; ++m) {
+        if (DL(m, 0) != 0) {
+            int lcd = to_int(DL(m, 3), &ok);
+            want(lcd >= 1 && lcd <= ncode, &ok);
+            (void)to_uword(DL(m, 1), nl, &ok);            /* V(sbus(m), 0) */
+            (void)to_uword(DL(m, 2) - 1, nn - 1, &ok);    /* Ib.row(rbus(m) - 1) */
+            (void)to_uword(DL(m, 2), nl, &ok);            /* V(rbus(m), 0) */
+        }
+    }
+    want(nl >= nn, &ok);                                  /* V(j + 1, 0), j < nn-1 :226-229 */
+    for (i = 0; i < nl; ++i) want(isfinite(DL(i, 4)) || DL(i, 0) == 0, &ok);
+    return ok ? 0 : REF_BAD_INPUT;
+}
+
+/* drop = lng * (Ib(1x3) * Zt(3x3)) in reference-BLAS ZGEMM order */
+static void row_times(double lng, const cx ib[3], const cx zt[9] /* zt[r*3+c] = Z(r,c) */, cx out[3])
+{
+    cx alpha = mk(lng, 0.0); /* partial_unwrap folds lng: alpha = cx(lng,0)*cx(1,0) */
+    int a, l;
+    alpha = cmul(alpha, mk(1.0, 0.0));
+    for (a = 0; a < 3; ++a) {
+        cx c = mk(0.0, 0.0);
+        for (l = 0; l < 3; ++l) {
+            cx temp = cmul(alpha, zt[l * 3 + a]);
+            c = cadd(c, cmul(temp, ib[l]));
+        }
+        out[a] = c;
+    }
+}
+
+typedef struct ws_t {
+    int nl, nn, ncode;
+    cx *zl;   /* ncode x 9 */
+    cx *sld;  /* nl x 3 */
+    cx *v;    /* nl x 3 */
+    cx *il;   /* nn x 3 */
+    cx *ib;   /* (nn-1) x 3 */
+} ws_t;
+
+static int ws_alloc(ws_t *w, int nl, int nn, int ncode)
+{
+    w->nl = nl; w->nn = nn; w->ncode = ncode;
+    w->zl = (cx *)calloc((size_t)ncode * 9, sizeof(cx));
+    w->sld = (cx *)calloc((size_t)nl * 3, sizeof(cx));
+    w->v = (cx *)calloc((size_t)nl * 3, sizeof(cx));
+    w->il = (cx *)calloc((size_t)nn * 3, sizeof(cx));
+    w->ib = (cx *)calloc((size_t)(nn - 1) * 3, sizeof(cx));
+    return (w->zl && w->sld && w->v && w->il && w->ib) ? 0 : -1;
+}
+static void ws_free(ws_t *w)
+{
+    free(w->zl); free(w->sld); free(w->v); free(w->il); free(w->ib);
+}
+
+static int solve_ws(const double *dl, int nl, const double *z, int z_rows,
+                    const ref_opts *o, ws_t *w, ref_out *out)
+{
+    const double bkva = o->bkva, bkv = o->bkv, eps = o->eps;
+    const int mxitr = o->mxitr, nn = w->nn;
+    double vo = o->vo_kv, Zb, s3;
+    cx V0[3], Ibo[3], Ibl[3];
+    int rz = z_rows / 3, i, j, m, a, iters = 0, status = REF_NONCONVERGED;
+    double errmx = 0.0;
+
+    /* Sld = (P + jQ) / (bkva/3)  :46-50 */
+    for (j = 0; j < nl; ++j)
+        for (a = 0; a < 3; ++a)
+            w->sld[j * 3 + a] = cdiv(mk(DL(j, 6 + 2 * a), DL(j, 7 + 2 * a)), mk(bkva / 3, 0.0));
+    /* Zl = [Z1/Zb | Z2/Zb | ...]  :54-80 */
+    Zb = 1000 * pow(bkv, 2) / bkva;
+    for (i = 0; i < rz; ++i) {
+        int r, c;
+        for (r = 0; r < 3; ++r)
+            for (c = 0; c < 3; ++c) {
+                size_t zi = (size_t)(3 * i + r) + (size_t)c * (size_t)z_rows;
+                w->zl[i * 9 + r * 3 + c] = cdiv(mk(z[2 * zi], z[2 * zi + 1]), mk(Zb, 0.0));
+            }
+    }
+    /* V0  :84-89 */
+    vo = vo / bkv;
+    V0[0] = mk(vo, 0);
+    V0[1] = mk((-0.5) * vo, (-0.5 * sqrt(3)) * vo);
+    V0[2] = mk((-0.5) * vo, (0.5 * sqrt(3)) * vo);
+    for (j = 0; j < nl; ++j)
+        for (a = 0; a < 3; ++a) w->v[j * 3 + a] = V0[a];   /* :92-96 */
+    for (a = 0; a < 3; ++a) Ibo[a] = mk(0.0, 0.0);
+
+    for (i = 0; i < mxitr; ++i) {
+        /* load currents  :106-130 */
+        memset(w->il, 0, sizeof(cx) * (size_t)nn * 3);
+        for (j = 0; j < nl; ++j) {
+            if (DL(j, 0) > 0) {
+                int ndr = (int)DL(j, 2);
+                for (a = 0; a < 3; ++a) {
+                    cx vt = w->v[ndr * 3 + a];
+                    if (vt.re == 0 && vt.im == 0)      /* abs(v) == 0 */
+                        w->il[(ndr - 1) * 3 + a] = mk(0.0, 0.0);
+                    else
+                        w->il[(ndr - 1) * 3 + a] = cconj(cdiv(w->sld[j * 3 + a], vt));
+                }
+            }
+        }
+        /* backward sweep  :134-160 */
+        memset(w->ib, 0, sizeof(cx) * (size_t)(nn - 1) * 3);
+        for (a = 0; a < 3; ++a) Ibl[a] = mk(0.0, 0.0);
+        for (m = nl - 1; m >= 0; --m) {
+            if (DL(m, 0) == 0) {
+                int node = (int)DL(m + 1, 1);
+                for (a = 0; a < 3; ++a)
+                    w->ib[(node - 1) * 3 + a] = cadd(w->ib[(node - 1) * 3 + a], Ibl[a]);
+                for (a = 0; a < 3; ++a) Ibl[a] = mk(0.0, 0.0);
+            } else {
+                int ndr = (int)DL(m, 2);
+                for (a = 0; a < 3; ++a)
+                    w->ib[(ndr - 1) * 3 + a] =
+                        cadd(cadd(w->ib[(ndr - 1) * 3 + a], Ibl[a]), w->il[(ndr - 1) * 3 + a]);
+                for (a = 0; a < 3; ++a) Ibl[a] = w->ib[(ndr - 1) * 3 + a];
+            }
+        }
+        /* forward sweep  :163-195 */
+        {
+            cx d[3];
+            int lcd1 = (int)DL(0, 3);
+            row_times(DL(0, 4), &w->ib[0], &w->zl[(lcd1 - 1) * 9], d);
+            for (a = 0; a < 3; ++a) w->v[1 * 3 + a] = csub(V0[a], d[a]);
+        }
+        for (m = 1; m < nl; ++m) {
+            if (DL(m, 0) != 0) {
+                int lcd = (int)DL(m, 3);
+                const cx *zt = &w->zl[(lcd - 1) * 9];
+                int src = (int)DL(m, 1), ibr = (int)(DL(m, 2) - 1), dst = (int)DL(m, 2);
+                cx sv[3], d[3], rv[3];
+                for (a = 0; a < 3; ++a) sv[a] = w->v[src * 3 + a];
+                row_times(DL(m, 4), &w->ib[ibr * 3], zt, d);
+                for (a = 0; a < 3; ++a) rv[a] = csub(sv[a], d[a]);
+                for (a = 0; a < 3; ++a)
+                    if (zt[a * 3 + a].re == 0 && zt[a * 3 + a].im == 0) rv[a] = mk(0.0, 0.0);
+                for (a = 0; a < 3; ++a) w->v[dst * 3 + a] = rv[a];
+            }
+        }
+        /* convergence  :199-210 */
+        errmx = -INFINITY;
+        {
+            double df[3];
+            for (a = 0; a < 3; ++a) {
+                cx dd = csub(w->ib[a], Ibo[a]);
+                df[a] = hypot(dd.re, dd.im);
+            }
+            /* Armadillo max(): first element, then strict '>' updates */
+            errmx = df[0];
+            for (a = 1; a < 3; ++a) if (df[a] > errmx) errmx = df[a];
+        }
+        for (a = 0; a < 3; ++a) Ibo[a] = w->ib[a];
+        iters = i + 1;
+        if (errmx < eps) { status = REF_CONVERGED; break; }
+    }
+
+    /* post-processing  :222-253 ; slot k of the outputs is V(k) (substation first) */
+    s3 = bkva / 3;
+    for (j = 0; j < nn; ++j) {
+        for (a = 0; a < 3; ++a) {
+            cx vv = w->v[j * 3 + a];
+            cx ibv = (j == 0) ? w->ib[0 * 3 + a] : w->ib[(j - 1) * 3 + a];
+            cx ilv = (j == 0) ? w->il[(nn - 1) * 3 + a] : w->il[(j - 1) * 3 + a];
+            cx sv = cmul(vv, mk(s3, 0.0));
+            if (out->vpolar) {
+                double mag = hypot(vv.re, vv.im);
+                double ang = (180 / M_PI) * atan(vv.im / vv.re);
+                if (!isfinite(ang)) ang = 0;
+                if (a == 1) ang = ang - 180;
+                if (a == 2) ang = ang + 180;
+                out->vpolar[j + (size_t)(2 * a) * nn] = mag;
+                out->vpolar[j + (size_t)(2 * a + 1) * nn] = ang;
+            }
+            if (out->pqb) {
+                cx sb = cmul(sv, cconj(ibv));
+                out->pqb[j + (size_t)(2 * a) * nn] = sb.re;
+                out->pqb[j + (size_t)(2 * a + 1) * nn] = sb.im;
+            }
+            if (out->pql) {
+                cx sl = cmul(sv, cconj(ilv));
+                out->pql[j + (size_t)(2 * a) * nn] = sl.re;
+                out->pql[j + (size_t)(2 * a + 1) * nn] = sl.im;
+            }
+            if (out->v) {
+                out->v[2 * (j + (size_t)a * nn)] = vv.re;
+                out->v[2 * (j + (size_t)a * nn) + 1] = vv.im;
+            }
+        }
+    }
+    if (out->ib)
+        for (j = 0; j < nn - 1; ++j)
+            for (a = 0; a < 3; ++a) {
+                out->ib[2 * (j + (size_t)a * (nn - 1))] = w->ib[j * 3 + a].re;
+                out->ib[2 * (j + (size_t)a * (nn - 1)) + 1] = w->ib[j * 3 + a].im;
+            }
+    if (out->il)
+        for (j = 0; j < nn; ++j)
+            for (a = 0; a < 3; ++a) {
+                out->il[2 * (j + (size_t)a * nn)] = w->il[j * 3 + a].re;
+                out->il[2 * (j + (size_t)a * nn) + 1] = w->il[j * 3 + a].im;
+            }
+    out->iters = iters;
+    out->status = status;
+    out->errmx = errmx;
+    return status;
+}
+
+int ref_dpf_solve(const double *dl, int nl, int ncols,
+                  const double *z, int z_rows, int z_cols,
+                  const ref_opts *o, ref_out *out)
+{
+    ws_t w;
+    int nn, rc;
+    ref_opts od;
+    if (!o) { ref_opts_default(&od); o = &od; }
+    rc = ref_check(dl, nl, ncols, z_rows, z_cols);
+    if (rc) { out->status = rc; out->iters = 0; return rc; }
+    nn = ref_count_nodes(dl, nl, ncols);
+    if (ws_alloc(&w, nl, nn, z_rows / 3 > 0 ? z_rows / 3 : 1)) { ws_free(&w); out->status = REF_BAD_INPUT; return REF_BAD_INPUT; }
+    rc = solve_ws(dl, nl, z, z_rows, o, &w, out);
+    ws_free(&w);
+    return rc;
+}
+
+int ref_lnum(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+             double bkva, double bkv, int lnum[3])
+{
+    /* form_Yabc.cpp:11-58 */
+    double Zb = pow(bkv, 2) / bkva * 1000;
+    int i, j = 0, lbr = 0, p;
+    cx *brn;
+    (void)z_cols;
+    if (ncols < 12) return REF_BAD_INPUT;
+    for (i = 0; i < nl; ++i) if (DL(i, 0) > 0) lbr++;
+    brn = (cx *)calloc((size_t)(lbr > 0 ? lbr : 1) * 3, sizeof(cx));
+    for (i = 0; i < nl && j < lbr; ++i) {
+        int code = (int)DL(i, 3);
+        int idx = 3 * (code - 1);
+        if ((int)DL(i, 0) != 0) {
+            if (idx < 0 || idx + 2 >= z_rows) { free(brn); return REF_BAD_INPUT; }
+            for (p = 0; p < 3; ++p) {
+                size_t zi = (size_t)(idx + p) + (size_t)p * (size_t)z_rows;
+                cx zz = mk(z[2 * zi], z[2 * zi + 1]);
+                if (code == 7) {
+                    brn[j * 3 + p] = zz;
+                } else {
+                    double lng = DL(i, 4);
+                    cx t = mk(zz.re * lng, zz.im * lng);          /* double * complex */
+                    brn[j * 3 + p] = mk(t.re / Zb, t.im / Zb);     /* complex / double */
+                }
+            }
+            ++j;
+        }
+    }
+    for (p = 0; p < 3; ++p) {
+        int c = 0;
+        for (i = 0; i < lbr; ++i)
+            if (hypot(brn[i * 3 + p].re, brn[i * 3 + p].im) > 0) c++;
+        lnum[p] = c;
+    }
+    free(brn);
+    return 0;
+}
+
+void ref_vvc_reduce(const double *vpolar, const double *pqb, const double *pql, int nn,
+                    const int lnum[3], double *loss, double *vmin, double *vmax)
+{
+    double x[3], pmin[3], pmax[3];
+    int p;
+    /* loss :1152-1161 */
+    for (p = 0; p < 3; ++p) {
+        double pl = arma_accu(pql + (size_t)(2 * p) * nn, nn, 1);
+        x[p] = pqb[(size_t)(2 * p) * nn] - pl;
+    }
+    if (loss) *loss = arma_accu(x, 3, 1);
+    /* V_abc_list.cpp:7-81, then min/max :1201-1207 */
+    for (p = 0; p < 3; ++p) {
+        int K = lnum[p] + 1, jj = 0, i;
+        double mn = 0, mx = 0;
+        double *vals = (double *)calloc((size_t)K, sizeof(double));
+        for (i = 0; i < nn && jj < K; ++i) {
+            double vv = vpolar[i + (size_t)(2 * p) * nn];
+            if (vv != 0) vals[jj++] = vv;
+        }
+        mn = vals[0]; mx = vals[0];
+        for (i = 1; i < K; ++i) {
+            if (vals[i] < mn) mn = vals[i];
+            if (vals[i] > mx) mx = vals[i];
+        }
+        pmin[p] = mn; pmax[p] = mx;
+        free(vals);
+    }
+    if (vmin) {
+        double mn = pmin[0];
+        for (p = 1; p < 3; ++p) if (pmin[p] < mn) mn = pmin[p];
+        *vmin = mn;
+    }
+    if (vmax) {
+        double mx = pmax[0];
+        for (p = 1; p < 3; ++p) if (pmax[p] > mx) mx = pmax[p];
+        *vmax = mx;
+    }
+}
+
+/* ------------------------------------------------------------------ batch */
+
+typedef struct batch_job {
+    const double *dl; int nl, ncols;
+    const double *z; int z_rows, z_cols;
+    const ref_opts *o;
+    int n_scen, s0, s1, nn;
+    const int *lnum;
+    const double *pq;
+    double *vpolar, *pqb, *pql, *v_re, *v_im, *loss, *vmin, *vmax;
+    int *iters; signed char *status;
+    int n_nonconv, rc;
+} batch_job;
+
+static void *batch_worker(void *arg)
+{
+    batch_job *jb = (batch_job *)arg;
+    const int nl = jb->nl, nn = jb->nn, B = jb->n_scen;
+    double *dl = (double *)malloc(sizeof(double) * (size_t)nl * (size_t)jb->ncols);
+    double *vp = (double *)malloc(sizeof(double) * (size_t)nn * 6);
+    double *pb = (double *)malloc(sizeof(double) * (size_t)nn * 6);
+    double *pl = (double *)malloc(sizeof(double) * (size_t)nn * 6);
+    double *vv = (double *)malloc(sizeof(double) * (size_t)nn * 6);
+    ws_t w;
+    int s, r, c;
+    jb->n_nonconv = 0;
+    jb->rc = 0;
+    if (!dl || !vp || !pb || !pl || !vv ||
+        ws_alloc(&w, nl, nn, jb->z_rows / 3 > 0 ? jb->z_rows / 3 : 1)) {
+        jb->rc = REF_BAD_INPUT;
+        free(dl); free(vp); free(pb); free(pl); free(vv);
+        return NULL;
+    }
+    memcpy(dl, jb->dl, sizeof(double) * (size_t)nl * (size_t)jb->ncols);
+    for (s = jb->s0; s < jb->s1; ++s) {
+        ref_out out;
+        for (c = 0; c < 6; ++c)
+            for (r = 0; r < nl; ++r)
+                dl[r + (size_t)(6 + c) * nl] = jb->pq[((size_t)c * nl + r) * B + s];
+        memset(&out, 0, sizeof(out));
+        out.vpolar = vp; out.pqb = pb; out.pql = pl; out.v = vv;
+        solve_ws(dl, nl, jb->z, jb->z_rows, jb->o, &w, &out);
+        if (out.status != REF_CONVERGED) jb->n_nonconv++;
+        if (jb->iters) jb->iters[s] = out.iters;
+        if (jb->status) jb->status[s] = (signed char)out.status;
+        if (jb->loss || jb->vmin || jb->vmax) {
+            double l, mn, mx;
+            ref_vvc_reduce(vp, pb, pl, nn, jb->lnum, &l, &mn, &mx);
+            if (jb->loss) jb->loss[s] = l;
+            if (jb->vmin) jb->vmin[s] = mn;
+            if (jb->vmax) jb->vmax[s] = mx;
+        }
+        for (c = 0; c < 6; ++c)
+            for (r = 0; r < nn; ++r) {
+                size_t o = ((size_t)c * nn + r) * B + s;
+                if (jb->vpolar) jb->vpolar[o] = vp[r + (size_t)c * nn];
+                if (jb->pqb) jb->pqb[o] = pb[r + (size_t)c * nn];
+                if (jb->pql) jb->pql[o] = pl[r + (size_t)c * nn];
+            }
+        for (c = 0; c < 3; ++c)
+            for (r = 0; r < nn; ++r) {
+                size_t o = ((size_t)c * nn + r) * B + s;
+                if (jb->v_re) jb->v_re[o] = vv[2 * (r + (size_t)c * nn)];
+                if (jb->v_im) jb->v_im[o] = vv[2 * (r + (size_t)c * nn) + 1];
+            }
+    }
+    ws_free(&w);
+    free(dl); free(vp); free(pb); free(pl); free(vv);
+    return NULL;
+}
+
+int ref_dpf_batch(const double *dl, int nl, int ncols,
+                  const double *z, int z_rows, int z_cols,
+                  const ref_opts *o, int n_scen, const double *pq,
+                  double *vpolar, double *pqb, double *pql,
+                  double *v_re, double *v_im,
+                  int *iters, signed char *status,
+                  double *loss, double *vmin, double *vmax,
+                  int nthreads)
+{
+    int rc, nn, t, lnum[3], total = 0;
+    ref_opts od;
+    batch_job *jobs;
+    pthread_t *th;
+    if (!o) { ref_opts_default(&od); o = &od; }
+    rc = ref_check(dl, nl, ncols, z_rows, z_cols);
+    if (rc) return rc;
+    if (ref_lnum(dl, nl, ncols, z, z_rows, z_cols, o->bkva, o->bkv, lnum)) return REF_BAD_INPUT;
+    nn = ref_count_nodes(dl, nl, ncols);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > n_scen) nthreads = n_scen > 0 ? n_scen : 1;
+    jobs = (batch_job *)calloc((size_t)nthreads, sizeof(batch_job));
+    th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (t = 0; t < nthreads; ++t) {
+        batch_job *jb = &jobs[t];
+        jb->dl = dl; jb->nl = nl; jb->ncols = ncols; jb->z = z; jb->z_rows = z_rows; jb->z_cols = z_cols;
+        jb->o = o; jb->n_scen = n_scen; jb->nn = nn; jb->lnum = lnum; jb->pq = pq;
+        jb->s0 = (int)((long long)n_scen * t / nthreads);
+        jb->s1 = (int)((long long)n_scen * (t + 1) / nthreads);
+        jb->vpolar = vpolar; jb->pqb = pqb; jb->pql = pql; jb->v_re = v_re; jb->v_im = v_im;
+        jb->iters = iters; jb->status = status; jb->loss = loss; jb->vmin = vmin; jb->vmax = vmax;
+        if (nthreads == 1) batch_worker(jb);
+        else pthread_create(&th[t], NULL, batch_worker, jb);
+    }
+    rc = 0;
+    for (t = 0; t < nthreads; ++t) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+        total += jobs[t].n_nonconv;
+    }
+    free(jobs); free(th);
+    return rc ? rc : total;
+}

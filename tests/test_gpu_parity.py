@@ -1,0 +1,203 @@
+"""GPU parity tests: libfreedm_pf (gfx950 kernels, through the C ABI) against the
+oracle on the same inputs.
+
+Bar (north_star): bus voltages within 1e-10 relative of the reference path and
+identical iteration counts.  The kernels perform the reference's operations in
+the reference's order with FMA contraction off, so the stronger checks below
+also hold: complex V, PQb, PQL and loss are bit-identical to the oracle; only
+results that pass through hypot/atan (Vpolar, Vmin/Vmax) may differ by a few
+ulp (ocml vs glibc) -- tolerance 1e-14 relative (angles 1e-12 degrees).
+"""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, load_golden
+from freedm_amd import feeder as F
+
+pytestmark = pytest.mark.gpu
+
+WF = {"g1_demo", "g1_demo_batch", "g2_dlnew", "g3_123bus", "g4_2048bus", "g5_nonconv", "g6_missing_phase"}
+
+
+def _pf(Dl, Z, **kw):
+    from freedm_amd import PowerFlow
+    return PowerFlow(F.Feeder(Dl, Z), **kw)
+
+
+def _vrel(a_re, a_im, b_re, b_im):
+    a = a_re + 1j * a_im
+    b = b_re + 1j * b_im
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))
+
+
+@pytest.mark.parametrize("kernel", ["generic", "tiled"])
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_matches_golden(name, kernel):
+    g = load_golden(name)
+    pf = _pf(g["Dl"], g["Z"], kernel=kernel)
+    assert pf.kernel == kernel
+    r = pf.solve(g["pq"])
+    # the north-star bar
+    assert (r["iters"] == g["iters"]).all()
+    assert (r["status"] == g["status"]).all()
+    assert _vrel(r["V_re"], r["V_im"], g["V_re"], g["V_im"]) <= 1e-10
+    # the stronger claim: same operations, same order -> same bits
+    np.testing.assert_array_equal(r["V_re"], g["V_re"])
+    np.testing.assert_array_equal(r["V_im"], g["V_im"])
+    np.testing.assert_array_equal(r["PQb"][:, :, :4], g["PQb"])
+    np.testing.assert_array_equal(r["PQL"][:, :, :4], g["PQL"])
+    np.testing.assert_array_equal(r["loss"], g["loss"])
+    # hypot / atan: ocml vs glibc, a few ulp
+    np.testing.assert_allclose(r["Vpolar"][0::2, :, :4], g["Vpolar"][0::2], rtol=1e-14, atol=0)
+    np.testing.assert_allclose(r["Vpolar"][1::2, :, :4], g["Vpolar"][1::2], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(r["vmin"], g["vmin"], rtol=1e-14)
+    np.testing.assert_allclose(r["vmax"], g["vmax"], rtol=1e-14)
+
+
+def test_auto_kernel_choice():
+    g = load_golden("g3_123bus")
+    assert _pf(g["Dl"], g["Z"]).kernel == "tiled"
+    f = F.demo_feeder()
+    Dl = f.Dl[[0, 6, 7, 8, 5, 1, 2, 3, 4]].copy()     # lateral before its tap's row: legal, not well formed
+    Dl[4] = 0
+    pf = _pf(Dl, f.Z)
+    assert pf.kernel == "generic" and pf.info["well_formed"] == 0
+    from freedm_amd import DPFError
+    with pytest.raises(DPFError):
+        _pf(Dl, f.Z, kernel="tiled")
+
+
+def test_malformed_order_matches_oracle():
+    from oracle import oracle as O
+    f = F.demo_feeder()
+    Dl = f.Dl[[0, 6, 7, 8, 5, 1, 2, 3, 4]].copy()
+    Dl[4] = 0
+    pq = F.scenario_loads(F.Feeder(Dl, f.Z), np.arange(40))
+    r = _pf(Dl, f.Z).solve(pq)
+    c = O.dpf_batch(Dl, f.Z, pq, nthreads=4)
+    assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+    np.testing.assert_array_equal(r["V_re"], c["V_re"])
+    np.testing.assert_array_equal(r["V_im"], c["V_im"])
+
+
+@pytest.mark.parametrize("tile", [1, 3, 5, 8])
+def test_tiles_and_ragged_batches(tile):
+    g = load_golden("g3_123bus")
+    ref = _pf(g["Dl"], g["Z"], kernel="generic").solve(g["pq"][:, :, :13])
+    r = _pf(g["Dl"], g["Z"], kernel="tiled", tile=tile).solve(g["pq"][:, :, :13])
+    for k in ("V_re", "V_im", "PQb", "PQL", "Vpolar", "iters", "status", "loss", "vmin", "vmax"):
+        np.testing.assert_array_equal(r[k], ref[k], err_msg=k)
+
+
+def test_empty_and_single():
+    g = load_golden("g1_demo")
+    pf = _pf(g["Dl"], g["Z"])
+    r0 = pf.solve(np.zeros((6, pf.nl, 0)))
+    assert r0["iters"].size == 0 and r0["n_nonconv"] == 0
+    r1 = pf.solve(g["pq"])
+    np.testing.assert_array_equal(r1["V_re"], g["V_re"])
+
+
+def test_dpf_return7_dropin():
+    from freedm_amd import DPF_return7, NonConvergedError
+    from oracle import oracle as O
+    f = F.demo_feeder()
+    vpq = DPF_return7(f.Dl, f.Z)
+    c = O.dpf_solve(f.Dl, f.Z)
+    assert vpq.iters == c["iters"] == 5
+    np.testing.assert_array_equal(vpq.PQb, c["PQb"])
+    np.testing.assert_array_equal(vpq.PQL, c["PQL"])
+    np.testing.assert_allclose(vpq.Vpolar, c["Vpolar"], rtol=1e-14, atol=1e-12)
+    np.testing.assert_array_equal(vpq.Qset_b[:, 0], f.Dl[:, 9])
+    g = load_golden("g5_nonconv")
+    Dl = g["Dl"].copy()
+    with pytest.raises(NonConvergedError):
+        DPF_return7(Dl, g["Z"])
+
+
+def test_bad_feeders_raise_topology_error():
+    from freedm_amd import DPFError
+    f = F.demo_feeder()
+    for Dl in (np.vstack([f.Dl, np.zeros((1, 13))]), np.delete(f.Dl, 5, axis=0)):
+        with pytest.raises(DPFError) as e:
+            _pf(Dl, f.Z)
+        assert e.value.code == -2
+
+
+def test_full_config2_properties():
+    """BASELINE config 2 at full size (123-bus, 4096 scenarios): size-independent
+    properties -- the two kernels agree bit for bit, the fused loss equals the
+    reference formula recomputed from PQb/PQL, the aggregate matches, and the
+    solve is deterministic."""
+    f = F.synthetic_feeder(123, 123)
+    pq = F.scenario_loads(f, np.arange(4096))
+    t = _pf(f.Dl, f.Z, kernel="tiled")
+    gen = _pf(f.Dl, f.Z, kernel="generic")
+    a = t.solve(pq)
+    b = gen.solve(pq)
+    a2 = t.solve(pq)
+    for k in ("V_re", "V_im", "PQb", "PQL", "iters", "status", "loss", "vmin", "vmax"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        np.testing.assert_array_equal(a[k], a2[k], err_msg=k)
+    assert (a["status"] == 0).all()
+    # loss = accu([PQb(0,2p) - sum(PQL.col(2p))]) in Armadillo's order
+    nn = t.nn
+    x = []
+    for p in range(3):
+        col = a["PQL"][2 * p]
+        acc1 = np.zeros(4096)
+        acc2 = np.zeros(4096)
+        for k in range(nn):
+            if k & 1:
+                acc2 = acc2 + col[k]
+            else:
+                acc1 = acc1 + col[k]
+        x.append(a["PQb"][2 * p, 0] - (acc1 + acc2))
+    np.testing.assert_array_equal(a["loss"], ((0.0 + x[0]) + x[2]) + (0.0 + x[1]))
+    ag = a["aggregate"]
+    conv = a["status"] == 0
+    assert ag["n_conv"] == conv.sum() and ag["n_scen"] == 4096
+    assert ag["vmin"] == a["vmin"][conv].min() and ag["vmax"] == a["vmax"][conv].max()
+    assert ag["loss_sum"] == pytest.approx(a["loss"][conv].sum(), rel=1e-12)
+    assert ag["n_under"] == (a["vmin"][conv] < 0.96).sum() and ag["n_over"] == (a["vmax"][conv] > 1.05).sum()
+    # a sample against the oracle
+    from oracle import oracle as O
+    idx = np.arange(0, 4096, 97)
+    c = O.dpf_batch(f.Dl, f.Z, pq[:, :, idx], nthreads=8)
+    np.testing.assert_array_equal(a["V_re"][:, :, idx], c["V_re"])
+    np.testing.assert_array_equal(a["iters"][idx], c["iters"])
+
+
+def test_device_api_on_torch_stream():
+    import torch
+    f = F.synthetic_feeder(123, 123)
+    pq = F.scenario_loads(f, np.arange(1000))
+    pf = _pf(f.Dl, f.Z)
+    host = pf.solve(pq)
+    dev = torch.device("cuda:0")
+    d_pq = torch.from_numpy(pq).to(dev)
+    B = pq.shape[2]
+    out = {"iters": torch.zeros(B, dtype=torch.int32, device=dev), "status": torch.zeros(B, dtype=torch.int8, device=dev),
+           "loss": torch.zeros(B, dtype=torch.float64, device=dev), "vmin": torch.zeros(B, dtype=torch.float64, device=dev),
+           "vmax": torch.zeros(B, dtype=torch.float64, device=dev),
+           "v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
+           "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
+    agg = torch.zeros(8, dtype=torch.float64, device=dev)
+    pf.solve_device(d_pq, out, agg=agg, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["v_re"].cpu().numpy(), host["V_re"])
+    np.testing.assert_array_equal(out["loss"].cpu().numpy(), host["loss"])
+    np.testing.assert_array_equal(out["iters"].cpu().numpy(), host["iters"])
+    assert agg.cpu().numpy()[3] == host["aggregate"]["n_conv"]
+
+
+def test_hosting_shards_are_invariant():
+    """Config 4 partitioning: a scenario's result does not depend on which shard
+    (GPU) solved it (seeds derive from the global scenario index)."""
+    f = F.synthetic_feeder(123, 123)
+    pf = _pf(f.Dl, f.Z)
+    full = pf.solve(F.hosting_loads(f, np.arange(512)))
+    lo = pf.solve(F.hosting_loads(f, np.arange(0, 256)))
+    hi = pf.solve(F.hosting_loads(f, np.arange(256, 512)))
+    np.testing.assert_array_equal(np.concatenate([lo["V_re"], hi["V_re"]], axis=2), full["V_re"])
+    np.testing.assert_array_equal(np.concatenate([lo["loss"], hi["loss"]]), full["loss"])
