@@ -75,7 +75,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("FPF_LIB_PATH") or LIB_PATH   # override: diagnostic builds only
     if not os.path.exists(path):
         raise RuntimeError(f"libfreedm_pf not built: {path} missing (run __graft_entry__.build() "
                            "or `make -C freedm_amd/csrc`); there is no CPU fallback")

@@ -124,6 +124,10 @@ struct HostFeeder {
     bool wf = false;
     std::string wf_why;
     std::vector<NodeOp> node;
+    struct BwIdx { int k, a, p; };            // node, tap read (-1 none), separator target (-1 none)
+    struct FwIdx { int dst, src, mask; };
+    std::vector<BwIdx> bwi;
+    std::vector<FwIdx> fwi;
     std::vector<SeqBw> seq_bw;
     std::vector<SeqFw> seq_fw;
     int n_taps = 0, depth = 0;
@@ -310,21 +314,20 @@ void analyse_tiled(HostFeeder &h) {
             if (tap_of[t] < 0) tap_of[t] = h.n_taps++;
             h.node[t].tap = tap_of[t];
         }
-    if (h.n_taps > 32767) return no("too many taps");
-    h.seq_bw.clear();
-    h.seq_fw.clear();
+    if (h.n_taps > 32766) return no("too many taps");
+    // sequential programs in index form: a separator row folds into the branch
+    // op processed just before it (row m+1, DPF_return7.cpp:138-146)
+    h.bwi.clear();
+    h.fwi.clear();
     for (int m = nl - 1; m >= 0; --m) {
         if (h.at(m, 0) == 0) {
-            h.seq_bw.push_back(SeqBw{0, (int16_t)(tap_of[(int)h.at(m + 1, 1)] + 1)});
+            h.bwi.back().p = tap_of[(int)h.at(m + 1, 1)];
         } else {
             const int k = (int)h.at(m, 2);
-            h.seq_bw.push_back(SeqBw{(int16_t)k, (int16_t)(tap_of[k] + 1)});
+            h.bwi.push_back({k, tap_of[k], -1});
         }
     }
-    for (const FwOp &op : h.fw) {
-        const int src = op.src < 0 ? 0 : op.src;
-        h.seq_fw.push_back(SeqFw{(int16_t)op.dst, (uint16_t)(src | (op.mask << 13))});
-    }
+    for (const FwOp &op : h.fw) h.fwi.push_back({op.dst, op.src < 0 ? 0 : op.src, op.mask});
     // depth of the node tree (longest chain) for the info record
     std::vector<int> dep(nn, 0);
     int d = 0;
@@ -334,6 +337,53 @@ void analyse_tiled(HostFeeder &h) {
     }
     h.depth = d;
     h.wf = true;
+}
+
+// Chunked sequential programs for one tile size (see fpf_internal.h).
+void build_seq_programs(HostFeeder &h, int tile) {
+    const int nn = h.nn, U = SEQ_CHUNK;
+    const uint32_t slot = 3u * (uint32_t)tile * 16u;
+    const uint32_t w_bytes = (uint32_t)(nn + 2) * slot;
+    auto W = [&](int k) { return (uint32_t)k * slot; };
+    auto T = [&](int t) { return w_bytes + (uint32_t)t * slot; };
+    const int ZW = nn, DW = nn + 1, ZT = h.n_taps, DT = h.n_taps + 1;
+    h.seq_bw.clear();
+    h.seq_fw.clear();
+    // backward: no op may read or add into a T slot an earlier op of its chunk adds into
+    std::vector<int> written;
+    auto pad_bw = [&]() {
+        while (h.seq_bw.size() % U) h.seq_bw.push_back({W(ZW), W(DW), T(ZT), T(DT)});
+        written.clear();
+    };
+    for (const auto &op : h.bwi) {
+        const bool clash = (op.a >= 0 && std::count(written.begin(), written.end(), op.a)) ||
+                           (op.p >= 0 && std::count(written.begin(), written.end(), op.p));
+        if (clash) pad_bw();
+        const uint32_t p = op.p >= 0 ? (T(op.p) | BW_SEP) : T(DT);
+        h.seq_bw.push_back({W(op.k), W(op.k), T(op.a >= 0 ? op.a : ZT), p});
+        if (op.p >= 0) written.push_back(op.p);
+        if (h.seq_bw.size() % U == 0) written.clear();
+    }
+    pad_bw();
+    // forward: V(src) comes from the previous op (register) or from LDS written
+    // before this chunk; otherwise the chunk is closed first
+    std::vector<int> wrote;
+    int prev_dst = -1;
+    auto pad_fw = [&]() {
+        while (h.seq_fw.size() % U) h.seq_fw.push_back({W(DW), W(ZW), 0u, 0u});
+        wrote.clear();
+        prev_dst = -1;
+    };
+    for (const auto &op : h.fwi) {
+        const bool prev = op.src != 0 && op.src == prev_dst;
+        if (!prev && op.src != 0 && std::count(wrote.begin(), wrote.end(), op.src)) pad_fw();
+        const bool prev2 = op.src != 0 && op.src == prev_dst;
+        h.seq_fw.push_back({W(op.dst), W(op.src), (uint32_t)op.mask | (prev2 ? FW_PREV : 0u), 0u});
+        wrote.push_back(op.dst);
+        prev_dst = op.dst;
+        if (h.seq_fw.size() % U == 0) wrote.clear();
+    }
+    pad_fw();
 }
 
 template <class T>
@@ -380,6 +430,18 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     for (int p = 0; p < 3; ++p) in.lnum[p] = h.lnum[p];
     in.depth = h.depth;
 
+    // tile of the tiled kernel (the sequential programs are built for it)
+    int tile = 0;
+    if (h.wf) {
+        FeederDev probe{};
+        probe.nn = h.nn;
+        probe.n_taps = h.n_taps;
+        probe.n_seq_bw = (int)((h.bwi.size() * 2 + SEQ_CHUNK) / SEQ_CHUNK * SEQ_CHUNK);
+        probe.n_seq_fw = (int)((h.fwi.size() * 2 + SEQ_CHUNK) / SEQ_CHUNK * SEQ_CHUNK);
+        const int tmax = tiled_max_tile(probe);
+        tile = o.tile > 0 ? std::min(o.tile, tmax) : tmax;
+        if (tile >= 1) build_seq_programs(h, tile);
+    }
     // upload all tables as one blob
     std::vector<char> blob;
     const size_t o_tz = push_blob(blob, h.tz);
@@ -428,22 +490,18 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     d.seq_fw = (const SeqFw *)(base + o_sfw);
     d.n_seq_bw = (int)h.seq_bw.size();
     d.n_seq_fw = (int)h.seq_fw.size();
+    d.tile = tile;
 
     // kernel choice
     int kern = o.kernel;
-    if (kern == FPF_KERNEL_AUTO) kern = (h.wf && tiled_max_tile(d) >= 1) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
-    if (kern == FPF_KERNEL_TILED && (!h.wf || tiled_max_tile(d) < 1)) {
+    if (kern == FPF_KERNEL_AUTO) kern = (h.wf && tile >= 1) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
+    if (kern == FPF_KERNEL_TILED && (!h.wf || tile < 1)) {
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_UNSUPPORTED,
                     "tiled kernel needs a well-formed feeder that fits in LDS: " + (h.wf ? std::string("too large") : h.wf_why));
     }
     in.kernel = kern;
-    if (kern == FPF_KERNEL_TILED) {
-        int t = o.tile > 0 ? o.tile : 0;
-        const int tmax = tiled_max_tile(d);
-        if (t == 0) t = tmax;
-        in.tile = std::min(t, tmax);
-    }
+    in.tile = kern == FPF_KERNEL_TILED ? tile : 0;
     *out = f;
     return FPF_OK;
 }
@@ -508,7 +566,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         int rc = fpf_feeder_reserve(f, n_scen);
         if (rc) return rc;
     }
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the default stream
     fpf_outputs none;
     std::memset(&none, 0, sizeof(none));
     const fpf_outputs &u = d_out ? *d_out : none;
@@ -525,7 +583,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     o.vmax = u.vmax ? u.vmax : f->d_vmax;
     hipError_t e;
     if (f->info.kernel == FPF_KERNEL_TILED) {
-        e = launch_tiled(f->dev, n_scen, d_pq, o, f->info.tile, st);
+        e = launch_tiled(f->dev, n_scen, d_pq, o, st);
     } else {
         if (!f->d_scratch || f->scratch_ld < (size_t)n_scen) {
             int rc = fpf_feeder_reserve(f, n_scen);
@@ -547,7 +605,7 @@ extern "C" int fpf_aggregate_device(fpf_feeder *f, int n_scen, const signed char
         return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "fpf_aggregate_device: bad arguments");
     fpf_ctx *ctx = f->ctx;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t st = (hipStream_t)stream;
     hipError_t e = launch_aggregate(n_scen, (const int8_t *)d_status, d_loss, d_vmin, d_vmax, f->dev.lb_v, f->dev.ub_v,
                                     d_agg, st);
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("aggregate launch: ") + hipGetErrorString(e));
@@ -601,7 +659,7 @@ extern "C" int fpf_solve_batch(fpf_feeder *f, int n_scen, const double *pq, cons
     d.loss = (double *)dptr(8);
     d.vmin = (double *)dptr(9);
     d.vmax = (double *)dptr(10);
-    int rc = fpf_solve_batch_device(f, n_scen, (const double *)dptr(0), &d, f->d_agg, ctx->stream);
+    int rc = fpf_solve_batch_device(f, n_scen, (const double *)dptr(0), &d, f->d_agg, (void *)ctx->stream);
     if (rc) return rc;
     for (int i = 1; i < 11; ++i)
         if (parts[i].host)

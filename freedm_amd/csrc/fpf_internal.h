@@ -37,14 +37,26 @@ struct NodeOp {
     int32_t tap;     // tap-accumulator slot, -1 if no separator targets k
 };
 
-// Sequential-stage program of the tiled kernel (one entry per Dl row).
-//   backward, reverse row order: node >= 1 -> branch of that node, tap1 = its
-//            tap-accumulator slot + 1 (0 = none); node == 0 -> separator adding
-//            Ibl into accumulator tap1 - 1
-//   forward, row order: V(dst) = V(src) - drop(dst), phases in `mask` zeroed;
-//            src == 0 reads the constant V0 kept in slot 0
-struct SeqBw { int16_t node, tap1; };
-struct SeqFw { int16_t dst; uint16_t src_mask; };   // src = low 13 bits, mask = top 3
+// Sequential-stage programs of the tiled kernel, built for one tile size (LDS
+// byte offsets are baked in).  LDS holds W = (nn + 2) slots x 3 phases x TILE
+// scenarios of complex fp64 -- slot nn is a permanent zero, slot nn+1 a dummy
+// sink -- then the tap accumulators T = (n_taps + 2) slots laid out the same way
+// (zero and dummy last).  A sequential lane (s, p) adds its own lane offset
+// (p*TILE + s)*16 to every offset.
+//
+// Backward program (one op per branch row, reverse row order; a separator row
+// is folded into the branch op processed just before it):
+//     x = (T[a] + Ibl) + W[r];  W[w] = x;  T[p] += x (if sep);  Ibl = sep ? 0 : x
+// Forward program (one op per branch row, row order):
+//     V = (prev ? Vprev : W[src]) - W[dst];  zero phases in mask;  W[dst] = V
+// Both run in chunks of SEQ_CHUNK ops whose LDS reads are all issued first; the
+// host pads chunks with identity ops so no op reads what an earlier op of its
+// chunk writes.
+constexpr int SEQ_CHUNK = 8;
+struct SeqBw { uint32_t r, w, a, p; };     // byte offsets; p bit 31 = separator (T[p] += x; Ibl = 0)
+struct SeqFw { uint32_t dst, src, flags, pad; };  // flags: bits 0-2 zero mask, bit 3 = src is previous op
+constexpr uint32_t BW_SEP = 0x80000000u;
+constexpr uint32_t FW_PREV = 8u;
 
 struct FeederDev {
     // sizes
@@ -64,9 +76,10 @@ struct FeederDev {
     const BwOp *bw_ops;
     const FwOp *fw_ops;
     const NodeOp *node_ops;  // [nn] (index 0 unused) -- tiled only
-    const SeqBw *seq_bw;     // tiled only
-    const SeqFw *seq_fw;     // tiled only
+    const SeqBw *seq_bw;     // tiled only (padded to SEQ_CHUNK)
+    const SeqFw *seq_fw;     // tiled only (padded to SEQ_CHUNK)
     int32_t n_seq_bw, n_seq_fw;
+    int32_t tile;            // tile the programs were built for
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -80,8 +93,7 @@ struct OutDev {
 // launchers (fpf_kernels.hip)
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st);
-hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
-                        int tile, hipStream_t st);
+hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss,
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
                             double *d_agg, hipStream_t st);

@@ -150,8 +150,8 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
                             const fpf_outputs *out, fpf_aggregate *agg);
 
 /* Device-memory batch: every pointer (pq, out fields, d_agg) is device memory;
- * enqueued on `stream` (a hipStream_t; NULL = the ctx's stream) and returns
- * without synchronising.  d_agg (8 doubles, fpf_aggregate layout) may be NULL.
+ * enqueued on `stream` (a hipStream_t; NULL = the NULL/default stream, as in
+ * every HIP API) and returns without synchronising.  d_agg (8 doubles, fpf_aggregate layout) may be NULL.
  * Returns FPF_OK or an error (the non-converged count is in d_agg / status). */
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);

@@ -58,8 +58,7 @@ def test_auto_kernel_choice():
     g = load_golden("g3_123bus")
     assert _pf(g["Dl"], g["Z"]).kernel == "tiled"
     f = F.demo_feeder()
-    Dl = f.Dl[[0, 6, 7, 8, 5, 1, 2, 3, 4]].copy()     # lateral before its tap's row: legal, not well formed
-    Dl[4] = 0
+    Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # 2->3 before 1->2: legal for the reference, not well formed
     pf = _pf(Dl, f.Z)
     assert pf.kernel == "generic" and pf.info["well_formed"] == 0
     from freedm_amd import DPFError
@@ -70,8 +69,7 @@ def test_auto_kernel_choice():
 def test_malformed_order_matches_oracle():
     from oracle import oracle as O
     f = F.demo_feeder()
-    Dl = f.Dl[[0, 6, 7, 8, 5, 1, 2, 3, 4]].copy()
-    Dl[4] = 0
+    Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # forward reads V(2) of the previous sweep
     pq = F.scenario_loads(F.Feeder(Dl, f.Z), np.arange(40))
     r = _pf(Dl, f.Z).solve(pq)
     c = O.dpf_batch(Dl, f.Z, pq, nthreads=4)
