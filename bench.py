@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--scenarios", type=int, default=SCEN_PER_GPU, help="scenarios per GPU per step")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--no-specialize", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -113,7 +114,7 @@ def main():
     from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
 
     feeder = synthetic_feeder(FEEDER_NODES, FEEDER_SEED)
-    pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile)
+    pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize)
     B = args.scenarios
     pf.reserve(B)
     ids = np.arange(rank * B, (rank + 1) * B)
@@ -193,7 +194,7 @@ def main():
             "data": "synthetic (seeded 123-bus radial feeder + seeded load/PV scenarios)",
             "config": {"workload": f"BASELINE config 2: 123-bus feeder, {B} scenarios per GPU per step",
                        "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
-                       "tile": pf.info["tile"], "parallelism": f"scenario shards x{world}"},
+                       "tile": pf.info["tile"], "specialized": pf.info["specialized"], "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "dpf_tiled_kernel" if pf.kernel == "tiled" else "dpf_generic_kernel",

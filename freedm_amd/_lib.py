@@ -26,13 +26,14 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
 class FpfOpts(C.Structure):
     _fields_ = [("bkva", C.c_double), ("bkv", C.c_double), ("vo_kv", C.c_double), ("eps", C.c_double),
                 ("mxitr", C.c_int), ("kernel", C.c_int), ("lb_v", C.c_double), ("ub_v", C.c_double),
-                ("tile", C.c_int), ("reserved", C.c_int * 7)]
+                ("tile", C.c_int), ("specialize", C.c_int), ("reserved", C.c_int * 6)]
 
 
 class FpfFeederInfo(C.Structure):
     _fields_ = [("nl", C.c_int), ("ncols", C.c_int), ("nn", C.c_int), ("nb", C.c_int), ("n_codes", C.c_int),
                 ("n_sep", C.c_int), ("n_taps", C.c_int), ("well_formed", C.c_int), ("lnum", C.c_int * 3),
-                ("depth", C.c_int), ("kernel", C.c_int), ("tile", C.c_int), ("reserved", C.c_int * 4)]
+                ("depth", C.c_int), ("kernel", C.c_int), ("tile", C.c_int), ("specialized", C.c_int),
+                ("reserved", C.c_int * 3)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("reserved", "lnum")}

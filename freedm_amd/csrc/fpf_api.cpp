@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -51,6 +52,9 @@ struct fpf_feeder {
     size_t stage_bytes = 0;
     void *d_stage = nullptr;
     double *d_agg = nullptr;
+    // topology-specialised tiled kernel (hipRTC), if built
+    bool rtc = false;
+    RtcKernel rtc_kernel{};
 };
 
 static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
@@ -79,6 +83,7 @@ extern "C" void fpf_opts_default(fpf_opts *o) {
     o->lb_v = 0.96;             // load_system_data.cpp:23
     o->ub_v = 1.05;             // load_system_data.cpp:24
     o->tile = 0;
+    o->specialize = 1;
 }
 
 extern "C" int fpf_ctx_create(int device, fpf_ctx **out) {
@@ -491,6 +496,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     d.n_seq_bw = (int)h.seq_bw.size();
     d.n_seq_fw = (int)h.seq_fw.size();
     d.tile = tile;
+    d.prog_lds = 1;
+    if (tile >= 1 && tiled_lds_bytes(d, tile) > 160 * 1024) d.prog_lds = 0;   // programs stay in HBM/L2
 
     // kernel choice
     int kern = o.kernel;
@@ -502,6 +509,26 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     }
     in.kernel = kern;
     in.tile = kern == FPF_KERNEL_TILED ? tile : 0;
+    if (kern == FPF_KERNEL_TILED && o.specialize) {
+        RtcSpec sp;
+        sp.tile = tile;
+        sp.nn = h.nn;
+        sp.n_taps = h.n_taps;
+        sp.nt = tiled_threads(d, tile);
+        for (const auto &op : h.bwi) sp.bw.push_back({op.k, op.a, op.p});
+        for (const auto &op : h.fwi) sp.fw.push_back({op.dst, op.src, op.mask});
+        const char *lim = getenv("FPF_RTC_MAX_OPS");
+        const size_t max_ops = lim ? (size_t)atol(lim) : 1024;
+        if (sp.bw.size() <= max_ops && tiled_lds_bytes_rtc(d, tile) <= 64 * 1024) {
+            std::string err;
+            if (rtc_build(ctx->device, sp, &f->rtc_kernel, &err) == 0) {
+                f->rtc = true;
+            } else {
+                ctx->err = err;   // not fatal: the interpreted tiled kernel runs instead
+            }
+        }
+    }
+    in.specialized = f->rtc ? 1 : 0;
     *out = f;
     return FPF_OK;
 }
@@ -583,7 +610,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     o.vmax = u.vmax ? u.vmax : f->d_vmax;
     hipError_t e;
     if (f->info.kernel == FPF_KERNEL_TILED) {
-        e = launch_tiled(f->dev, n_scen, d_pq, o, st);
+        e = f->rtc ? rtc_launch(f->rtc_kernel, f->dev, n_scen, d_pq, o, st) : launch_tiled(f->dev, n_scen, d_pq, o, st);
     } else {
         if (!f->d_scratch || f->scratch_ld < (size_t)n_scen) {
             int rc = fpf_feeder_reserve(f, n_scen);

@@ -2,8 +2,22 @@
 // kernels (fpf_kernels.hip).  Everything the kernels read about a feeder is
 // precomputed once by fpf_feeder_create and lives in device memory.
 #pragma once
+#ifdef __HIPCC_RTC__
+// hipRTC (topology-specialised tiled kernel, fpf_rtc.cpp): no system headers
+using __hip_internal::int8_t;
+using __hip_internal::int16_t;
+using __hip_internal::int32_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+#define INFINITY __builtin_huge_val()
+#else
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <array>
+#include <string>
+#include <vector>
+#endif
 
 namespace fpf {
 
@@ -80,6 +94,7 @@ struct FeederDev {
     const SeqFw *seq_fw;     // tiled only (padded to SEQ_CHUNK)
     int32_t n_seq_bw, n_seq_fw;
     int32_t tile;            // tile the programs were built for
+    int32_t prog_lds;        // 1: stage the programs in LDS; 0: read them from global memory
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -90,7 +105,8 @@ struct OutDev {
     double *loss, *vmin, *vmax;
 };
 
-// launchers (fpf_kernels.hip)
+#ifndef __HIPCC_RTC__
+// launchers (fpf_generic.hip, fpf_tiled.hip, fpf_rtc.cpp)
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st);
 hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
@@ -98,6 +114,24 @@ hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
                             double *d_agg, hipStream_t st);
 size_t tiled_lds_bytes(const FeederDev &f, int tile);
+size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile);
 int tiled_max_tile(const FeederDev &f);
+int tiled_threads(const FeederDev &f, int tile);
+
+// topology-specialised tiled kernel (fpf_rtc.cpp)
+struct RtcSpec {
+    int tile, nn, n_taps, nt;
+    std::vector<std::array<int, 3>> bw;   // backward ops: node, tap read (-1), separator target (-1)
+    std::vector<std::array<int, 3>> fw;   // forward ops: dst, src, zero mask
+};
+struct RtcKernel {
+    hipModule_t mod;
+    hipFunction_t fn;
+    int nt;
+};
+int rtc_build(int device, const RtcSpec &spec, RtcKernel *out, std::string *err);
+hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
+                      hipStream_t st);
+#endif
 
 }  // namespace fpf

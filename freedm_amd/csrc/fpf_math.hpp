@@ -3,8 +3,10 @@
 // The library is compiled with -ffp-contract=off: the reference is ISO C++98
 // built without FMA contraction, and bit-exact V needs the same roundings.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <math.h>
+#endif
 
 #pragma clang fp contract(off)
 

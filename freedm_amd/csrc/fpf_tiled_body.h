@@ -1,0 +1,380 @@
+// fpf_tiled_body.h -- the tiled batched DPF kernel body for gfx950 (well-formed feeders).
+//
+// One workgroup owns a tile of TILE scenarios for the whole solve; their state
+// lives in LDS for all sweeps, so HBM only sees the loads in and the results
+// out.  One LDS slot per (node k, phase p, scenario s) -- byte offset
+// k*3*TILE*16 + (p*TILE + s)*16, a complex fp64 -- holds, in turn within a sweep:
+//     V(k)  --P1-->  IL(k-1)  --S1-->  Ib(k-1)  --P2-->  drop(k)  --S2-->  V(k)
+// Slot 0 keeps the constant V0 (the substation, DPF_return7.cpp:84-96).
+//
+//   P1 (parallel, one task per (s,k), 3 phases per lane):  IL = conj(Sld/V)   :106-130
+//   S1 (sequential, one lane per (s,p)): the backward program in row order     :134-160
+//      with tap accumulators in LDS, then the substation convergence test     :199-210
+//   P2 (parallel): drop(k) = lng*(Ib(k-1) . Zl)  (TEMP table, ZGEMM order)    :163-178
+//   S2 (sequential): V(dst) = V(src) - drop(dst), phase zeroing               :169-195
+//   epilogue for scenarios that finish this sweep: Vpolar/PQb/PQL/V to HBM   :222-253
+//      and the VVC reductions (loss, Vmin/Vmax) in the reference's order.
+// Every arithmetic step is the reference's operation on the same operands, so V
+// is bit-identical to the sequential program (and to the oracle).
+//
+// The parallel stages carry the divisions and the 3x3 products; the sequential
+// stages are 1-2 dependent complex adds per row, three lanes (phases) per
+// scenario on one wave per SIMD.  Their programs (fpf_internal.h: separators
+// folded into branch ops, LDS byte offsets baked in, zero/dummy slots instead
+// of branches) sit in LDS and run in chunks of SEQ_CHUNK ops: a chunk's
+// descriptors and all its LDS operands are loaded first, so the dependent chain
+// waits on the adds, not on LDS latency.  A lane keeps Sld, IL and Ib of its
+// tasks in VGPRs across the sweep.
+#pragma once
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fpf {
+
+#ifdef FPF_STAMPS
+// diagnostic build only: lane 0 of each of the first 64 workgroups records
+// s_memtime at every stage boundary (never read by the kernel itself)
+__device__ unsigned long long *fpf_stamp_buf = nullptr;
+#define STAMP(idx)                                                                                  \
+    do {                                                                                            \
+        if (fpf_stamp_buf && threadIdx.x == 0 && blockIdx.x < 64 && (idx) < 128)                    \
+            fpf_stamp_buf[blockIdx.x * 128 + (idx)] = __builtin_amdgcn_s_memtime();                 \
+    } while (0)
+#else
+#define STAMP(idx) ((void)0)
+#endif
+
+namespace {
+
+constexpr int MAXT = 2;          // tasks per lane
+constexpr int MAX_SEQ_TILE = 16; // scenarios per workgroup (flag arrays)
+constexpr int U = SEQ_CHUNK;
+
+struct Flags {
+    int active[MAX_SEQ_TILE];    // still iterating
+    int fin[MAX_SEQ_TILE];       // 1 = converged this sweep, 2 = hit mxitr this sweep
+};
+
+__device__ __forceinline__ cx lds_ld(const double2 *w, int i) {
+    const double2 v = w[i];
+    return mk(v.x, v.y);
+}
+__device__ __forceinline__ void lds_st(double2 *w, int i, cx v) { w[i] = make_double2(v.re, v.im); }
+
+// Outputs of node k, phase p (DPF_return7.cpp:222-253).  Not inlined: it runs
+// once per node per scenario, and inlining its hypot/atan six times per lane
+// would cost the sweep loop its occupancy.  Returns (Re SL, |V|) for the
+// ordered VVC reductions.
+__device__ __noinline__ double2 emit_node(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
+                                          cx v, cx ilv, cx ibv) {
+    const cx sv = cmul(v, mk(s3, 0.0));
+    const cx sb = cmul(sv, cconj(ibv));
+    const cx sl = cmul(sv, cconj(ilv));
+    const double mag = hypot(v.re, v.im);
+    const size_t o6 = ((size_t)(2 * p) * nn + k) * B + gs, o6i = o6 + (size_t)nn * B;
+    if (o.vpolar) { o.vpolar[o6] = mag; o.vpolar[o6i] = polar_angle(v, p); }
+    if (o.pqb) { o.pqb[o6] = sb.re; o.pqb[o6i] = sb.im; }
+    if (o.pql) { o.pql[o6] = sl.re; o.pql[o6i] = sl.im; }
+    if (o.v_re) o.v_re[((size_t)p * nn + k) * B + gs] = v.re;
+    if (o.v_im) o.v_im[((size_t)p * nn + k) * B + gs] = v.im;
+    return make_double2(sl.re, mag);
+}
+
+
+// Sequential stages from the LDS-staged op programs (fpf_internal.h: SeqBw/SeqFw),
+// executed in chunks of SEQ_CHUNK ops with all of a chunk's LDS operands
+// loaded before its dependent arithmetic.
+struct RuntimeProg {
+    static constexpr int kTile = 0;
+    static constexpr bool kLdsProgram = true;
+
+    __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *pbw, int nbw, cx &ibl) {
+        auto at = [&](uint32_t off) -> double2 * { return (double2 *)(L + off); };
+        for (int q0 = 0; q0 < nbw; q0 += U) {
+            SeqBw e[U];
+            cx vil[U], va[U], vt[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                e[u] = pbw[q0 + u];
+                e[u].r = __builtin_amdgcn_readfirstlane(e[u].r);
+                e[u].w = __builtin_amdgcn_readfirstlane(e[u].w);
+                e[u].a = __builtin_amdgcn_readfirstlane(e[u].a);
+                e[u].p = __builtin_amdgcn_readfirstlane(e[u].p);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double2 a = *at(e[u].r + lane_off), b = *at(e[u].a + lane_off),
+                              c = *at((e[u].p & ~BW_SEP) + lane_off);
+                vil[u] = mk(a.x, a.y);
+                va[u] = mk(b.x, b.y);
+                vt[u] = mk(c.x, c.y);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const cx x = cadd(cadd(va[u], ibl), vil[u]);
+                *at(e[u].w + lane_off) = make_double2(x.re, x.im);
+                const cx t = cadd(vt[u], x);
+                *at((e[u].p & ~BW_SEP) + lane_off) = make_double2(t.re, t.im);
+                ibl = (e[u].p & BW_SEP) ? mk(0, 0) : x;
+            }
+        }
+    }
+
+    __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, const SeqFw *pfw, int nfw, int qp) {
+        auto at = [&](uint32_t off) -> double2 * { return (double2 *)(L + off); };
+        cx vprev = mk(0, 0);
+        for (int q0 = 0; q0 < nfw; q0 += U) {
+            SeqFw e[U];
+            cx vd[U], vs[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                e[u] = pfw[q0 + u];
+                e[u].dst = __builtin_amdgcn_readfirstlane(e[u].dst);
+                e[u].src = __builtin_amdgcn_readfirstlane(e[u].src);
+                e[u].flags = __builtin_amdgcn_readfirstlane(e[u].flags);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double2 a = *at(e[u].dst + lane_off), b = *at(e[u].src + lane_off);
+                vd[u] = mk(a.x, a.y);
+                vs[u] = mk(b.x, b.y);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const cx sv = (e[u].flags & FW_PREV) ? vprev : vs[u];
+                cx rv = csub(sv, vd[u]);
+                if ((e[u].flags >> qp) & 1) rv = mk(0, 0);
+                *at(e[u].dst + lane_off) = make_double2(rv.re, rv.im);
+                vprev = rv;
+            }
+        }
+    }
+};
+
+}  // namespace
+
+// The kernel body.  Prog supplies the two sequential stages: RuntimeProg runs
+// the LDS-staged op programs (any well-formed feeder); the hipRTC path
+// (fpf_rtc.cpp) generates a Prog whose stages are the feeder's programs as
+// straight-line code with constant LDS offsets and a compile-time tile.
+template <int NT, class Prog>
+__device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const double *__restrict__ pq,
+                                           const OutDev &o) {
+    extern __shared__ double2 lds[];
+    constexpr int NW = NT / 64;
+    const int TILE = Prog::kTile > 0 ? Prog::kTile : f.tile;
+    const int nn = f.nn, nb = nn - 1, nl = f.nl;
+    const int nbw = f.n_seq_bw, nfw = f.n_seq_fw;
+    const uint32_t slot = 3u * (uint32_t)TILE * 16u;           // bytes per node slot
+    char *const L = (char *)lds;
+    const uint32_t w_bytes = (uint32_t)(nn + 2) * slot;
+    const uint32_t t_bytes = (uint32_t)(f.n_taps + 2) * slot;
+    Flags *fl = (Flags *)(L + w_bytes + t_bytes);
+    const bool plds = Prog::kLdsProgram && f.prog_lds;
+    SeqBw *pbw = plds ? (SeqBw *)(fl + 1) : (SeqBw *)f.seq_bw;
+    SeqFw *pfw = plds ? (SeqFw *)((SeqBw *)(fl + 1) + nbw) : (SeqFw *)f.seq_fw;
+    auto at = [&](uint32_t off) -> double2 * { return (double2 *)(L + off); };
+
+    const int tid = threadIdx.x;
+    const int s0 = blockIdx.x * TILE;
+    const int ns = min(TILE, B - s0);
+    const int ntask = TILE * nb;
+    const cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+    STAMP(0);
+
+    // ---- init: V slots = V0 (:92-96), zero/dummy slots 0, taps 0, flags, programs
+    for (int i = tid; i < (nn + 2) * 3 * TILE; i += NT) {
+        const int p = (i / TILE) % 3;
+        const cx v = i >= nn * 3 * TILE ? mk(0, 0) : (p == 0 ? v0[0] : (p == 1 ? v0[1] : v0[2]));
+        lds_st(lds, i, v);
+    }
+    for (int i = tid; i < (f.n_taps + 2) * 3 * TILE; i += NT) lds_st((double2 *)(L + w_bytes), i, mk(0, 0));
+    if (plds) {
+        for (int i = tid; i < nbw; i += NT) pbw[i] = f.seq_bw[i];
+        for (int i = tid; i < nfw; i += NT) pfw[i] = f.seq_fw[i];
+    }
+    if (tid < MAX_SEQ_TILE) {
+        fl->active[tid] = tid < ns ? 1 : 0;
+        fl->fin[tid] = 0;
+    }
+
+    // ---- per-task constants: LDS offset, TEMP block, Sld = (P + jQ)/(bkva/3) (:46-50)
+    cx sld[MAXT][3], il[MAXT][3], ib[MAXT][3];
+    const double *tz[MAXT];
+    uint32_t woff[MAXT];
+    int tsc[MAXT];                                   // scenario of the task, -1 = none
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+        const int t = tid + j * NT;
+        const int s = t % TILE, k = 1 + t / TILE;
+        tz[j] = f.tz;
+        woff[j] = 0;
+        tsc[j] = -1;
+        if (t < ntask && s < ns) {
+            const NodeOp nd = f.node_ops[k];
+            tz[j] = f.tz + 18 * (size_t)nd.fw;
+            woff[j] = (uint32_t)k * slot + (uint32_t)s * 16u;
+            tsc[j] = s;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx sl = mk(pq[((size_t)(2 * p) * nl + nd.row) * B + s0 + s],
+                                 pq[((size_t)(2 * p + 1) * nl + nd.row) * B + s0 + s]);
+                sld[j][p] = cdiv(sl, mk(f.s3, 0.0));
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) { il[j][p] = mk(0, 0); ib[j][p] = mk(0, 0); }
+    }
+
+    // sequential lanes: one sequential wave per SIMD (waves 0..3 of a workgroup
+    // land on distinct SIMDs); scenario s runs on wave s % NWS, lanes 3*(s/NWS) + p
+    constexpr int NWS = NW < 4 ? NW : 4;
+    const int wv = tid >> 6, ln = tid & 63;
+    const int qj = ln / 3, qp = ln - 3 * qj;
+    const int qs = qj * NWS + wv;
+    const bool qlane = wv < NWS && qj < 21 && qs < ns;
+    const int gbase = qj * 3;
+    const uint32_t lane_off = qlane ? ((uint32_t)qp * TILE + qs) * 16u : 0u;
+    cx ibo = mk(0, 0);
+    __syncthreads();
+    STAMP(1);
+
+    int n_active = ns;
+    for (int it = 0; it < f.mxitr && n_active > 0; ++it) {
+        // ---- P1: load currents
+#pragma unroll
+        for (int j = 0; j < MAXT; ++j) {
+            if (tsc[j] >= 0 && fl->active[tsc[j]]) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    double2 *w = at(woff[j] + p * TILE * 16);
+                    il[j][p] = load_current(sld[j][p], mk(w->x, w->y));
+                    *w = make_double2(il[j][p].re, il[j][p].im);
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(2 + it * 5);
+
+        // ---- S1: backward program + convergence
+        if (qlane && fl->active[qs]) {
+            cx ibl = mk(0, 0);
+            Prog::s1(L, lane_off, pbw, nbw, ibl);
+            // reset this lane's tap accumulators for the next sweep
+            for (int tp = 0; tp < f.n_taps; ++tp) *at(w_bytes + tp * slot + lane_off) = make_double2(0, 0);
+            // errmx = max_p |Ib(0,p) - Ibo(p)|  (first element, then strict '>')
+            const double2 b0 = *at(1 * slot + lane_off);
+            const cx ib0 = mk(b0.x, b0.y);
+            const cx d = csub(ib0, ibo);
+            const double df = hypot(d.re, d.im);
+            const double d0 = __shfl(df, gbase + 0, 64), d1 = __shfl(df, gbase + 1, 64),
+                         d2 = __shfl(df, gbase + 2, 64);
+            double errmx = d0;
+            if (d1 > errmx) errmx = d1;
+            if (d2 > errmx) errmx = d2;
+            ibo = ib0;
+            if (qp == 0) {
+                fl->fin[qs] = errmx < f.eps ? 1 : (it == f.mxitr - 1 ? 2 : 0);
+                if (errmx < f.eps || it == f.mxitr - 1) {
+                    if (o.iters) o.iters[s0 + qs] = it + 1;
+                    if (o.status) o.status[s0 + qs] = errmx < f.eps ? 0 : 1;
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(3 + it * 5);
+
+        // ---- P2: branch drops
+#pragma unroll
+        for (int j = 0; j < MAXT; ++j) {
+            if (tsc[j] >= 0 && fl->active[tsc[j]]) {
+                double2 *w0 = at(woff[j]), *w1 = at(woff[j] + TILE * 16), *w2 = at(woff[j] + 2 * TILE * 16);
+                ib[j][0] = mk(w0->x, w0->y);
+                ib[j][1] = mk(w1->x, w1->y);
+                ib[j][2] = mk(w2->x, w2->y);
+                const cx d0 = drop_col(tz[j], ib[j][0], ib[j][1], ib[j][2], 0);
+                const cx d1 = drop_col(tz[j], ib[j][0], ib[j][1], ib[j][2], 1);
+                const cx d2 = drop_col(tz[j], ib[j][0], ib[j][1], ib[j][2], 2);
+                *w0 = make_double2(d0.re, d0.im);
+                *w1 = make_double2(d1.re, d1.im);
+                *w2 = make_double2(d2.re, d2.im);
+            }
+        }
+        __syncthreads();
+        STAMP(4 + it * 5);
+
+        // ---- S2: forward program
+        if (qlane && fl->active[qs]) {
+            Prog::s2(L, lane_off, pfw, nfw, qp);
+        }
+        __syncthreads();
+        STAMP(5 + it * 5);
+
+        // ---- epilogue for scenarios finishing this sweep
+        int any_fin = 0;
+        for (int s = 0; s < ns; ++s) any_fin |= fl->active[s] && fl->fin[s];
+        if (any_fin) {
+#pragma unroll
+            for (int j = 0; j < MAXT; ++j) {
+                const int s = tsc[j];
+                if (s >= 0 && fl->active[s] && fl->fin[s]) {
+                    const int k = 1 + (tid + j * NT) / TILE;
+                    const size_t gs = (size_t)s0 + s;
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        double2 *w = at(woff[j] + p * TILE * 16);
+                        *w = emit_node(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p], ib[j][p]);
+                    }
+                }
+            }
+            __syncthreads();
+            if (qlane && fl->active[qs] && fl->fin[qs]) {
+                const int gs = s0 + qs;
+                // substation row 0: V0, Ib(0) (= ibo, this sweep's), IL(nn-1) = 0
+                const cx v = qp == 0 ? v0[0] : (qp == 1 ? v0[1] : v0[2]);
+                const double2 r0 = emit_node(o, f.s3, nn, B, 0, qp, (size_t)gs, v, mk(0, 0), ibo);
+                const cx sb = cmul(cmul(v, mk(f.s3, 0.0)), cconj(ibo));
+                const double mag0 = r0.y;
+                // loss: Armadillo accumulate over PQL col 2p (even rows -> acc1, odd -> acc2)
+                double acc1 = 0.0 + r0.x, acc2 = 0.0;
+                // V_abc_list: first K_p nonzero |V| in row order, zero padded
+                double mn = INFINITY, mx = -INFINITY;
+                int cnt = 0;
+                const int K = qp == 0 ? f.K[0] : (qp == 1 ? f.K[1] : f.K[2]);
+                if (mag0 != 0 && cnt < K) { mn = fmin(mn, mag0); mx = fmax(mx, mag0); ++cnt; }
+                for (int k = 1; k < nn; ++k) {
+                    const double2 r = *at(k * slot + lane_off);
+                    if (k & 1) acc2 += r.x; else acc1 += r.x;
+                    if (r.y != 0 && cnt < K) { mn = fmin(mn, r.y); mx = fmax(mx, r.y); ++cnt; }
+                }
+                if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+                const double x = sb.re - (acc1 + acc2);
+                const double x0 = __shfl(x, gbase + 0, 64), x1 = __shfl(x, gbase + 1, 64), x2 = __shfl(x, gbase + 2, 64);
+                const double n0 = __shfl(mn, gbase + 0, 64), n1 = __shfl(mn, gbase + 1, 64), n2 = __shfl(mn, gbase + 2, 64);
+                const double m0 = __shfl(mx, gbase + 0, 64), m1 = __shfl(mx, gbase + 1, 64), m2 = __shfl(mx, gbase + 2, 64);
+                if (qp == 0) {
+                    double vmin = n0, vmax = m0;
+                    if (n1 < vmin) vmin = n1;
+                    if (n2 < vmin) vmin = n2;
+                    if (m1 > vmax) vmax = m1;
+                    if (m2 > vmax) vmax = m2;
+                    if (o.loss) o.loss[gs] = ((0.0 + x0) + x2) + (0.0 + x1);
+                    if (o.vmin) o.vmin[gs] = vmin;
+                    if (o.vmax) o.vmax[gs] = vmax;
+                }
+            }
+            __syncthreads();
+            if (tid < ns && fl->fin[tid]) fl->active[tid] = 0;
+            __syncthreads();
+        }
+        STAMP(6 + it * 5);
+        n_active = 0;
+        for (int s = 0; s < ns; ++s) n_active += fl->active[s];
+    }
+    STAMP(127);
+}
+
+
+}  // namespace fpf

@@ -85,11 +85,12 @@ class VPQ:
 class PowerFlow:
     """Batched DPF_return7 on one GPU for one feeder."""
 
-    def __init__(self, feeder: Feeder, device: int = 0, kernel: str = "auto", tile: int = 0, **opts):
+    def __init__(self, feeder: Feeder, device: int = 0, kernel: str = "auto", tile: int = 0,
+                 specialize: bool = True, **opts):
         L = _lib.load()
         self.feeder = feeder
         self.ctx = _Ctx.get(device)
-        o = _lib.default_opts(kernel=kernel, tile=tile, **opts)
+        o = _lib.default_opts(kernel=kernel, tile=tile, specialize=int(bool(specialize)), **opts)
         self.opts = o
         dl = np.asfortranarray(feeder.Dl, dtype=np.float64)
         Z = np.asarray(feeder.Z, dtype=np.complex128)
@@ -107,6 +108,9 @@ class PowerFlow:
         self.info = info.as_dict()
         self.nl, self.nn = self.info["nl"], self.info["nn"]
         self.kernel = {1: "generic", 2: "tiled"}[self.info["kernel"]]
+        # a hipRTC failure is not fatal (the interpreted tiled kernel runs); keep why
+        self.rtc_error = self.ctx.err() if (self.kernel == "tiled" and specialize
+                                            and not self.info["specialized"]) else ""
 
     def __del__(self):
         try:

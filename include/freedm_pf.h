@@ -83,7 +83,9 @@ typedef struct fpf_opts {
     double lb_v;       /* 0.96  load_system_data.cpp:23 (hosting counters) */
     double ub_v;       /* 1.05  load_system_data.cpp:24                    */
     int    tile;       /* scenarios per workgroup for the tiled kernel, 0 = auto */
-    int    reserved[7];
+    int    specialize; /* 1 (default): compile the tiled kernel for the feeder's topology
+                          with hipRTC at fpf_feeder_create; 0: interpret its programs */
+    int    reserved[6];
 } fpf_opts;
 
 typedef struct fpf_feeder_info {
@@ -99,7 +101,8 @@ typedef struct fpf_feeder_info {
     int depth;         /* longest root-to-leaf chain                  */
     int kernel;        /* kernel AUTO resolves to                     */
     int tile;          /* scenarios per workgroup (tiled)             */
-    int reserved[4];
+    int specialized;   /* 1 if the tiled kernel is the hipRTC build   */
+    int reserved[3];
 } fpf_feeder_info;
 
 /* Per-scenario outputs; every pointer may be NULL (= not produced). */
