@@ -24,6 +24,15 @@ namespace fpf {
 
 #include "fpf_rtc_src.inc"
 
+#ifdef FPF_STAMPS
+// diagnostic build: the stamp buffer of the hipRTC module (fpf::fpf_stamp_buf)
+void *g_rtc_stamp_ptr = nullptr;
+extern "C" int fpf_debug_set_rtc_stamp_buffer(void *dptr) {
+    g_rtc_stamp_ptr = dptr;
+    return 0;
+}
+#endif
+
 namespace {
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, RtcKernel> g_cache;
@@ -90,8 +99,13 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
         *err = "hiprtcCreateProgram failed";
         return -1;
     }
+#ifdef FPF_STAMPS
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-DFPF_STAMPS"};
+    hiprtcResult rr = hiprtcCompileProgram(prog, 5, opts);
+#else
     const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
     hiprtcResult rr = hiprtcCompileProgram(prog, 4, opts);
+#endif
     if (rr != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -127,6 +141,14 @@ hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const 
     void *args[] = {&fa, &B, &p, &oa};
     const unsigned grid = (unsigned)((n_scen + f.tile - 1) / f.tile);
     const size_t lds = tiled_lds_bytes_rtc(f, f.tile);
+#ifdef FPF_STAMPS
+    {
+        hipDeviceptr_t sym;
+        size_t bytes = 0;
+        if (hipModuleGetGlobal(&sym, &bytes, k.mod, "_ZN3fpf13fpf_stamp_bufE") == hipSuccess && bytes == sizeof(void *))
+            (void)hipMemcpyHtoDAsync(sym, &g_rtc_stamp_ptr, sizeof(void *), st);
+    }
+#endif
     return hipModuleLaunchKernel(k.fn, grid, 1, 1, (unsigned)k.nt, 1, 1, (unsigned)lds, st, args, nullptr);
 }
 

@@ -24,14 +24,17 @@ def main():
     f = synthetic_feeder(nn, nn)
     L = _lib.load()
     L.fpf_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
+    L.fpf_debug_set_rtc_stamp_buffer.argtypes = [ctypes.c_void_p]
+    spec = os.environ.get("SPEC", "1") == "1"
     buf = torch.zeros(64 * 128, dtype=torch.int64, device="cuda")
-    pf = PowerFlow(f, tile=tile)
+    pf = PowerFlow(f, tile=tile, specialize=spec)
     pq = torch.from_numpy(scenario_loads(f, np.arange(B))).cuda()
     out = {"loss": torch.zeros(B, dtype=torch.float64, device="cuda"),
            "iters": torch.zeros(B, dtype=torch.int32, device="cuda")}
     pf.solve_device(pq, out)
     torch.cuda.synchronize()
     assert L.fpf_debug_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
+    assert L.fpf_debug_set_rtc_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
     pf.solve_device(pq, out)
     torch.cuda.synchronize()
     st = buf.view(64, 128).cpu().numpy().astype(np.int64)
@@ -52,7 +55,7 @@ def main():
         rows.append(d)
     keys = ["init"] + names + ["total"]
     mean = {k: float(np.mean([r[k] for r in rows])) for k in keys}
-    print(json.dumps({"nn": nn, "B": B, "tile": pf.info["tile"], "iters": iters, "blocks": len(rows),
+    print(json.dumps({"nn": nn, "B": B, "tile": pf.info["tile"], "specialized": pf.info["specialized"], "iters": iters, "blocks": len(rows),
                       "mean_cycles": mean,
                       "share": {k: mean[k] / mean["total"] for k in keys if k != "total"}}))
 
