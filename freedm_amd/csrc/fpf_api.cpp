@@ -391,6 +391,44 @@ void build_seq_programs(HostFeeder &h, int tile) {
     pad_fw();
 }
 
+bool wants_rtc(const HostFeeder &h, const fpf_opts &o) {
+    const char *lim = getenv("FPF_RTC_MAX_OPS");
+    const size_t max_ops = lim ? (size_t)atol(lim) : 1024;
+    return h.wf && o.specialize && (o.kernel == FPF_KERNEL_AUTO || o.kernel == FPF_KERNEL_TILED) &&
+           h.bwi.size() <= max_ops;
+}
+
+// tile for the tiled kernel; *nt / *maxt describe the specialised build's geometry
+int choose_tile(const HostFeeder &h, const fpf_opts &o, int *nt = nullptr, int *maxt = nullptr) {
+    if (!h.wf) return 0;
+    FeederDev probe{};
+    probe.nn = h.nn;
+    probe.n_taps = h.n_taps;
+    int tmax, n = 0, m = 0;
+    if (wants_rtc(h, o)) {
+        tmax = rtc_tile(probe, &n, &m);
+        if (tmax < 1) tmax = tiled_max_tile(probe);
+    } else {
+        tmax = tiled_max_tile(probe);
+    }
+    if (nt) *nt = n;
+    if (maxt) *maxt = m;
+    return o.tile > 0 ? std::min(o.tile, tmax) : tmax;
+}
+
+RtcSpec make_rtc_spec(const HostFeeder &h, int tile, int nt, int maxt) {
+    RtcSpec sp;
+    sp.tile = tile;
+    sp.nn = h.nn;
+    sp.n_taps = h.n_taps;
+    sp.nt = nt;
+    sp.maxt = maxt;
+    sp.min_waves = maxt == 1 ? 4 : 2;
+    for (const auto &op : h.bwi) sp.bw.push_back({op.k, op.a, op.p});
+    for (const auto &op : h.fwi) sp.fw.push_back({op.dst, op.src, op.mask});
+    return sp;
+}
+
 template <class T>
 size_t push_blob(std::vector<char> &blob, const std::vector<T> &v) {
     size_t off = (blob.size() + 255) & ~(size_t)255;
@@ -436,17 +474,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     in.depth = h.depth;
 
     // tile of the tiled kernel (the sequential programs are built for it)
-    int tile = 0;
-    if (h.wf) {
-        FeederDev probe{};
-        probe.nn = h.nn;
-        probe.n_taps = h.n_taps;
-        probe.n_seq_bw = (int)((h.bwi.size() * 2 + SEQ_CHUNK) / SEQ_CHUNK * SEQ_CHUNK);
-        probe.n_seq_fw = (int)((h.fwi.size() * 2 + SEQ_CHUNK) / SEQ_CHUNK * SEQ_CHUNK);
-        const int tmax = tiled_max_tile(probe);
-        tile = o.tile > 0 ? std::min(o.tile, tmax) : tmax;
-        if (tile >= 1) build_seq_programs(h, tile);
-    }
+    const int tile = choose_tile(h, o);
+    if (tile >= 1) build_seq_programs(h, tile);
     // upload all tables as one blob
     std::vector<char> blob;
     const size_t o_tz = push_blob(blob, h.tz);
@@ -509,17 +538,13 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     }
     in.kernel = kern;
     in.tile = kern == FPF_KERNEL_TILED ? tile : 0;
-    if (kern == FPF_KERNEL_TILED && o.specialize) {
-        RtcSpec sp;
-        sp.tile = tile;
-        sp.nn = h.nn;
-        sp.n_taps = h.n_taps;
-        sp.nt = tiled_threads(d, tile);
-        for (const auto &op : h.bwi) sp.bw.push_back({op.k, op.a, op.p});
-        for (const auto &op : h.fwi) sp.fw.push_back({op.dst, op.src, op.mask});
-        const char *lim = getenv("FPF_RTC_MAX_OPS");
-        const size_t max_ops = lim ? (size_t)atol(lim) : 1024;
-        if (sp.bw.size() <= max_ops && tiled_lds_bytes_rtc(d, tile) <= 64 * 1024) {
+    int rtc_nt = 0, rtc_maxt = 0;
+    (void)choose_tile(h, o, &rtc_nt, &rtc_maxt);
+    // an explicit tile above the default geometry takes more tasks per lane
+    while (rtc_nt > 0 && rtc_maxt < 4 && tile * (h.nn - 1) > rtc_nt * rtc_maxt) ++rtc_maxt;
+    if (kern == FPF_KERNEL_TILED && wants_rtc(h, o) && rtc_nt > 0 && tile * (h.nn - 1) <= rtc_nt * rtc_maxt) {
+        const RtcSpec sp = make_rtc_spec(h, tile, rtc_nt, rtc_maxt);
+        if (tiled_lds_bytes_rtc(d, tile) <= 64 * 1024) {
             std::string err;
             if (rtc_build(ctx->device, sp, &f->rtc_kernel, &err) == 0) {
                 f->rtc = true;
@@ -696,4 +721,35 @@ extern "C" int fpf_solve_batch(fpf_feeder *f, int n_scen, const double *pq, cons
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (agg) std::memcpy(agg, h_agg, sizeof(h_agg));
     return (int)h_agg[4];   // non-converged count
+}
+
+extern "C" long fpf_feeder_rtc_source(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+                                      const fpf_opts *opts, char *buf, size_t buf_size) {
+    if (!dl || nl < 1 || ncols < 12 || z_rows < 0 || (z_rows > 0 && !z)) return FPF_ERR_ARG;
+    fpf_opts o;
+    if (opts) o = *opts;
+    else fpf_opts_default(&o);
+    HostFeeder h;
+    h.nl = nl;
+    h.ncols = ncols;
+    h.dl.assign(dl, dl + (size_t)nl * ncols);
+    std::string why = build_ops(h, z, z_rows, z_cols, o);
+    if (why.empty()) why = build_lnum(h, z, z_rows, o);
+    if (!why.empty()) return FPF_ERR_TOPOLOGY;
+    analyse_tiled(h);
+    const int tile = choose_tile(h, o);
+    if (tile < 1) return FPF_ERR_UNSUPPORTED;
+    FeederDev d{};
+    d.nn = h.nn;
+    d.n_taps = h.n_taps;
+    int nt = 0, maxt = 0;
+    (void)choose_tile(h, o, &nt, &maxt);
+    if (nt == 0) return FPF_ERR_UNSUPPORTED;
+    const std::string src = rtc_source(make_rtc_spec(h, tile, nt, maxt));
+    if (buf && buf_size > 0) {
+        const size_t n = std::min(buf_size - 1, src.size());
+        std::memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return (long)src.size() + 1;
 }

@@ -117,10 +117,13 @@ size_t tiled_lds_bytes(const FeederDev &f, int tile);
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile);
 int tiled_max_tile(const FeederDev &f);
 int tiled_threads(const FeederDev &f, int tile);
+int rtc_tile(const FeederDev &f, int *nt, int *maxt);
 
 // topology-specialised tiled kernel (fpf_rtc.cpp)
 struct RtcSpec {
     int tile, nn, n_taps, nt;
+    int maxt = 1;                         // tasks per lane
+    int min_waves = 4;                    // __launch_bounds__ minimum waves per SIMD
     std::vector<std::array<int, 3>> bw;   // backward ops: node, tap read (-1), separator target (-1)
     std::vector<std::array<int, 3>> fw;   // forward ops: dst, src, zero mask
 };
@@ -129,6 +132,7 @@ struct RtcKernel {
     hipFunction_t fn;
     int nt;
 };
+std::string rtc_source(const RtcSpec &spec);
 int rtc_build(int device, const RtcSpec &spec, RtcKernel *out, std::string *err);
 hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
                       hipStream_t st);

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -37,6 +38,13 @@ namespace {
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, RtcKernel> g_cache;
 
+// Straight-line sequential programs, emitted in chunks of kChunk ops: each
+// chunk first loads every LDS operand no earlier op of the chunk writes, then
+// runs its dependent arithmetic, so LDS latency overlaps the chain instead of
+// sitting on it.  Operands an earlier op of the chunk writes (a tap accumulator
+// a separator of the same chunk just added into) are read in program order.
+constexpr int kChunk = 8;
+
 std::string gen_program(const RtcSpec &sp) {
     const long slot = 3L * sp.tile;                       // double2 per node slot
     const long tbase = (long)(sp.nn + 2) * slot;
@@ -45,48 +53,108 @@ std::string gen_program(const RtcSpec &sp) {
     std::ostringstream o;
     o << "namespace fpf {\nstruct GenProg {\n"
       << "  static constexpr int kTile = " << sp.tile << ";\n"
-      << "  static constexpr bool kLdsProgram = false;\n"
-      // backward: x = (T[a] + Ibl) + IL[k]  (T[a] = 0 for non-taps; 0 + Ibl == Ibl bit for
-      // bit because Ibl is never -0), Ib[k] = x, separator: T[p] += x, Ibl = 0
-      << "  __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *, int, cx &ibl) {\n"
-      << "    double2 *B = (double2 *)(L + lane_off);\n    double2 w_, t_;\n    cx x;\n";
-    for (const auto &op : sp.bw) {
-        o << "    w_ = B[" << W(op[0]) << "];";
-        if (op[1] >= 0)
-            o << " t_ = B[" << T(op[1]) << "]; x = cadd(cadd(mk(t_.x, t_.y), ibl), mk(w_.x, w_.y));";
-        else
-            o << " x = cadd(ibl, mk(w_.x, w_.y));";
-        o << " B[" << W(op[0]) << "] = make_double2(x.re, x.im);";
-        if (op[2] >= 0)
-            o << " t_ = B[" << T(op[2]) << "]; B[" << T(op[2]) << "] = make_double2(t_.x + x.re, t_.y + x.im); ibl = mk(0, 0);\n";
-        else
-            o << " ibl = x;\n";
+      << "  static constexpr int kNN = " << sp.nn << ";\n"
+      << "  static constexpr bool kInlineEmit = false;\n"
+      << "  static constexpr bool kLdsProgram = false;\n";
+    // backward: x = (T[a] + Ibl) + IL[k]  (non-taps: 0 + Ibl == Ibl bit for bit, Ibl is
+    // never -0), Ib[k] = x; a separator folded in: T[p] = T[p] + x, Ibl = 0
+    o << "  __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *, int, cx &ibl) {\n"
+      << "    double2 *B = (double2 *)(L + lane_off);\n";
+    const int nbw = (int)sp.bw.size();
+    for (int c0 = 0; c0 < nbw; c0 += kChunk) {
+        const int c1 = std::min(nbw, c0 + kChunk);
+        o << "    {\n";
+        std::vector<int> tw;   // T slots written so far in this chunk
+        std::vector<char> ta_early(c1 - c0, 0), tp_early(c1 - c0, 0);
+        for (int i = c0; i < c1; ++i) {
+            const auto &op = sp.bw[i];
+            o << "      const double2 w" << i - c0 << " = B[" << W(op[0]) << "];\n";
+            if (op[1] >= 0 && std::find(tw.begin(), tw.end(), op[1]) == tw.end()) {
+                ta_early[i - c0] = 1;
+                o << "      const double2 a" << i - c0 << " = B[" << T(op[1]) << "];\n";
+            }
+            if (op[2] >= 0 && std::find(tw.begin(), tw.end(), op[2]) == tw.end()) {
+                tp_early[i - c0] = 1;
+                o << "      const double2 p" << i - c0 << " = B[" << T(op[2]) << "];\n";
+            }
+            if (op[2] >= 0) tw.push_back(op[2]);
+        }
+        for (int i = c0; i < c1; ++i) {
+            const auto &op = sp.bw[i];
+            const int j = i - c0;
+            o << "      {";
+            if (op[1] >= 0) {
+                if (ta_early[j]) o << " const double2 t_ = a" << j << ";";
+                else o << " const double2 t_ = B[" << T(op[1]) << "];";
+                o << " const cx x = cadd(cadd(mk(t_.x, t_.y), ibl), mk(w" << j << ".x, w" << j << ".y));";
+            } else {
+                o << " const cx x = cadd(ibl, mk(w" << j << ".x, w" << j << ".y));";
+            }
+            o << " B[" << W(op[0]) << "] = make_double2(x.re, x.im);";
+            if (op[2] >= 0) {
+                if (tp_early[j]) o << " const double2 q_ = p" << j << ";";
+                else o << " const double2 q_ = B[" << T(op[2]) << "];";
+                o << " B[" << T(op[2]) << "] = make_double2(q_.x + x.re, q_.y + x.im); ibl = mk(0, 0); }\n";
+            } else {
+                o << " ibl = x; }\n";
+            }
+        }
+        o << "    }\n";
     }
-    o << "  }\n"
-      // forward: V[dst] = V[src] - drop[dst], phases in mask zeroed
-      << "  __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, const SeqFw *, int, int qp) {\n"
-      << "    double2 *B = (double2 *)(L + lane_off);\n    double2 d_, s_;\n    cx v = mk(0, 0);\n";
+    o << "  }\n";
+    // forward: V[dst] = V[src] - drop[dst], phases in mask zeroed
+    o << "  __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, const SeqFw *, int, int qp) {\n"
+      << "    double2 *B = (double2 *)(L + lane_off);\n    cx v = mk(0, 0);\n";
+    const int nfw = (int)sp.fw.size();
     int prev = -1;
-    for (const auto &op : sp.fw) {
-        o << "    d_ = B[" << W(op[0]) << "];";
-        if (!(op[1] != 0 && op[1] == prev)) o << " s_ = B[" << W(op[1]) << "]; v = mk(s_.x, s_.y);";
-        o << " v = csub(v, mk(d_.x, d_.y));";
-        if (op[2]) o << " if ((" << op[2] << " >> qp) & 1) v = mk(0, 0);";
-        o << " B[" << W(op[0]) << "] = make_double2(v.re, v.im);\n";
-        prev = op[0];
+    for (int c0 = 0; c0 < nfw; c0 += kChunk) {
+        const int c1 = std::min(nfw, c0 + kChunk);
+        o << "    {\n";
+        std::vector<int> written;
+        std::vector<char> s_early(c1 - c0, 0), s_prev(c1 - c0, 0);
+        int pv = prev;
+        for (int i = c0; i < c1; ++i) {
+            const auto &op = sp.fw[i];
+            o << "      const double2 d" << i - c0 << " = B[" << W(op[0]) << "];\n";
+            if (op[1] != 0 && op[1] == pv) {
+                s_prev[i - c0] = 1;
+            } else if (std::find(written.begin(), written.end(), op[1]) == written.end()) {
+                s_early[i - c0] = 1;
+                o << "      const double2 s" << i - c0 << " = B[" << W(op[1]) << "];\n";
+            }
+            written.push_back(op[0]);
+            pv = op[0];
+        }
+        for (int i = c0; i < c1; ++i) {
+            const auto &op = sp.fw[i];
+            const int j = i - c0;
+            o << "      {";
+            if (s_early[j]) o << " v = mk(s" << j << ".x, s" << j << ".y);";
+            else if (!s_prev[j]) o << " { const double2 s_ = B[" << W(op[1]) << "]; v = mk(s_.x, s_.y); }";
+            o << " v = csub(v, mk(d" << j << ".x, d" << j << ".y));";
+            if (op[2]) o << " if ((" << op[2] << " >> qp) & 1) v = mk(0, 0);";
+            o << " B[" << W(op[0]) << "] = make_double2(v.re, v.im); }\n";
+            prev = op[0];
+        }
+        o << "    }\n";
     }
     o << "  }\n};\n}  // namespace fpf\n"
-      << "extern \"C\" __global__ __launch_bounds__(" << sp.nt << ", 2) void fpf_rtc_tiled(fpf::FeederDev f, int B, "
+      << "extern \"C\" __global__ __launch_bounds__(" << sp.nt << ", " << sp.min_waves << ") void fpf_rtc_tiled(fpf::FeederDev f, int B, "
       << "const double *__restrict__ pq, fpf::OutDev o) {\n"
-      << "  fpf::tiled_body<" << sp.nt << ", fpf::GenProg>(f, B, pq, o);\n}\n";
+      << "  fpf::tiled_body<" << sp.nt << ", " << sp.maxt << ", fpf::GenProg>(f, B, pq, o);\n}\n";
     return o.str();
 }
 }  // namespace
 
-int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
+std::string rtc_source(const RtcSpec &sp) {
     std::string src;
     for (const char *part : kRtcSources) src += part;
     src += gen_program(sp);
+    return src;
+}
+
+int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
+    const std::string src = rtc_source(sp);
     std::lock_guard<std::mutex> lk(g_mu);
     auto key = std::make_pair(device, src);
     auto it = g_cache.find(key);

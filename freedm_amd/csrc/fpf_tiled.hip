@@ -9,7 +9,7 @@ namespace fpf {
 template <int NT>
 __global__ __launch_bounds__(NT, 2) void dpf_tiled_kernel(FeederDev f, int B, const double *__restrict__ pq,
                                                           OutDev o) {
-    tiled_body<NT, RuntimeProg>(f, B, pq, o);
+    tiled_body<NT, AOT_MAXT, RuntimeProg>(f, B, pq, o);
 }
 
 namespace {
@@ -32,13 +32,29 @@ hipError_t launch_nt(const FeederDev &f, int n_scen, const double *pq, const Out
 
 int tiled_threads(const FeederDev &f, int tile) {
     const int tasks = tile * (f.nn - 1);
-    if (tasks <= 256 * MAXT) return 256;
-    if (tasks <= 512 * MAXT) return 512;
+    if (tasks <= 256 * AOT_MAXT) return 256;
+    if (tasks <= 512 * AOT_MAXT) return 512;
     return 1024;
 }
 namespace {
 int threads_for(const FeederDev &f, int tile) { return tiled_threads(f, tile); }
 }  // namespace
+
+// The specialised build keeps one task per lane in 512-thread workgroups capped
+// at 128 VGPRs, so two workgroups (tiles) share a CU and one's sequential
+// stages overlap the other's parallel stages.
+int rtc_tile(const FeederDev &f, int *nt, int *maxt) {
+    const int nb = f.nn - 1;
+    int t = std::min(MAX_SEQ_TILE, 512 / nb);
+    *nt = 512;
+    *maxt = 1;
+    if (t == 0) {
+        t = std::min(MAX_SEQ_TILE, 1024 / nb);
+        *maxt = 2;
+    }
+    while (t > 0 && tiled_lds_bytes_rtc(f, t) > 64 * 1024) --t;
+    return t;
+}
 
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile) {
     return sizeof(double2) * 3 * (size_t)tile * (size_t)(f.nn + 2 + f.n_taps + 2) + sizeof(Flags);
@@ -52,12 +68,9 @@ size_t tiled_lds_bytes(const FeederDev &f, int tile) {
 
 int tiled_max_tile(const FeederDev &f) {
     const int nb = f.nn - 1;
-    int t = std::min(MAX_SEQ_TILE, (512 * MAXT) / nb);
-    if (t == 0) t = std::min(MAX_SEQ_TILE, (1024 * MAXT) / nb);
+    int t = std::min(MAX_SEQ_TILE, (512 * AOT_MAXT) / nb);
+    if (t == 0) t = std::min(MAX_SEQ_TILE, (1024 * AOT_MAXT) / nb);
     while (t > 0 && tiled_lds_bytes_rtc(f, t) > 160 * 1024) --t;
-    // every sequential lane group must fit a wave: ceil(t / seq waves) * 3 <= 63
-    auto nws = [&](int tt) { return std::min(threads_for(f, tt) / 64, 4); };
-    while (t > 0 && (t + nws(t) - 1) / nws(t) > 21) --t;
     return t;
 }
 

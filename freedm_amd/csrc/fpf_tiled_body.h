@@ -48,7 +48,7 @@ __device__ unsigned long long *fpf_stamp_buf = nullptr;
 
 namespace {
 
-constexpr int MAXT = 2;          // tasks per lane
+constexpr int AOT_MAXT = 2;      // tasks per lane of the AOT (interpreted) build
 constexpr int MAX_SEQ_TILE = 16; // scenarios per workgroup (flag arrays)
 constexpr int U = SEQ_CHUNK;
 
@@ -67,8 +67,8 @@ __device__ __forceinline__ void lds_st(double2 *w, int i, cx v) { w[i] = make_do
 // once per node per scenario, and inlining its hypot/atan six times per lane
 // would cost the sweep loop its occupancy.  Returns (Re SL, |V|) for the
 // ordered VVC reductions.
-__device__ __noinline__ double2 emit_node(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
-                                          cx v, cx ilv, cx ibv) {
+__device__ __forceinline__ double2 emit_node_impl(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
+                                                 cx v, cx ilv, cx ibv) {
     const cx sv = cmul(v, mk(s3, 0.0));
     const cx sb = cmul(sv, cconj(ibv));
     const cx sl = cmul(sv, cconj(ilv));
@@ -81,6 +81,16 @@ __device__ __noinline__ double2 emit_node(const OutDev &o, double s3, int nn, in
     if (o.v_im) o.v_im[((size_t)p * nn + k) * B + gs] = v.im;
     return make_double2(sl.re, mag);
 }
+__device__ __noinline__ double2 emit_node_call(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
+                                               cx v, cx ilv, cx ibv) {
+    return emit_node_impl(o, s3, nn, B, k, p, gs, v, ilv, ibv);
+}
+template <bool kInline>
+__device__ __forceinline__ double2 emit_node(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
+                                             cx v, cx ilv, cx ibv) {
+    if constexpr (kInline) return emit_node_impl(o, s3, nn, B, k, p, gs, v, ilv, ibv);
+    else return emit_node_call(o, s3, nn, B, k, p, gs, v, ilv, ibv);
+}
 
 
 // Sequential stages from the LDS-staged op programs (fpf_internal.h: SeqBw/SeqFw),
@@ -88,6 +98,8 @@ __device__ __noinline__ double2 emit_node(const OutDev &o, double s3, int nn, in
 // loaded before its dependent arithmetic.
 struct RuntimeProg {
     static constexpr int kTile = 0;
+    static constexpr int kNN = 0;
+    static constexpr bool kInlineEmit = false;
     static constexpr bool kLdsProgram = true;
 
     __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *pbw, int nbw, cx &ibl) {
@@ -159,13 +171,13 @@ struct RuntimeProg {
 // the LDS-staged op programs (any well-formed feeder); the hipRTC path
 // (fpf_rtc.cpp) generates a Prog whose stages are the feeder's programs as
 // straight-line code with constant LDS offsets and a compile-time tile.
-template <int NT, class Prog>
+template <int NT, int MAXT, class Prog>
 __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const double *__restrict__ pq,
                                            const OutDev &o) {
     extern __shared__ double2 lds[];
     constexpr int NW = NT / 64;
     const int TILE = Prog::kTile > 0 ? Prog::kTile : f.tile;
-    const int nn = f.nn, nb = nn - 1, nl = f.nl;
+    const int nn = Prog::kNN > 0 ? Prog::kNN : f.nn, nb = nn - 1, nl = f.nl;
     const int nbw = f.n_seq_bw, nfw = f.n_seq_fw;
     const uint32_t slot = 3u * (uint32_t)TILE * 16u;           // bytes per node slot
     char *const L = (char *)lds;
@@ -228,9 +240,10 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
         for (int p = 0; p < 3; ++p) { il[j][p] = mk(0, 0); ib[j][p] = mk(0, 0); }
     }
 
-    // sequential lanes: one sequential wave per SIMD (waves 0..3 of a workgroup
-    // land on distinct SIMDs); scenario s runs on wave s % NWS, lanes 3*(s/NWS) + p
-    constexpr int NWS = NW < 4 ? NW : 4;
+    // sequential lanes: the stages are latency-bound chains, so a tile uses as
+    // few waves as fit it (21 scenarios x 3 phases per wave); scenario s runs on
+    // wave s % NWS, lanes 3*(s/NWS) + p
+    const int NWS = (TILE + 20) / 21 < NW ? (TILE + 20) / 21 : NW;
     const int wv = tid >> 6, ln = tid & 63;
     const int qj = ln / 3, qp = ln - 3 * qj;
     const int qs = qj * NWS + wv;
@@ -325,7 +338,7 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         double2 *w = at(woff[j] + p * TILE * 16);
-                        *w = emit_node(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p], ib[j][p]);
+                        *w = emit_node<Prog::kInlineEmit>(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p], ib[j][p]);
                     }
                 }
             }
@@ -334,7 +347,7 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
                 const int gs = s0 + qs;
                 // substation row 0: V0, Ib(0) (= ibo, this sweep's), IL(nn-1) = 0
                 const cx v = qp == 0 ? v0[0] : (qp == 1 ? v0[1] : v0[2]);
-                const double2 r0 = emit_node(o, f.s3, nn, B, 0, qp, (size_t)gs, v, mk(0, 0), ibo);
+                const double2 r0 = emit_node<Prog::kInlineEmit>(o, f.s3, nn, B, 0, qp, (size_t)gs, v, mk(0, 0), ibo);
                 const cx sb = cmul(cmul(v, mk(f.s3, 0.0)), cconj(ibo));
                 const double mag0 = r0.y;
                 // loss: Armadillo accumulate over PQL col 2p (even rows -> acc1, odd -> acc2)
@@ -344,10 +357,18 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
                 int cnt = 0;
                 const int K = qp == 0 ? f.K[0] : (qp == 1 ? f.K[1] : f.K[2]);
                 if (mag0 != 0 && cnt < K) { mn = fmin(mn, mag0); mx = fmax(mx, mag0); ++cnt; }
-                for (int k = 1; k < nn; ++k) {
-                    const double2 r = *at(k * slot + lane_off);
-                    if (k & 1) acc2 += r.x; else acc1 += r.x;
-                    if (r.y != 0 && cnt < K) { mn = fmin(mn, r.y); mx = fmax(mx, r.y); ++cnt; }
+                // rows 1..nn-1 in order; operands loaded 8 at a time ahead of the ordered adds
+                for (int k0 = 1; k0 < nn; k0 += 8) {
+                    double2 r[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) r[u] = k0 + u < nn ? *at((k0 + u) * slot + lane_off) : make_double2(0, 0);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (k0 + u < nn) {
+                            if ((k0 + u) & 1) acc2 += r[u].x; else acc1 += r[u].x;
+                            if (r[u].y != 0 && cnt < K) { mn = fmin(mn, r[u].y); mx = fmax(mx, r[u].y); ++cnt; }
+                        }
+                    }
                 }
                 if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
                 const double x = sb.re - (acc1 + acc2);

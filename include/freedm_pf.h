@@ -159,6 +159,13 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);
 
+/* Diagnostics (no device needed): the hipRTC source fpf_feeder_create would
+ * compile for this feeder's tiled kernel.  Writes at most buf_size bytes
+ * (NUL-terminated) and returns the full size including the NUL, or FPF_ERR_*. */
+long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
+                                  const double *z, int z_rows, int z_cols,
+                                  const fpf_opts *opts, char *buf, size_t buf_size);
+
 /* Device-memory batch aggregate over per-scenario results (deterministic
  * reduction); same layout as fpf_aggregate.  Lets a caller aggregate several
  * batches, or time the solve kernel alone. */
