@@ -38,107 +38,84 @@ namespace {
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, RtcKernel> g_cache;
 
-// Straight-line sequential programs, emitted in chunks of kChunk ops: each
-// chunk first loads every LDS operand no earlier op of the chunk writes, then
-// runs its dependent arithmetic, so LDS latency overlaps the chain instead of
-// sitting on it.  Operands an earlier op of the chunk writes (a tap accumulator
-// a separator of the same chunk just added into) are read in program order.
-constexpr int kChunk = 8;
+// Straight-line sequential programs as register dataflow: Ibl, the tap
+// accumulators and the forward voltages are SSA values, so a row's dependent
+// adds wait on the previous row's adds, never on an LDS store->load round trip.
+// LDS only supplies the operands the parallel stages produced (IL, drop) --
+// independent loads the compiler issues early -- and receives Ib / V for the
+// parallel stages and the epilogue.
+//
+// Zero folding (exact): Ibl, Ib and tap sums are never -0 (each is a sum with
+// an IL term; x + y == -0 needs both -0), so 0 + Ibl == Ibl and T + 0 == T bit
+// for bit; a fresh Ibl (+0) plus IL keeps its add because IL may be -0.
+// LDS operands are loaded kAhead rows ahead of their use: with the row's store
+// in between, 2*kAhead LDS ops are in flight, inside lgkmcnt's 4-bit range.
+constexpr int kAhead = 6;
 
 std::string gen_program(const RtcSpec &sp) {
     const long slot = 3L * sp.tile;                       // double2 per node slot
-    const long tbase = (long)(sp.nn + 2) * slot;
     auto W = [&](int k) { return (long)k * slot; };
-    auto T = [&](int t) { return tbase + (long)t * slot; };
     std::ostringstream o;
     o << "namespace fpf {\nstruct GenProg {\n"
       << "  static constexpr int kTile = " << sp.tile << ";\n"
       << "  static constexpr int kNN = " << sp.nn << ";\n"
-      << "  static constexpr bool kInlineEmit = false;\n"
-      << "  static constexpr bool kLdsProgram = false;\n";
-    // backward: x = (T[a] + Ibl) + IL[k]  (non-taps: 0 + Ibl == Ibl bit for bit, Ibl is
-    // never -0), Ib[k] = x; a separator folded in: T[p] = T[p] + x, Ibl = 0
-    o << "  __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *, int, cx &ibl) {\n"
+      << "  static constexpr bool kLdsProgram = false;\n"
+      << "  static constexpr bool kLdsTaps = false;\n"
+      << "  __device__ static __forceinline__ cx ld(const double2 *B, int i) { const double2 v = B[i]; return mk(v.x, v.y); }\n"
+      << "  __device__ static __forceinline__ void st(double2 *B, int i, cx v) { B[i] = make_double2(v.re, v.im); }\n";
+    // backward (DPF_return7.cpp:134-160 with separators folded into the preceding op):
+    // x = (T[a] + Ibl) + IL[k]; Ib[k] = x; separator: T[p] = T[p] + x, Ibl = 0
+    o << "  __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *, int, cx &) {\n"
       << "    double2 *B = (double2 *)(L + lane_off);\n";
-    const int nbw = (int)sp.bw.size();
-    for (int c0 = 0; c0 < nbw; c0 += kChunk) {
-        const int c1 = std::min(nbw, c0 + kChunk);
-        o << "    {\n";
-        std::vector<int> tw;   // T slots written so far in this chunk
-        std::vector<char> ta_early(c1 - c0, 0), tp_early(c1 - c0, 0);
-        for (int i = c0; i < c1; ++i) {
+    {
+        std::string ibl;                       // "" = +0
+        std::map<int, std::string> tap;        // absent = +0
+        const size_t nbw = sp.bw.size();
+        auto load_il = [&](size_t i) { o << "    const cx il" << i << " = ld(B, " << W(sp.bw[i][0]) << ");\n"; };
+        for (size_t i = 0; i < std::min(nbw, (size_t)kAhead); ++i) load_il(i);
+        for (size_t i = 0; i < nbw; ++i) {
             const auto &op = sp.bw[i];
-            o << "      const double2 w" << i - c0 << " = B[" << W(op[0]) << "];\n";
-            if (op[1] >= 0 && std::find(tw.begin(), tw.end(), op[1]) == tw.end()) {
-                ta_early[i - c0] = 1;
-                o << "      const double2 a" << i - c0 << " = B[" << T(op[1]) << "];\n";
-            }
-            if (op[2] >= 0 && std::find(tw.begin(), tw.end(), op[2]) == tw.end()) {
-                tp_early[i - c0] = 1;
-                o << "      const double2 p" << i - c0 << " = B[" << T(op[2]) << "];\n";
-            }
-            if (op[2] >= 0) tw.push_back(op[2]);
-        }
-        for (int i = c0; i < c1; ++i) {
-            const auto &op = sp.bw[i];
-            const int j = i - c0;
-            o << "      {";
-            if (op[1] >= 0) {
-                if (ta_early[j]) o << " const double2 t_ = a" << j << ";";
-                else o << " const double2 t_ = B[" << T(op[1]) << "];";
-                o << " const cx x = cadd(cadd(mk(t_.x, t_.y), ibl), mk(w" << j << ".x, w" << j << ".y));";
-            } else {
-                o << " const cx x = cadd(ibl, mk(w" << j << ".x, w" << j << ".y));";
-            }
-            o << " B[" << W(op[0]) << "] = make_double2(x.re, x.im);";
+            if (i + kAhead < nbw) load_il(i + kAhead);
+            const std::string il = "il" + std::to_string(i), x = "x" + std::to_string(i);
+            const std::string t = (op[1] >= 0 && tap.count(op[1])) ? tap[op[1]] : "";
+            o << "    const cx " << x << " = ";
+            if (!t.empty()) o << (ibl.empty() ? "cadd(" + t + ", " + il + ")" : "cadd(cadd(" + t + ", " + ibl + "), " + il + ")");
+            else o << (ibl.empty() ? "cadd(mk(0, 0), " + il + ")" : "cadd(" + ibl + ", " + il + ")");
+            o << "; st(B, " << W(op[0]) << ", " << x << ");";
             if (op[2] >= 0) {
-                if (tp_early[j]) o << " const double2 q_ = p" << j << ";";
-                else o << " const double2 q_ = B[" << T(op[2]) << "];";
-                o << " B[" << T(op[2]) << "] = make_double2(q_.x + x.re, q_.y + x.im); ibl = mk(0, 0); }\n";
+                auto it = tap.find(op[2]);
+                if (it == tap.end()) {
+                    tap[op[2]] = x;
+                } else {
+                    const std::string tn = "t" + std::to_string(i);
+                    o << " const cx " << tn << " = cadd(" << it->second << ", " << x << ");";
+                    it->second = tn;
+                }
+                ibl.clear();
             } else {
-                o << " ibl = x; }\n";
+                ibl = x;
             }
+            o << "\n";
         }
-        o << "    }\n";
     }
     o << "  }\n";
-    // forward: V[dst] = V[src] - drop[dst], phases in mask zeroed
+    // forward (:163-195): V[dst] = V[src] - drop[dst], phases in mask zeroed
     o << "  __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, const SeqFw *, int, int qp) {\n"
-      << "    double2 *B = (double2 *)(L + lane_off);\n    cx v = mk(0, 0);\n";
-    const int nfw = (int)sp.fw.size();
-    int prev = -1;
-    for (int c0 = 0; c0 < nfw; c0 += kChunk) {
-        const int c1 = std::min(nfw, c0 + kChunk);
-        o << "    {\n";
-        std::vector<int> written;
-        std::vector<char> s_early(c1 - c0, 0), s_prev(c1 - c0, 0);
-        int pv = prev;
-        for (int i = c0; i < c1; ++i) {
-            const auto &op = sp.fw[i];
-            o << "      const double2 d" << i - c0 << " = B[" << W(op[0]) << "];\n";
-            if (op[1] != 0 && op[1] == pv) {
-                s_prev[i - c0] = 1;
-            } else if (std::find(written.begin(), written.end(), op[1]) == written.end()) {
-                s_early[i - c0] = 1;
-                o << "      const double2 s" << i - c0 << " = B[" << W(op[1]) << "];\n";
-            }
-            written.push_back(op[0]);
-            pv = op[0];
-        }
-        for (int i = c0; i < c1; ++i) {
-            const auto &op = sp.fw[i];
-            const int j = i - c0;
-            o << "      {";
-            if (s_early[j]) o << " v = mk(s" << j << ".x, s" << j << ".y);";
-            else if (!s_prev[j]) o << " { const double2 s_ = B[" << W(op[1]) << "]; v = mk(s_.x, s_.y); }";
-            o << " v = csub(v, mk(d" << j << ".x, d" << j << ".y));";
-            if (op[2]) o << " if ((" << op[2] << " >> qp) & 1) v = mk(0, 0);";
-            o << " B[" << W(op[0]) << "] = make_double2(v.re, v.im); }\n";
-            prev = op[0];
-        }
-        o << "    }\n";
+      << "    double2 *B = (double2 *)(L + lane_off);\n"
+      << "    const cx v0 = ld(B, 0);\n";
+    const size_t nfw = sp.fw.size();
+    auto load_d = [&](size_t i) { o << "    const cx d" << i << " = ld(B, " << W(sp.fw[i][0]) << ");\n"; };
+    for (size_t i = 0; i < std::min(nfw, (size_t)kAhead); ++i) load_d(i);
+    for (size_t i = 0; i < nfw; ++i) {
+        const auto &op = sp.fw[i];
+        if (i + kAhead < nfw) load_d(i + kAhead);
+        const std::string v = "v" + std::to_string(op[0]);
+        o << "    cx " << v << " = csub(v" << op[1] << ", d" << i << ");";
+        if (op[2]) o << " if ((" << op[2] << " >> qp) & 1) " << v << " = mk(0, 0);";
+        o << " st(B, " << W(op[0]) << ", " << v << ");\n";
     }
-    o << "  }\n};\n}  // namespace fpf\n"
+    o << "  }\n";
+    o << "};\n}  // namespace fpf\n"
       << "extern \"C\" __global__ __launch_bounds__(" << sp.nt << ", " << sp.min_waves << ") void fpf_rtc_tiled(fpf::FeederDev f, int B, "
       << "const double *__restrict__ pq, fpf::OutDev o) {\n"
       << "  fpf::tiled_body<" << sp.nt << ", " << sp.maxt << ", fpf::GenProg>(f, B, pq, o);\n}\n";

@@ -12,7 +12,8 @@
 //      with tap accumulators in LDS, then the substation convergence test     :199-210
 //   P2 (parallel): drop(k) = lng*(Ib(k-1) . Zl)  (TEMP table, ZGEMM order)    :163-178
 //   S2 (sequential): V(dst) = V(src) - drop(dst), phase zeroing               :169-195
-//   epilogue for scenarios that finish this sweep: Vpolar/PQb/PQL/V to HBM   :222-253
+//   (a scenario retires after its last sweep; its state stays frozen)
+//   epilogue once per tile: Vpolar/PQb/PQL/V to HBM                           :222-253
 //      and the VVC reductions (loss, Vmin/Vmax) in the reference's order.
 // Every arithmetic step is the reference's operation on the same operands, so V
 // is bit-identical to the sequential program (and to the oracle).
@@ -63,12 +64,10 @@ __device__ __forceinline__ cx lds_ld(const double2 *w, int i) {
 }
 __device__ __forceinline__ void lds_st(double2 *w, int i, cx v) { w[i] = make_double2(v.re, v.im); }
 
-// Outputs of node k, phase p (DPF_return7.cpp:222-253).  Not inlined: it runs
-// once per node per scenario, and inlining its hypot/atan six times per lane
-// would cost the sweep loop its occupancy.  Returns (Re SL, |V|) for the
-// ordered VVC reductions.
-__device__ __forceinline__ double2 emit_node_impl(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
-                                                 cx v, cx ilv, cx ibv) {
+// Outputs of node k, phase p (DPF_return7.cpp:222-253).  Returns (Re SL, |V|)
+// for the ordered VVC reductions.
+__device__ __forceinline__ double2 emit_node(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs, cx v,
+                                             cx ilv, cx ibv) {
     const cx sv = cmul(v, mk(s3, 0.0));
     const cx sb = cmul(sv, cconj(ibv));
     const cx sl = cmul(sv, cconj(ilv));
@@ -81,17 +80,6 @@ __device__ __forceinline__ double2 emit_node_impl(const OutDev &o, double s3, in
     if (o.v_im) o.v_im[((size_t)p * nn + k) * B + gs] = v.im;
     return make_double2(sl.re, mag);
 }
-__device__ __noinline__ double2 emit_node_call(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
-                                               cx v, cx ilv, cx ibv) {
-    return emit_node_impl(o, s3, nn, B, k, p, gs, v, ilv, ibv);
-}
-template <bool kInline>
-__device__ __forceinline__ double2 emit_node(const OutDev &o, double s3, int nn, int B, int k, int p, size_t gs,
-                                             cx v, cx ilv, cx ibv) {
-    if constexpr (kInline) return emit_node_impl(o, s3, nn, B, k, p, gs, v, ilv, ibv);
-    else return emit_node_call(o, s3, nn, B, k, p, gs, v, ilv, ibv);
-}
-
 
 // Sequential stages from the LDS-staged op programs (fpf_internal.h: SeqBw/SeqFw),
 // executed in chunks of SEQ_CHUNK ops with all of a chunk's LDS operands
@@ -99,8 +87,8 @@ __device__ __forceinline__ double2 emit_node(const OutDev &o, double s3, int nn,
 struct RuntimeProg {
     static constexpr int kTile = 0;
     static constexpr int kNN = 0;
-    static constexpr bool kInlineEmit = false;
     static constexpr bool kLdsProgram = true;
+    static constexpr bool kLdsTaps = true;
 
     __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *pbw, int nbw, cx &ibl) {
         auto at = [&](uint32_t off) -> double2 * { return (double2 *)(L + off); };
@@ -276,7 +264,8 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
             cx ibl = mk(0, 0);
             Prog::s1(L, lane_off, pbw, nbw, ibl);
             // reset this lane's tap accumulators for the next sweep
-            for (int tp = 0; tp < f.n_taps; ++tp) *at(w_bytes + tp * slot + lane_off) = make_double2(0, 0);
+            if (Prog::kLdsTaps)
+                for (int tp = 0; tp < f.n_taps; ++tp) *at(w_bytes + tp * slot + lane_off) = make_double2(0, 0);
             // errmx = max_p |Ib(0,p) - Ibo(p)|  (first element, then strict '>')
             const double2 b0 = *at(1 * slot + lane_off);
             const cx ib0 = mk(b0.x, b0.y);
@@ -318,81 +307,77 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
         __syncthreads();
         STAMP(4 + it * 5);
 
-        // ---- S2: forward program
+        // ---- S2: forward program; a scenario whose last sweep this was retires
+        // (its state -- V in LDS, IL/Ib in the task registers, Ib(0) in ibo -- is
+        // then frozen until the epilogue)
         if (qlane && fl->active[qs]) {
             Prog::s2(L, lane_off, pfw, nfw, qp);
+            if (qp == 0 && fl->fin[qs]) fl->active[qs] = 0;
         }
         __syncthreads();
         STAMP(5 + it * 5);
-
-        // ---- epilogue for scenarios finishing this sweep
-        int any_fin = 0;
-        for (int s = 0; s < ns; ++s) any_fin |= fl->active[s] && fl->fin[s];
-        if (any_fin) {
-#pragma unroll
-            for (int j = 0; j < MAXT; ++j) {
-                const int s = tsc[j];
-                if (s >= 0 && fl->active[s] && fl->fin[s]) {
-                    const int k = 1 + (tid + j * NT) / TILE;
-                    const size_t gs = (size_t)s0 + s;
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) {
-                        double2 *w = at(woff[j] + p * TILE * 16);
-                        *w = emit_node<Prog::kInlineEmit>(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p], ib[j][p]);
-                    }
-                }
-            }
-            __syncthreads();
-            if (qlane && fl->active[qs] && fl->fin[qs]) {
-                const int gs = s0 + qs;
-                // substation row 0: V0, Ib(0) (= ibo, this sweep's), IL(nn-1) = 0
-                const cx v = qp == 0 ? v0[0] : (qp == 1 ? v0[1] : v0[2]);
-                const double2 r0 = emit_node<Prog::kInlineEmit>(o, f.s3, nn, B, 0, qp, (size_t)gs, v, mk(0, 0), ibo);
-                const cx sb = cmul(cmul(v, mk(f.s3, 0.0)), cconj(ibo));
-                const double mag0 = r0.y;
-                // loss: Armadillo accumulate over PQL col 2p (even rows -> acc1, odd -> acc2)
-                double acc1 = 0.0 + r0.x, acc2 = 0.0;
-                // V_abc_list: first K_p nonzero |V| in row order, zero padded
-                double mn = INFINITY, mx = -INFINITY;
-                int cnt = 0;
-                const int K = qp == 0 ? f.K[0] : (qp == 1 ? f.K[1] : f.K[2]);
-                if (mag0 != 0 && cnt < K) { mn = fmin(mn, mag0); mx = fmax(mx, mag0); ++cnt; }
-                // rows 1..nn-1 in order; operands loaded 8 at a time ahead of the ordered adds
-                for (int k0 = 1; k0 < nn; k0 += 8) {
-                    double2 r[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) r[u] = k0 + u < nn ? *at((k0 + u) * slot + lane_off) : make_double2(0, 0);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        if (k0 + u < nn) {
-                            if ((k0 + u) & 1) acc2 += r[u].x; else acc1 += r[u].x;
-                            if (r[u].y != 0 && cnt < K) { mn = fmin(mn, r[u].y); mx = fmax(mx, r[u].y); ++cnt; }
-                        }
-                    }
-                }
-                if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
-                const double x = sb.re - (acc1 + acc2);
-                const double x0 = __shfl(x, gbase + 0, 64), x1 = __shfl(x, gbase + 1, 64), x2 = __shfl(x, gbase + 2, 64);
-                const double n0 = __shfl(mn, gbase + 0, 64), n1 = __shfl(mn, gbase + 1, 64), n2 = __shfl(mn, gbase + 2, 64);
-                const double m0 = __shfl(mx, gbase + 0, 64), m1 = __shfl(mx, gbase + 1, 64), m2 = __shfl(mx, gbase + 2, 64);
-                if (qp == 0) {
-                    double vmin = n0, vmax = m0;
-                    if (n1 < vmin) vmin = n1;
-                    if (n2 < vmin) vmin = n2;
-                    if (m1 > vmax) vmax = m1;
-                    if (m2 > vmax) vmax = m2;
-                    if (o.loss) o.loss[gs] = ((0.0 + x0) + x2) + (0.0 + x1);
-                    if (o.vmin) o.vmin[gs] = vmin;
-                    if (o.vmax) o.vmax[gs] = vmax;
-                }
-            }
-            __syncthreads();
-            if (tid < ns && fl->fin[tid]) fl->active[tid] = 0;
-            __syncthreads();
-        }
-        STAMP(6 + it * 5);
         n_active = 0;
         for (int s = 0; s < ns; ++s) n_active += fl->active[s];
+    }
+    STAMP(126);
+
+    // ---- epilogue, once per tile: outputs of every (scenario, node, phase)
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+        const int s = tsc[j];
+        if (s >= 0) {
+            const int k = 1 + (tid + j * NT) / TILE;
+            const size_t gs = (size_t)s0 + s;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                double2 *w = at(woff[j] + p * TILE * 16);
+                *w = emit_node(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p], ib[j][p]);
+            }
+        }
+    }
+    __syncthreads();
+    if (qlane) {
+        const int gs = s0 + qs;
+        // substation row 0: V0, Ib(0) (= ibo, the last sweep's), IL(nn-1) = 0
+        const cx v = qp == 0 ? v0[0] : (qp == 1 ? v0[1] : v0[2]);
+        const double2 r0 = emit_node(o, f.s3, nn, B, 0, qp, (size_t)gs, v, mk(0, 0), ibo);
+        const cx sb = cmul(cmul(v, mk(f.s3, 0.0)), cconj(ibo));
+        const double mag0 = r0.y;
+        // loss: Armadillo accumulate over PQL col 2p (even rows -> acc1, odd -> acc2)
+        double acc1 = 0.0 + r0.x, acc2 = 0.0;
+        // V_abc_list: first K_p nonzero |V| in row order, zero padded
+        double mn = INFINITY, mx = -INFINITY;
+        int cnt = 0;
+        const int K = qp == 0 ? f.K[0] : (qp == 1 ? f.K[1] : f.K[2]);
+        if (mag0 != 0 && cnt < K) { mn = fmin(mn, mag0); mx = fmax(mx, mag0); ++cnt; }
+        // rows 1..nn-1 in order; operands loaded 8 at a time ahead of the ordered adds
+        for (int k0 = 1; k0 < nn; k0 += 8) {
+            double2 r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r[u] = k0 + u < nn ? *at((k0 + u) * slot + lane_off) : make_double2(0, 0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (k0 + u < nn) {
+                    if ((k0 + u) & 1) acc2 += r[u].x; else acc1 += r[u].x;
+                    if (r[u].y != 0 && cnt < K) { mn = fmin(mn, r[u].y); mx = fmax(mx, r[u].y); ++cnt; }
+                }
+            }
+        }
+        if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+        const double x = sb.re - (acc1 + acc2);
+        const double x0 = __shfl(x, gbase + 0, 64), x1 = __shfl(x, gbase + 1, 64), x2 = __shfl(x, gbase + 2, 64);
+        const double n0 = __shfl(mn, gbase + 0, 64), n1 = __shfl(mn, gbase + 1, 64), n2 = __shfl(mn, gbase + 2, 64);
+        const double m0 = __shfl(mx, gbase + 0, 64), m1 = __shfl(mx, gbase + 1, 64), m2 = __shfl(mx, gbase + 2, 64);
+        if (qp == 0) {
+            double vmin = n0, vmax = m0;
+            if (n1 < vmin) vmin = n1;
+            if (n2 < vmin) vmin = n2;
+            if (m1 > vmax) vmax = m1;
+            if (m2 > vmax) vmax = m2;
+            if (o.loss) o.loss[gs] = ((0.0 + x0) + x2) + (0.0 + x1);
+            if (o.vmin) o.vmin[gs] = vmin;
+            if (o.vmax) o.vmax[gs] = vmax;
+        }
     }
     STAMP(127);
 }

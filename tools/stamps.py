@@ -39,20 +39,23 @@ def main():
     torch.cuda.synchronize()
     st = buf.view(64, 128).cpu().numpy().astype(np.int64)
     iters = int(out["iters"].max().item())
-    names = ["P1", "S1", "P2", "S2", "epi"]
+    names = ["P1", "S1", "P2", "S2"]
     rows = []
     for b in range(64):
         s = st[b]
         if s[0] == 0:
             continue
-        d = {"init": s[1] - s[0], "total": s[127] - s[0]}
-        for it in range(iters):
-            prev = s[1] if it == 0 else s[6 + (it - 1) * 5]
-            cur = [s[2 + it * 5 + q] for q in range(5)]
-            seg = [cur[0] - prev] + [cur[q] - cur[q - 1] for q in range(1, 5)]
+        d = {"init": s[1] - s[0], "total": s[127] - s[0], "epi": s[127] - s[126]}
+        it = 0
+        while it < 24 and s[2 + it * 5] != 0:
+            prev = s[1] if it == 0 else s[5 + (it - 1) * 5]
+            cur = [s[2 + it * 5 + q] for q in range(4)]
+            seg = [cur[0] - prev] + [cur[q] - cur[q - 1] for q in range(1, 4)]
             for nme, v in zip(names, seg):
                 d[nme] = d.get(nme, 0) + v
+            it += 1
         rows.append(d)
+    names = names + ["epi"]
     keys = ["init"] + names + ["total"]
     mean = {k: float(np.mean([r[k] for r in rows])) for k in keys}
     print(json.dumps({"nn": nn, "B": B, "tile": pf.info["tile"], "specialized": pf.info["specialized"], "iters": iters, "blocks": len(rows),
