@@ -423,7 +423,11 @@ RtcSpec make_rtc_spec(const HostFeeder &h, int tile, int nt, int maxt) {
     sp.n_taps = h.n_taps;
     sp.nt = nt;
     sp.maxt = maxt;
-    sp.min_waves = maxt == 1 ? 4 : 2;
+    sp.min_waves = std::max(1, 4 * 256 / nt);   // <= 128 VGPRs: 4 waves per SIMD
+    if (const char *g = getenv("FPF_RTC_GEOM")) {
+        int n = 0, m = 0, w = 0;
+        if (sscanf(g, "%d,%d,%d", &n, &m, &w) == 3 && w >= 1 && w <= 8) sp.min_waves = w;
+    }
     for (const auto &op : h.bwi) sp.bw.push_back({op.k, op.a, op.p});
     for (const auto &op : h.fwi) sp.fw.push_back({op.dst, op.src, op.mask});
     return sp;
@@ -542,9 +546,10 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     (void)choose_tile(h, o, &rtc_nt, &rtc_maxt);
     // an explicit tile above the default geometry takes more tasks per lane
     while (rtc_nt > 0 && rtc_maxt < 4 && tile * (h.nn - 1) > rtc_nt * rtc_maxt) ++rtc_maxt;
+    while (rtc_nt > 256 && tile * (h.nn - 1) <= (rtc_nt / 2) * rtc_maxt) rtc_nt /= 2;
     if (kern == FPF_KERNEL_TILED && wants_rtc(h, o) && rtc_nt > 0 && tile * (h.nn - 1) <= rtc_nt * rtc_maxt) {
         const RtcSpec sp = make_rtc_spec(h, tile, rtc_nt, rtc_maxt);
-        if (tiled_lds_bytes_rtc(d, tile) <= 64 * 1024) {
+        if (tiled_lds_bytes_rtc(d, tile) <= 160 * 1024) {
             std::string err;
             if (rtc_build(ctx->device, sp, &f->rtc_kernel, &err) == 0) {
                 f->rtc = true;

@@ -172,6 +172,8 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
         return -1;
     }
     k.nt = sp.nt;
+    // dynamic LDS above the default 64 KiB (gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     g_cache[key] = k;
     *out = k;
     return 0;

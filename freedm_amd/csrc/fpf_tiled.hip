@@ -4,6 +4,9 @@
 // (fpf_rtc.cpp); this one runs any well-formed feeder that fits in LDS.
 #include "fpf_tiled_body.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace fpf {
 
 template <int NT>
@@ -40,19 +43,31 @@ namespace {
 int threads_for(const FeederDev &f, int tile) { return tiled_threads(f, tile); }
 }  // namespace
 
-// The specialised build keeps one task per lane in 512-thread workgroups capped
-// at 128 VGPRs, so two workgroups (tiles) share a CU and one's sequential
-// stages overlap the other's parallel stages.
+// Geometry of the specialised build.  The sequential stages cost ~45 cycles per
+// row per wave whatever the number of active lanes (each LDS wave-instruction
+// has a fixed issue cost), so one sequential wave should carry as many
+// scenarios as possible: up to 16 scenarios (48 lanes) per workgroup, two tasks
+// per lane, 1024 threads at <= 128 VGPRs -- one workgroup per CU, and a
+// 4096-scenario batch is exactly one wave of workgroups on 256 CUs.
 int rtc_tile(const FeederDev &f, int *nt, int *maxt) {
     const int nb = f.nn - 1;
-    int t = std::min(MAX_SEQ_TILE, 512 / nb);
-    *nt = 512;
-    *maxt = 1;
-    if (t == 0) {
-        t = std::min(MAX_SEQ_TILE, 1024 / nb);
-        *maxt = 2;
+    int m = 2, n = 1024;
+    int t = std::min(MAX_SEQ_TILE, n * m / nb);
+    if (t == 0) return 0;
+    // diagnostic override of the geometry: FPF_RTC_GEOM="nt,maxt[,min_waves]"
+    if (const char *g = getenv("FPF_RTC_GEOM")) {
+        int gn = 0, gm = 0;
+        if (sscanf(g, "%d,%d", &gn, &gm) == 2 && (gn == 256 || gn == 512 || gn == 1024) && gm >= 1 && gm <= 4) {
+            n = gn;
+            m = gm;
+            t = std::min(MAX_SEQ_TILE, n * m / nb);
+        }
     }
-    while (t > 0 && tiled_lds_bytes_rtc(f, t) > 64 * 1024) --t;
+    while (t > 0 && tiled_lds_bytes_rtc(f, t) > 160 * 1024) --t;
+    // small feeders: the fewest threads that hold the tile's tasks
+    while (n > 256 && t * nb <= (n / 2) * m) n /= 2;
+    *nt = n;
+    *maxt = m;
     return t;
 }
 
