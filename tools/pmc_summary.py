@@ -1,0 +1,63 @@
+"""Summarise a gpu_profile.sh run into profiles/<tag>/:
+
+    python tools/pmc_summary.py <tag> [kernel-name-substring]
+
+Copies the rocprofv3 kernel stats, and turns the separate FETCH_SIZE and
+WRITE_SIZE passes into per-launch HBM bytes of the dominant kernel, corrected
+as MI355X_MICROARCH.md section HBM prescribes: FETCH_SIZE (KiB) reports half
+the bytes of a wide coalesced read on gfx950, so it is doubled; WRITE_SIZE
+(KiB) is taken as is.  Writes profiles/<tag>/pmc.json and refreshes
+profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, counter, kname):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter and kname in row["Kernel_Name"]:
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    tag = sys.argv[1]
+    kname = sys.argv[2] if len(sys.argv) > 2 else "fpf_rtc_tiled"
+    out = os.path.join(ROOT, "gpurun_out")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(out, f"prof_{tag}", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    bench = [ln for ln in open(os.path.join(out, f"prof_{tag}_bench.log")) if ln.startswith("{")]
+    fetch = per_launch(os.path.join(out, f"pmc_{tag}_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE", kname)
+    write = per_launch(os.path.join(out, f"pmc_{tag}_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE", kname)
+    b = json.loads(bench[-1]) if bench else {}
+    fk = sum(fetch) / len(fetch)
+    wk = sum(write) / len(write)
+    hbm = (2 * fk + wk) * 1024
+    with open(os.path.join(dst, "kernel_stats.csv")) as f:
+        avg_ns = next(float(r["AverageNs"]) for r in csv.DictReader(f) if kname in r["Name"])
+    scen = b.get("config", {}).get("scenarios_per_gpu")
+    res = {
+        "tag": tag, "kernel": kname, "launches_fetch": len(fetch), "launches_write": len(write),
+        "FETCH_SIZE_KiB_per_launch": fk, "WRITE_SIZE_KiB_per_launch": wk,
+        "hbm_bytes_per_launch": hbm, "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
+        "rocprof_avg_kernel_ns": avg_ns, "bench_kernel_ms": b.get("roofline", {}).get("kernel_ms"),
+        "bytes_alg_per_launch": (b.get("roofline", {}).get("bytes_alg_per_scenario") or 0) * (scen or 0),
+        "workload": f"123-bus x {scen}",
+        "bench_line": b,
+    }
+    json.dump(res, open(os.path.join(dst, "pmc.json"), "w"), indent=1)
+    json.dump({k: res[k] for k in ("tag", "kernel", "hbm_bytes_per_launch", "workload", "rocprof_avg_kernel_ns")},
+              open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "bench_line"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
