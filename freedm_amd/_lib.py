@@ -20,7 +20,8 @@ KERNELS = {"auto": FPF_KERNEL_AUTO, "generic": FPF_KERNEL_GENERIC, "tiled": FPF_
 
 EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_destroy", "fpf_last_error",
            "fpf_feeder_create", "fpf_feeder_destroy", "fpf_feeder_get_info", "fpf_feeder_reserve",
-           "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source"]
+           "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source",
+           "fpf_selftest_division"]
 
 
 class FpfOpts(C.Structure):
@@ -103,6 +104,8 @@ def load(path: str | None = None):
     L.fpf_feeder_rtc_source.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
                                         C.c_char_p, C.c_size_t]
     L.fpf_feeder_rtc_source.restype = C.c_long
+    L.fpf_selftest_division.argtypes = [C.c_int, C.c_long, C.c_ulong]
+    L.fpf_selftest_division.restype = C.c_long
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
                  "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device"):
         getattr(L, name).restype = C.c_int

@@ -54,7 +54,10 @@ struct fpf_feeder {
     double *d_agg = nullptr;
     // topology-specialised tiled kernel (hipRTC), if built
     bool rtc = false;
-    RtcKernel rtc_kernel{};
+    RtcKernel rtc_kernel{};      // without the PQb output (no Ib kept in registers)
+    RtcKernel rtc_kernel_ib{};   // with PQb: built on the first solve that asks for it
+    bool rtc_ib = false;
+    RtcSpec rtc_spec;
 };
 
 static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
@@ -136,6 +139,8 @@ struct HostFeeder {
     std::vector<SeqBw> seq_bw;
     std::vector<SeqFw> seq_fw;
     int n_taps = 0, depth = 0;
+    TrackSched ts;                 // multi-track schedule of the specialised kernel
+    std::vector<NodeOp> node_rtc;  // node table with the schedule's slots
     double at(int i, int j) const { return dl[(size_t)i + (size_t)j * nl]; }
 };
 
@@ -281,7 +286,8 @@ std::string build_lnum(HostFeeder &h, const double *z, int z_rows, const fpf_opt
 void analyse_tiled(HostFeeder &h) {
     const int nl = h.nl, nn = h.nn;
     auto no = [&](const std::string &why) { h.wf = false; h.wf_why = why; };
-    h.node.assign(nn, NodeOp{-1, -1, -1, 0, -1});
+    h.node.assign(nn, NodeOp{-1, -1, -1, 0, -1, 0, {0, 0}});
+    for (int k = 0; k < nn; ++k) h.node[k].slot = k;   // interpreted layout: slot k = node k
     if (nn > 8192) return no("more than 8192 nodes");
     std::vector<int> row_of(nn, -1);
     std::vector<int> seen(nn, 0);
@@ -398,39 +404,303 @@ bool wants_rtc(const HostFeeder &h, const fpf_opts &o) {
            h.bwi.size() <= max_ops;
 }
 
-// tile for the tiled kernel; *nt / *maxt describe the specialised build's geometry
-int choose_tile(const HostFeeder &h, const fpf_opts &o, int *nt = nullptr, int *maxt = nullptr) {
-    if (!h.wf) return 0;
-    FeederDev probe{};
-    probe.nn = h.nn;
-    probe.n_taps = h.n_taps;
-    int tmax, n = 0, m = 0;
-    if (wants_rtc(h, o)) {
-        tmax = rtc_tile(probe, &n, &m);
-        if (tmax < 1) tmax = tiled_max_tile(probe);
-    } else {
-        tmax = tiled_max_tile(probe);
+// Multi-track list schedule of the sequential stages (fpf_internal.h: TrackSched).
+// Units are the feeder's blocks (Dl row runs between separator rows), each on
+// consecutive steps of one track.  Node v must come at least one step (D for
+// a fully prefetched LDS read) after node u for every cross-block dependency
+// u -> v: the forward source of a row that is not its block predecessor
+// (DPF_return7.cpp:176-178) and, backward, a tap before the first node of each
+// child block (the separator's Ib(sbus(m+1)) += Ibl, :138-146).  Blocks are
+// placed highest bottom-level first on the track where they can start earliest.
+TrackSched schedule_tracks(const HostFeeder &h, int T, int D) {
+    const int nl = h.nl, nn = h.nn;
+    TrackSched ts;
+    ts.T = T;
+    ts.fw_src.assign(nn, 0);
+    ts.fw_mask.assign(nn, 0);
+    ts.children.assign(nn, {});
+    ts.bw_reset.assign(nn, 0);
+    std::vector<std::vector<int>> blk(1);
+    std::vector<int> blk_of(nn, -1), pos(nn, -1);
+    for (int m = 0; m < nl; ++m) {
+        if (h.at(m, 0) == 0) {
+            if (!blk.back().empty()) blk.emplace_back();
+            continue;
+        }
+        const int k = (int)h.at(m, 2);
+        blk_of[k] = (int)blk.size() - 1;
+        pos[k] = (int)blk.back().size();
+        blk.back().push_back(k);
+        ts.fw_src[k] = m == 0 ? 0 : (int)h.at(m, 1);   // row 0 reads V0 (:168)
+        ts.fw_mask[k] = h.node[k].mask;
     }
-    if (nt) *nt = n;
-    if (maxt) *maxt = m;
-    return o.tile > 0 ? std::min(o.tile, tmax) : tmax;
+    if (blk.back().empty()) blk.pop_back();
+    const int nb = (int)blk.size();
+    // children in the backward accumulation order: descending separator row
+    for (int m = nl - 1; m >= 0; --m)
+        if (h.at(m, 0) == 0) ts.children[(int)h.at(m + 1, 1)].push_back((int)h.at(m + 1, 2));
+    for (const auto &b : blk) ts.bw_reset[b.back()] = 1;
+    // cross-block dependencies u -> v
+    std::vector<std::vector<int>> dep_in(nn), dep_out(nn);
+    for (int b = 0; b < nb; ++b)
+        for (size_t i = 0; i < blk[b].size(); ++i) {
+            const int k = blk[b][i], src = ts.fw_src[k];
+            if (src != 0 && !(i > 0 && blk[b][i - 1] == src)) { dep_in[k].push_back(src); dep_out[src].push_back(k); }
+        }
+    for (int k = 1; k < nn; ++k)
+        for (int c : ts.children[k]) { dep_in[c].push_back(k); dep_out[k].push_back(c); }
+    // bottom levels (deps always point to later rows, so reverse row order works)
+    std::vector<int> bl(nn, 1);
+    for (int b = nb - 1; b >= 0; --b)
+        for (int i = (int)blk[b].size() - 1; i >= 0; --i) {
+            const int k = blk[b][i];
+            int v = 1 + ((size_t)i + 1 < blk[b].size() ? bl[blk[b][i + 1]] : 0);
+            for (int w : dep_out[k]) v = std::max(v, D + bl[w]);
+            bl[k] = v;
+        }
+    std::vector<std::vector<int>> pred(nb);
+    for (int b = 0; b < nb; ++b)
+        for (int k : blk[b])
+            for (int u : dep_in[k])
+                if (blk_of[u] != b) pred[b].push_back(blk_of[u]);
+    std::vector<int> free(T, 0);
+    std::vector<char> done(nb, 0);
+    ts.step.assign(nn, -1);
+    ts.track.assign(nn, -1);
+    for (int n = 0; n < nb; ++n) {
+        int best = -1;
+        for (int b = 0; b < nb; ++b) {
+            if (done[b]) continue;
+            bool ready = true;
+            for (int p : pred[b]) ready = ready && done[p];
+            if (ready && (best < 0 || bl[blk[b][0]] > bl[blk[best][0]])) best = b;
+        }
+        int est = 0;
+        for (size_t i = 0; i < blk[best].size(); ++i)
+            for (int u : dep_in[blk[best][i]])
+                if (blk_of[u] != best) est = std::max(est, ts.step[u] + std::max(D, 1) - (int)i);
+        int bt = 0, bs = INT32_MAX;
+        for (int t = 0; t < T; ++t) {
+            const int st = std::max(free[t], est);
+            if (st < bs) { bs = st; bt = t; }
+        }
+        if (best == 0) { bt = 0; bs = 0; }   // node 1 (row 0) first, on track 0
+        for (size_t i = 0; i < blk[best].size(); ++i) {
+            ts.step[blk[best][i]] = bs + (int)i;
+            ts.track[blk[best][i]] = bt;
+        }
+        free[bt] = bs + (int)blk[best].size();
+        done[best] = 1;
+    }
+    ts.S = *std::max_element(free.begin(), free.end());
+    ts.cell.assign((size_t)ts.S * T, -1);
+    for (int k = 1; k < nn; ++k) ts.cell[(size_t)ts.step[k] * T + ts.track[k]] = k;
+    ts.n_slots = T + ts.S * T + T;
+    return ts;
 }
 
-RtcSpec make_rtc_spec(const HostFeeder &h, int tile, int nt, int maxt) {
+// Comb packing of the schedule's cells into LDS slots: step s gets the lowest
+// base b >= T such that b + t is free for every track t active at s.  A track
+// idle at s then points at a slot that may belong to another step -- it reads
+// there but never stores (fpf_rtc.cpp).  Slots 0..T-1 hold V0 (any track reads
+// it at offset 0), so node slots start at T and cross-track reads at
+// slot - t never go negative.
+void pack_slots(TrackSched &ts, int nn) {
+    const int T = ts.T, S = ts.S;
+    ts.base.assign(S, T);
+    ts.active.assign(S, 0u);
+    ts.slot_of.assign(nn, 0);
+    std::vector<char> used((size_t)T + (size_t)S * T + 2 * T, 0);
+    int hi = T - 1, lo = T;
+    for (int s = 0; s < S; ++s) {
+        unsigned act = 0;
+        for (int t = 0; t < T; ++t)
+            if (ts.cell[(size_t)s * T + t] >= 0) act |= 1u << t;
+        ts.active[s] = act;
+        while (used[lo]) ++lo;
+        int b = lo;
+        for (;; ++b) {
+            bool ok = true;
+            for (int t = 0; t < T && ok; ++t)
+                if (((act >> t) & 1) && used[(size_t)b + t]) ok = false;
+            if (ok) break;
+        }
+        ts.base[s] = b;
+        for (int t = 0; t < T; ++t)
+            if ((act >> t) & 1) {
+                used[(size_t)b + t] = 1;
+                ts.slot_of[ts.cell[(size_t)s * T + t]] = b + t;
+                hi = std::max(hi, b + t);
+            }
+    }
+    ts.n_slots = std::max(hi + 1, *std::max_element(ts.base.begin(), ts.base.end()) + T) + T;
+}
+
+// LDS bank model of the state layout (MI355X_MICROARCH.md, LDS table): element
+// (slot j, phase p, scenario s) sits at 16-byte unit j*SL + p*PS + s.  A
+// ds_read_b128 serves four 16-lane groups and is conflict-free when a group's
+// lanes hit distinct units mod 16; ds_write_b128 serves eight 8-lane groups,
+// distinct mod 8.  Returns the worst multiplicity over the groups.
+int bank_degree(const int units[64], bool write) {
+    static const int rg[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                  {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                  {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                  {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+    int worst = 1;
+    const int ng = write ? 8 : 4, gs = write ? 8 : 16, mod = write ? 8 : 16;
+    for (int g = 0; g < ng; ++g) {
+        int cnt[16] = {0};
+        for (int i = 0; i < gs; ++i) {
+            const int ln = write ? g * 8 + i : rg[g][i];
+            if (units[ln] < 0) continue;
+            worst = std::max(worst, ++cnt[units[ln] % mod]);
+        }
+    }
+    return worst;
+}
+
+struct BankLayout { int ps = 0, sl = 0, s_deg = 99, p_deg = 99; };
+
+// Phase stride PS >= tile and slot stride SL >= 3*PS (16-byte units) that make
+// the sequential lanes (phase p, track t, scenario s -> lane (p*T + t)*NS + s,
+// at comb offsets base + t) conflict-free, then the parallel lanes (16
+// scenarios of each of 4 nodes per wave), then the least padding.
+BankLayout bank_layout(int T, int NS, int tile) {
+    BankLayout best;
+    int units[64];
+    for (int ps = tile; ps <= tile + 8; ++ps)
+        for (int sl = 3 * ps; sl <= 3 * ps + 16; ++sl) {
+            int sd = 1;
+            for (int wv = 0; wv < 2; ++wv)
+                for (int base = 0; base < 4; ++base)
+                    for (int w = 0; w < 2; ++w) {
+                        std::fill(units, units + 64, -1);
+                        for (int p = 0; p < 3; ++p)
+                            for (int t = 0; t < T; ++t)
+                                for (int q = 0; q < NS; ++q)
+                                    units[(p * T + t) * NS + q] = (base + t) * sl + p * ps + wv * NS + q;
+                        sd = std::max(sd, bank_degree(units, w == 1));
+                    }
+            int pd = 1;
+            static const int nodes[3][4] = {{0, 1, 2, 3}, {5, 9, 2, 7}, {3, 10, 17, 24}};
+            for (const auto &nd : nodes)
+                for (int p = 0; p < 3; ++p) {
+                    for (int ln = 0; ln < 64; ++ln) {
+                        const int k = ln / tile, q = ln % tile;
+                        units[ln] = k < 4 ? nd[k] * sl + p * ps + q : -1;
+                    }
+                    pd = std::max(pd, bank_degree(units, false));
+                }
+            if (sd < best.s_deg || (sd == best.s_deg && (pd < best.p_deg || (pd == best.p_deg && sl < best.sl)))) {
+                best.ps = ps;
+                best.sl = sl;
+                best.s_deg = sd;
+                best.p_deg = pd;
+            }
+        }
+    return best;
+}
+
+// The specialised kernel's plan: tile, tracks, scenarios per sequential wave,
+// layout.  Largest tile whose tasks fit 1024 lanes x 2 and whose state fits
+// LDS; among (T, NS) for that tile the lowest estimated sequential-stage time
+// (steps x bank-conflict degree, sequential waves spread over the 4 SIMDs).
+struct RtcPlan {
+    TrackSched ts;
+    int tile = 0, ns = 0, nt = 0, maxt = 0;
+    BankLayout lay;
+};
+
+constexpr int MAX_TILE = 16;   // = MAX_SEQ_TILE of fpf_tiled_body.h (flag arrays)
+
+bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
+    int force_t = 0;
+    if (const char *e = getenv("FPF_RTC_TRACKS")) force_t = atoi(e);
+    std::vector<TrackSched> by_t(5);
+    for (int T = 1; T <= 4; ++T) {
+        if (force_t && T != force_t) continue;
+        for (int D = 1; D <= 4; ++D) {
+            TrackSched s = schedule_tracks(h, T, T == 1 ? 1 : D);
+            if (by_t[T].S == 0 || s.S <= by_t[T].S) by_t[T] = std::move(s);
+            if (T == 1) break;
+        }
+        pack_slots(by_t[T], h.nn);
+    }
+    const int nb = h.nn - 1;
+    int tmax = std::min(MAX_TILE, (1024 * 2) / std::max(nb, 1));
+    if (o.tile > 0) tmax = std::min(tmax, o.tile);
+    for (int tile = tmax; tile >= 1; --tile) {
+        double best_cost = 1e30;
+        for (int T = 1; T <= 4; ++T) {
+            if (by_t[T].S == 0) continue;
+            const int nsmax = std::min(21, 64 / (3 * T));
+            int tried = 0;
+            for (int w = 1; w <= 4; ++w) {
+                const int ns = (tile + w - 1) / w;   // NS scenarios per sequential wave, w waves
+                if (ns > nsmax || ns == tried) continue;
+                tried = ns;
+                const BankLayout lay = bank_layout(T, ns, tile);
+                FeederDev probe{};
+                probe.n_slots = by_t[T].n_slots;
+                probe.slot_bytes = lay.sl * 16;
+                if (tiled_lds_bytes_rtc(probe, tile) > 160 * 1024) continue;
+                const int nws = (tile + ns - 1) / ns;
+                const double cost = by_t[T].S * (double)std::max(lay.s_deg, 1) * (nws > 4 ? (nws + 3) / 4 : 1) +
+                                    0.01 * T + 0.001 * nws;
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    out->ts = by_t[T];
+                    out->tile = tile;
+                    out->ns = ns;
+                    out->lay = lay;
+                }
+            }
+        }
+        if (best_cost < 1e30) {
+            int n = 1024, m = 2;
+            if (const char *g = getenv("FPF_RTC_GEOM")) {
+                int gn = 0, gm = 0;
+                if (sscanf(g, "%d,%d", &gn, &gm) == 2 && (gn == 256 || gn == 512 || gn == 1024) && gm >= 1 && gm <= 4) {
+                    n = gn;
+                    m = gm;
+                }
+            }
+            while (m < 4 && tile * nb > n * m) ++m;
+            while (n > 256 && tile * nb <= (n / 2) * m) n /= 2;
+            if (tile * nb > n * m || (tile + out->ns - 1) / out->ns > n / 64) continue;
+            out->nt = n;
+            out->maxt = m;
+            return true;
+        }
+    }
+    return false;
+}
+
+RtcSpec make_rtc_spec(const HostFeeder &h, const RtcPlan &pl) {
     RtcSpec sp;
-    sp.tile = tile;
+    sp.tile = pl.tile;
     sp.nn = h.nn;
     sp.n_taps = h.n_taps;
-    sp.nt = nt;
-    sp.maxt = maxt;
-    sp.min_waves = std::max(1, 4 * 256 / nt);   // <= 128 VGPRs: 4 waves per SIMD
+    sp.nt = pl.nt;
+    sp.maxt = pl.maxt;
+    sp.min_waves = std::max(1, 4 * 256 / pl.nt);   // <= 128 VGPRs: 4 waves per SIMD
     if (const char *g = getenv("FPF_RTC_GEOM")) {
         int n = 0, m = 0, w = 0;
         if (sscanf(g, "%d,%d,%d", &n, &m, &w) == 3 && w >= 1 && w <= 8) sp.min_waves = w;
     }
-    for (const auto &op : h.bwi) sp.bw.push_back({op.k, op.a, op.p});
-    for (const auto &op : h.fwi) sp.fw.push_back({op.dst, op.src, op.mask});
+    if (const char *a = getenv("FPF_RTC_AHEAD")) sp.ahead = std::max(1, atoi(a));
+    sp.ts = pl.ts;
+    sp.ns = pl.ns;
+    sp.ps = pl.lay.ps;
+    sp.slot = pl.lay.sl;
     return sp;
+}
+
+// the node table of the specialised layout
+std::vector<NodeOp> node_table_rtc(const HostFeeder &h, const TrackSched &ts) {
+    std::vector<NodeOp> v = h.node;
+    for (int k = 0; k < h.nn; ++k) v[k].slot = ts.slot(k);
+    return v;
 }
 
 template <class T>
@@ -461,6 +731,12 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     if (why.empty()) why = build_lnum(h, z, z_rows, o);
     if (!why.empty()) return fail(ctx, FPF_ERR_TOPOLOGY, "feeder rejected (the reference would throw): " + why);
     analyse_tiled(h);
+    RtcPlan plan;
+    const bool have_plan = wants_rtc(h, o) && plan_rtc(h, o, &plan);
+    if (have_plan) {
+        h.ts = plan.ts;
+        h.node_rtc = node_table_rtc(h, plan.ts);
+    }
 
     fpf_feeder *f = new fpf_feeder();
     f->ctx = ctx;
@@ -477,8 +753,15 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     for (int p = 0; p < 3; ++p) in.lnum[p] = h.lnum[p];
     in.depth = h.depth;
 
-    // tile of the tiled kernel (the sequential programs are built for it)
-    const int tile = choose_tile(h, o);
+    // tile of the interpreted tiled kernel (its sequential programs are built for it)
+    int tile = 0;
+    if (h.wf) {
+        FeederDev probe{};
+        probe.nn = h.nn;
+        probe.n_taps = h.n_taps;
+        tile = tiled_max_tile(probe);
+        if (o.tile > 0) tile = std::min(tile, o.tile);
+    }
     if (tile >= 1) build_seq_programs(h, tile);
     // upload all tables as one blob
     std::vector<char> blob;
@@ -487,6 +770,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     const size_t o_bw = push_blob(blob, h.bw);
     const size_t o_fw = push_blob(blob, h.fw);
     const size_t o_node = push_blob(blob, h.node);
+    const size_t o_node_rtc = push_blob(blob, h.node_rtc);
     const size_t o_sbw = push_blob(blob, h.seq_bw);
     const size_t o_sfw = push_blob(blob, h.seq_fw);
     hipError_t e = hipSetDevice(ctx->device);
@@ -534,30 +818,35 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
 
     // kernel choice
     int kern = o.kernel;
-    if (kern == FPF_KERNEL_AUTO) kern = (h.wf && tile >= 1) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
-    if (kern == FPF_KERNEL_TILED && (!h.wf || tile < 1)) {
+    if (kern == FPF_KERNEL_AUTO) kern = (h.wf && (tile >= 1 || have_plan)) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
+    if (kern == FPF_KERNEL_TILED && (!h.wf || (tile < 1 && !have_plan))) {
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_UNSUPPORTED,
                     "tiled kernel needs a well-formed feeder that fits in LDS: " + (h.wf ? std::string("too large") : h.wf_why));
     }
     in.kernel = kern;
-    in.tile = kern == FPF_KERNEL_TILED ? tile : 0;
-    int rtc_nt = 0, rtc_maxt = 0;
-    (void)choose_tile(h, o, &rtc_nt, &rtc_maxt);
-    // an explicit tile above the default geometry takes more tasks per lane
-    while (rtc_nt > 0 && rtc_maxt < 4 && tile * (h.nn - 1) > rtc_nt * rtc_maxt) ++rtc_maxt;
-    while (rtc_nt > 256 && tile * (h.nn - 1) <= (rtc_nt / 2) * rtc_maxt) rtc_nt /= 2;
-    if (kern == FPF_KERNEL_TILED && wants_rtc(h, o) && rtc_nt > 0 && tile * (h.nn - 1) <= rtc_nt * rtc_maxt) {
-        const RtcSpec sp = make_rtc_spec(h, tile, rtc_nt, rtc_maxt);
-        if (tiled_lds_bytes_rtc(d, tile) <= 160 * 1024) {
-            std::string err;
-            if (rtc_build(ctx->device, sp, &f->rtc_kernel, &err) == 0) {
-                f->rtc = true;
-            } else {
-                ctx->err = err;   // not fatal: the interpreted tiled kernel runs instead
-            }
+    if (kern == FPF_KERNEL_TILED && have_plan) {
+        const RtcSpec sp = make_rtc_spec(h, plan);
+        std::string err;
+        RtcSpec sp0 = sp;
+        sp0.keep_ib = false;
+        if (rtc_build(ctx->device, sp0, &f->rtc_kernel, &err) == 0) {
+            f->rtc = true;
+            f->rtc_spec = sp;
+            d.node_ops = (const NodeOp *)(base + o_node_rtc);   // the schedule's slots
+            d.tile = plan.tile;
+            d.n_slots = plan.ts.n_slots;
+            d.slot_bytes = plan.lay.sl * 16;
+            d.phase_bytes = plan.lay.ps * 16;
+        } else {
+            ctx->err = err;   // not fatal: the interpreted tiled kernel runs instead
         }
     }
+    if (kern == FPF_KERNEL_TILED && !f->rtc && tile < 1) {
+        fpf_feeder_destroy(f);
+        return fail(ctx, FPF_ERR_UNSUPPORTED, "specialised kernel failed and the interpreted one does not fit: " + ctx->err);
+    }
+    in.tile = kern == FPF_KERNEL_TILED ? d.tile : 0;
     in.specialized = f->rtc ? 1 : 0;
     *out = f;
     return FPF_OK;
@@ -640,7 +929,14 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     o.vmax = u.vmax ? u.vmax : f->d_vmax;
     hipError_t e;
     if (f->info.kernel == FPF_KERNEL_TILED) {
-        e = f->rtc ? rtc_launch(f->rtc_kernel, f->dev, n_scen, d_pq, o, st) : launch_tiled(f->dev, n_scen, d_pq, o, st);
+        if (f->rtc && o.pqb && !f->rtc_ib) {
+            std::string err;
+            if (rtc_build(ctx->device, f->rtc_spec, &f->rtc_kernel_ib, &err) != 0)
+                return fail(ctx, FPF_ERR_HIP, "hipRTC build of the PQb variant: " + err);
+            f->rtc_ib = true;
+        }
+        e = f->rtc ? rtc_launch(o.pqb ? f->rtc_kernel_ib : f->rtc_kernel, f->dev, n_scen, d_pq, o, st)
+                   : launch_tiled(f->dev, n_scen, d_pq, o, st);
     } else {
         if (!f->d_scratch || f->scratch_ld < (size_t)n_scen) {
             int rc = fpf_feeder_reserve(f, n_scen);
@@ -742,15 +1038,12 @@ extern "C" long fpf_feeder_rtc_source(const double *dl, int nl, int ncols, const
     if (why.empty()) why = build_lnum(h, z, z_rows, o);
     if (!why.empty()) return FPF_ERR_TOPOLOGY;
     analyse_tiled(h);
-    const int tile = choose_tile(h, o);
-    if (tile < 1) return FPF_ERR_UNSUPPORTED;
-    FeederDev d{};
-    d.nn = h.nn;
-    d.n_taps = h.n_taps;
-    int nt = 0, maxt = 0;
-    (void)choose_tile(h, o, &nt, &maxt);
-    if (nt == 0) return FPF_ERR_UNSUPPORTED;
-    const std::string src = rtc_source(make_rtc_spec(h, tile, nt, maxt));
+    RtcPlan plan;
+    if (!wants_rtc(h, o) || !plan_rtc(h, o, &plan)) return FPF_ERR_UNSUPPORTED;
+    RtcSpec sp = make_rtc_spec(h, plan);
+    const char *kib = getenv("FPF_RTC_KEEP_IB");
+    sp.keep_ib = kib && atoi(kib);   // default: the variant solves without PQb run
+    const std::string src = rtc_source(sp);
     if (buf && buf_size > 0) {
         const size_t n = std::min(buf_size - 1, src.size());
         std::memcpy(buf, src.data(), n);

@@ -49,6 +49,9 @@ struct NodeOp {
     int32_t code;    // 0-based line code
     int32_t mask;    // phase-zeroing bits (0 for the special first branch)
     int32_t tap;     // tap-accumulator slot, -1 if no separator targets k
+    int32_t slot;    // LDS state slot of node k (k itself in the interpreted layout,
+                     // its schedule cell in the multi-track layout of fpf_rtc.cpp)
+    int32_t pad[2];
 };
 
 // Sequential-stage programs of the tiled kernel, built for one tile size (LDS
@@ -95,6 +98,9 @@ struct FeederDev {
     int32_t n_seq_bw, n_seq_fw;
     int32_t tile;            // tile the programs were built for
     int32_t prog_lds;        // 1: stage the programs in LDS; 0: read them from global memory
+    int32_t n_slots;         // LDS state slots of the specialised (multi-track) layout
+    int32_t slot_bytes;      // bytes per state slot of the specialised layout (padded, see fpf_api.cpp: bank_layout)
+    int32_t phase_bytes;     // bytes between the phases of one slot (specialised layout)
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -117,15 +123,39 @@ size_t tiled_lds_bytes(const FeederDev &f, int tile);
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile);
 int tiled_max_tile(const FeederDev &f);
 int tiled_threads(const FeederDev &f, int tile);
-int rtc_tile(const FeederDev &f, int *nt, int *maxt);
+
+// Multi-track schedule of the sequential stages (fpf_api.cpp: schedule_tracks).
+// The feeder's blocks (Dl row runs between separator rows) are list-scheduled
+// onto T tracks; each block occupies consecutive steps of one track.  Forward
+// runs steps 0..S-1, backward the same cells in reverse, so a cell's LDS slot
+// serves both.  Node k scheduled at (step s, track t) lives in slot
+// base[s] + t (pack_slots): every track finds its cell of step s at the same
+// offset from its own base, and the combs of different steps interleave.
+// Slots 0..T-1 hold V0; T more pad the end.
+struct TrackSched {
+    int T = 1, S = 0, n_slots = 0;
+    std::vector<int> cell;                 // [S*T] node or -1
+    std::vector<int> step, track;          // [nn] of each node (node 0: -1)
+    std::vector<int> base;                 // [S] slot of track 0's cell at step s
+    std::vector<unsigned> active;          // [S] bit t: track t has a node at step s
+    std::vector<int> slot_of;              // [nn] state slot of each node (node 0: 0)
+    std::vector<int> fw_src;               // [nn] forward source node (0 = V0)
+    std::vector<int> fw_mask;              // [nn] phase-zeroing bits
+    std::vector<std::vector<int>> children;// [nn] first nodes of the child blocks, in accumulation order
+    std::vector<char> bw_reset;            // [nn] Ibl = 0 before this node's backward op
+    int slot(int k) const { return k == 0 ? 0 : slot_of[k]; }
+};
 
 // topology-specialised tiled kernel (fpf_rtc.cpp)
 struct RtcSpec {
     int tile, nn, n_taps, nt;
     int maxt = 1;                         // tasks per lane
     int min_waves = 4;                    // __launch_bounds__ minimum waves per SIMD
-    std::vector<std::array<int, 3>> bw;   // backward ops: node, tap read (-1), separator target (-1)
-    std::vector<std::array<int, 3>> fw;   // forward ops: dst, src, zero mask
+    int ahead = 8;                        // LDS operand lookahead of the sequential stages (steps)
+    int ns = 21;                          // scenarios per sequential wave (3*T*ns <= 64)
+    int ps = 0, slot = 0;                 // phase / slot strides of the state layout (16-byte units)
+    bool keep_ib = true;                  // keep the last sweep's Ib for the PQb output
+    TrackSched ts;
 };
 struct RtcKernel {
     hipModule_t mod;

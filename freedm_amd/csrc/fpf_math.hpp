@@ -43,6 +43,60 @@ __host__ __device__ __forceinline__ cx cdiv(cx x, cx y) {
     return r;
 }
 
+// ---- correctly rounded fp64 division with a shared reciprocal ----------------
+// hipcc lowers a / b to div_scale(b), rcp, two Newton steps, q = a*y,
+// r = fma(-b, q, a), div_fmas(r, y, q), div_fixup.  When every operand is zero
+// or has an exponent in [-300, 300], div_scale scales nothing, div_fmas is the
+// plain fma and div_fixup returns its input except for a zero numerator (the
+// signed zero a*y), so dv_div below yields the same bits as a / b -- and one
+// reciprocal serves both quotients of Smith's method.  cdiv_rr is __divdc3 on
+// that division; callers guard its range with dv_in_range (checked on the GPU
+// against a / b bit for bit, tests/test_gpu_parity.py).
+__host__ __device__ __forceinline__ bool dv_in_range(double x) {
+    const double ax = fabs(x);
+    return ax == 0.0 || (ax >= 0x1p-300 && ax <= 0x1p300);
+}
+__host__ __device__ __forceinline__ double dv_rcp(double b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    double y = __builtin_amdgcn_rcp(b);
+#else
+    double y = 1.0 / b;
+#endif
+    double e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-b, y, 1.0);
+    return fma(y, e, y);
+}
+__host__ __device__ __forceinline__ double dv_div(double a, double b, double y) {
+    const double q = a * y;
+    const double r = fma(-b, q, a);
+    const double d = fma(r, y, q);
+    return a == 0.0 ? q : d;
+}
+__host__ __device__ __forceinline__ cx cdiv_rr(cx x, cx y) {
+    const double a = x.re, b = x.im, c = y.re, d = y.im;
+    cx r;
+    if (fabs(c) < fabs(d)) {
+        const double ratio = dv_div(c, d, dv_rcp(d));
+        const double denom = (c * ratio) + d;
+        const double yr = dv_rcp(denom);
+        r.re = dv_div((a * ratio) + b, denom, yr);
+        r.im = dv_div((b * ratio) - a, denom, yr);
+    } else {
+        const double ratio = dv_div(d, c, dv_rcp(c));
+        const double denom = (d * ratio) + c;
+        const double yr = dv_rcp(denom);
+        r.re = dv_div((b * ratio) + a, denom, yr);
+        r.im = dv_div(b - (a * ratio), denom, yr);
+    }
+    return r;
+}
+// load current with the shared-reciprocal division; valid when Sld and V are in range
+__host__ __device__ __forceinline__ cx load_current_rr(cx s, cx v) {
+    if (v.re == 0.0 && v.im == 0.0) return mk(0.0, 0.0);
+    return cconj(cdiv_rr(s, v));
+}
+
 // Load current of one phase, DPF_return7.cpp:117-125:
 //   abs(v) == 0 ? 0 : conj(S / v)
 __host__ __device__ __forceinline__ cx load_current(cx s, cx v) {
@@ -66,6 +120,33 @@ __host__ __device__ __forceinline__ cx drop_col(const double *t, const cx ib0, c
     c = cadd(c, cmul(mk(t[2 * (0 * 3 + a)], t[2 * (0 * 3 + a) + 1]), ib0));
     c = cadd(c, cmul(mk(t[2 * (1 * 3 + a)], t[2 * (1 * 3 + a) + 1]), ib1));
     c = cadd(c, cmul(mk(t[2 * (2 * 3 + a)], t[2 * (2 * 3 + a) + 1]), ib2));
+    return c;
+}
+
+// The 9 TEMP values of one branch (t as in drop_col) from global memory.  The
+// table pointer arrives through a struct of generic pointers; the explicit
+// global address space turns the loads into global_load_dwordx4 (a flat load
+// also waits on the LDS counter), issued together ahead of the products.
+__device__ __forceinline__ void load_temp(const double *t, cx tm[9]) {
+#ifdef __HIP_DEVICE_COMPILE__
+    typedef const __attribute__((address_space(1))) double2 gd2;
+    gd2 *g = (gd2 *)t;
+#else
+    const double2 *g = (const double2 *)t;
+#endif
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const double2 v = g[i];
+        tm[i] = mk(v.x, v.y);
+    }
+}
+
+// drop_col on TEMP values held in registers, tm[L*3 + a] = TEMP(L, a)
+__host__ __device__ __forceinline__ cx drop_col_r(const cx tm[9], const cx ib0, const cx ib1, const cx ib2, int a) {
+    cx c = mk(0.0, 0.0);
+    c = cadd(c, cmul(tm[0 * 3 + a], ib0));
+    c = cadd(c, cmul(tm[1 * 3 + a], ib1));
+    c = cadd(c, cmul(tm[2 * 3 + a], ib2));
     return c;
 }
 

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -38,83 +39,174 @@ namespace {
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, RtcKernel> g_cache;
 
-// Straight-line sequential programs as register dataflow: Ibl, the tap
-// accumulators and the forward voltages are SSA values, so a row's dependent
-// adds wait on the previous row's adds, never on an LDS store->load round trip.
-// LDS only supplies the operands the parallel stages produced (IL, drop) --
-// independent loads the compiler issues early -- and receives Ib / V for the
-// parallel stages and the epilogue.
+// The sequential stages as one straight-line instruction stream that runs the
+// feeder's multi-track schedule (fpf_internal.h: TrackSched): at step s every
+// lane of track t executes the op of cell (s, t).  Because node k's state lives
+// in slot base[s] + t, the slot of step s is B + OFF(s) for every track, with
+// B = L + lane_off + t*slot per lane -- one LDS read, 1-2 dependent complex adds
+// and one LDS write per step serve all T tracks.  A track idle at a step reads
+// whatever its comb position holds and does not store (its position may be
+// another step's cell).
 //
-// Zero folding (exact): Ibl, Ib and tap sums are never -0 (each is a sum with
-// an IL term; x + y == -0 needs both -0), so 0 + Ibl == Ibl and T + 0 == T bit
-// for bit; a fresh Ibl (+0) plus IL keeps its add because IL may be -0.
-// LDS operands are loaded kAhead rows ahead of their use: with the row's store
-// in between, 2*kAhead LDS ops are in flight, inside lgkmcnt's 4-bit range.
-constexpr int kAhead = 6;
-
+// Along a block the chain value (Ibl backward, V forward) stays in a register.
+// Values crossing tracks -- a lateral's source voltage V(tap) forward, the
+// child-block currents a tap accumulates backward -- go through LDS: the
+// producing lane writes its slot, the consuming lane reads it at a track-relative
+// offset, later in the same wave's program order (LDS executes a wave's
+// operations in order; a wavefront-scope fence keeps the compiler from hoisting
+// the read above the write).  Per-track differences (which lanes take a
+// cross-track operand, reset Ibl, zero a phase) are compile-time constants
+// tested against the lane's track.
+//
+// Arithmetic is the reference's (DPF_return7.cpp:134-195), so V stays
+// bit-identical.  Zero folding (exact): Ibl, Ib and tap sums are never -0
+// (each is a sum with an IL term; x + y == -0 needs both -0), so 0 + Ibl == Ibl
+// and T + 0 == T bit for bit; a fresh Ibl (+0) plus IL keeps its add because IL
+// may be -0.
 std::string gen_program(const RtcSpec &sp) {
-    const long slot = 3L * sp.tile;                       // double2 per node slot
-    auto W = [&](int k) { return (long)k * slot; };
+    const TrackSched &ts = sp.ts;
+    const int T = ts.T, S = ts.S, A = std::max(1, sp.ahead);
+    const long SL = sp.slot > 0 ? sp.slot : 3L * sp.tile;         // double2 per slot
+    const long PS = sp.ps > 0 ? sp.ps : sp.tile;                   // double2 per phase
+    auto OFF = [&](int s) { return (long)ts.base[s] * SL; };       // this step's cell, relative to B
+    auto XOFF = [&](int node, int tcons) { return (long)(ts.slot(node) - tcons) * SL; };
+    const unsigned all_tracks = (1u << T) - 1;
+    auto cell = [&](int s, int t) { return ts.cell[(size_t)s * T + t]; };
+    // a scheduling barrier after every step keeps the LDS reads where they are
+    // placed (A steps ahead) instead of letting the scheduler hoist them all
+    const char *sb_env = getenv("FPF_RTC_SCHEDBAR");
+    const std::string sbar = (!sb_env || atoi(sb_env)) ? "    __builtin_amdgcn_sched_barrier(0);\n" : "";
     std::ostringstream o;
     o << "namespace fpf {\nstruct GenProg {\n"
       << "  static constexpr int kTile = " << sp.tile << ";\n"
       << "  static constexpr int kNN = " << sp.nn << ";\n"
+      << "  static constexpr int kTracks = " << T << ";\n"
+      << "  static constexpr int kNs = " << sp.ns << ";\n"
+      << "  static constexpr int kSlots = " << ts.n_slots << ";\n"
+      << "  static constexpr int kSlotBytes = " << SL * 16 << ";\n"
+      << "  static constexpr int kPhaseBytes = " << PS * 16 << ";\n"
+      << "  static constexpr bool kKeepIb = " << (sp.keep_ib ? "true" : "false") << ";\n"
       << "  static constexpr bool kLdsProgram = false;\n"
       << "  static constexpr bool kLdsTaps = false;\n"
-      << "  __device__ static __forceinline__ cx ld(const double2 *B, int i) { const double2 v = B[i]; return mk(v.x, v.y); }\n"
-      << "  __device__ static __forceinline__ void st(double2 *B, int i, cx v) { B[i] = make_double2(v.re, v.im); }\n";
-    // backward (DPF_return7.cpp:134-160 with separators folded into the preceding op):
-    // x = (T[a] + Ibl) + IL[k]; Ib[k] = x; separator: T[p] = T[p] + x, Ibl = 0
-    o << "  __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *, int, cx &) {\n"
-      << "    double2 *B = (double2 *)(L + lane_off);\n";
+      << "  __device__ static __forceinline__ cx ld(const double2 *B, long i) { const double2 v = B[i]; return mk(v.x, v.y); }\n"
+      << "  __device__ static __forceinline__ void st(double2 *B, long i, cx v) { B[i] = make_double2(v.re, v.im); }\n"
+      << "  __device__ static __forceinline__ void xfence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, \"wavefront\"); }\n";
+
+    // reads to emit at each execution index: (text, needs fence)
+    struct Rd { std::string text; bool cross; };
+
+    // ---------------- forward (:163-195), execution index e = step s
     {
-        std::string ibl;                       // "" = +0
-        std::map<int, std::string> tap;        // absent = +0
-        const size_t nbw = sp.bw.size();
-        auto load_il = [&](size_t i) { o << "    const cx il" << i << " = ld(B, " << W(sp.bw[i][0]) << ");\n"; };
-        for (size_t i = 0; i < std::min(nbw, (size_t)kAhead); ++i) load_il(i);
-        for (size_t i = 0; i < nbw; ++i) {
-            const auto &op = sp.bw[i];
-            if (i + kAhead < nbw) load_il(i + kAhead);
-            const std::string il = "il" + std::to_string(i), x = "x" + std::to_string(i);
-            const std::string t = (op[1] >= 0 && tap.count(op[1])) ? tap[op[1]] : "";
-            o << "    const cx " << x << " = ";
-            if (!t.empty()) o << (ibl.empty() ? "cadd(" + t + ", " + il + ")" : "cadd(cadd(" + t + ", " + ibl + "), " + il + ")");
-            else o << (ibl.empty() ? "cadd(mk(0, 0), " + il + ")" : "cadd(" + ibl + ", " + il + ")");
-            o << "; st(B, " << W(op[0]) << ", " << x << ");";
-            if (op[2] >= 0) {
-                auto it = tap.find(op[2]);
-                if (it == tap.end()) {
-                    tap[op[2]] = x;
+        std::vector<std::vector<Rd>> reads(S);
+        auto place = [&](int want, int after, const std::string &txt, bool cross) {
+            int e = std::max(0, want);
+            if (after >= 0) e = std::max(e, after + 1);
+            reads[std::min(e, S - 1)].push_back({txt, cross});
+        };
+        for (int s = 0; s < S; ++s) {
+            place(s - A, -1, "const cx d" + std::to_string(s) + " = ld(B, " + std::to_string(OFF(s)) + ");", false);
+            for (int t = 0; t < T; ++t) {
+                const int k = cell(s, t);
+                if (k < 0) continue;
+                const int src = ts.fw_src[k];
+                const bool prev = s > 0 && src != 0 && cell(s - 1, t) == src;
+                if (prev) continue;
+                const std::string nm = "xs" + std::to_string(s) + "_" + std::to_string(t);
+                if (src == 0) {   // V0: slots 0..T-1, offset 0 from every track's B
+                    place(s - A, -1, "const cx " + nm + " = ld(B, 0);", false);
                 } else {
-                    const std::string tn = "t" + std::to_string(i);
-                    o << " const cx " << tn << " = cadd(" << it->second << ", " << x << ");";
-                    it->second = tn;
+                    place(s - A, ts.step[src], "const cx " + nm + " = ld(B, " + std::to_string(XOFF(src, t)) + ");", true);
                 }
-                ibl.clear();
-            } else {
-                ibl = x;
             }
-            o << "\n";
         }
+        o << "  __device__ static __forceinline__ void s2(char *L, uint32_t, uint32_t vbase, int trk, int qp, const SeqFw *, int) {\n"
+          << "    double2 *B = (double2 *)(L + vbase);\n"
+          << "    cx vp = mk(0, 0);\n";
+        for (int s = 0; s < S; ++s) {
+            bool fenced = false;
+            for (const Rd &r : reads[s]) {
+                if (r.cross && !fenced) { o << "    xfence();\n"; fenced = true; }
+                o << "    " << r.text << "\n";
+            }
+            o << "    { cx vin = vp;";
+            for (int t = 0; t < T; ++t) {
+                const int k = cell(s, t);
+                if (k < 0) continue;
+                const int src = ts.fw_src[k];
+                const bool prev = s > 0 && src != 0 && cell(s - 1, t) == src;
+                if (!prev) o << " if (trk == " << t << ") vin = xs" << s << "_" << t << ";";
+            }
+            o << " cx v = csub(vin, d" << s << ");";
+            for (int t = 0; t < T; ++t) {
+                const int k = cell(s, t);
+                if (k >= 0 && ts.fw_mask[k])
+                    o << " if (trk == " << t << " && ((" << ts.fw_mask[k] << " >> qp) & 1)) v = mk(0, 0);";
+            }
+            if (ts.active[s] == all_tracks) o << " st(B, " << OFF(s) << ", v);";
+            else o << " if ((" << ts.active[s] << "u >> trk) & 1u) st(B, " << OFF(s) << ", v);";   // idle cells alias other slots
+            o << " vp = v; }\n" << sbar;
+        }
+        o << "  }\n";
     }
-    o << "  }\n";
-    // forward (:163-195): V[dst] = V[src] - drop[dst], phases in mask zeroed
-    o << "  __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, const SeqFw *, int, int qp) {\n"
-      << "    double2 *B = (double2 *)(L + lane_off);\n"
-      << "    const cx v0 = ld(B, 0);\n";
-    const size_t nfw = sp.fw.size();
-    auto load_d = [&](size_t i) { o << "    const cx d" << i << " = ld(B, " << W(sp.fw[i][0]) << ");\n"; };
-    for (size_t i = 0; i < std::min(nfw, (size_t)kAhead); ++i) load_d(i);
-    for (size_t i = 0; i < nfw; ++i) {
-        const auto &op = sp.fw[i];
-        if (i + kAhead < nfw) load_d(i + kAhead);
-        const std::string v = "v" + std::to_string(op[0]);
-        o << "    cx " << v << " = csub(v" << op[1] << ", d" << i << ");";
-        if (op[2]) o << " if ((" << op[2] << " >> qp) & 1) " << v << " = mk(0, 0);";
-        o << " st(B, " << W(op[0]) << ", " << v << ");\n";
+
+    // ---------------- backward (:134-160), execution index e = S-1-s
+    {
+        std::vector<std::vector<Rd>> reads(S);
+        auto place = [&](int want, int after, const std::string &txt, bool cross) {
+            int e = std::max(0, want);
+            if (after >= 0) e = std::max(e, after + 1);
+            reads[std::min(e, S - 1)].push_back({txt, cross});
+        };
+        for (int e = 0; e < S; ++e) {
+            const int s = S - 1 - e;
+            place(e - A, -1, "const cx il" + std::to_string(s) + " = ld(B, " + std::to_string(OFF(s)) + ");", false);
+            for (int t = 0; t < T; ++t) {
+                const int k = cell(s, t);
+                if (k < 0) continue;
+                const auto &ch = ts.children[k];
+                for (size_t j = 0; j < ch.size(); ++j) {
+                    const int c = ch[j];
+                    const int prod = S - 1 - ts.step[c];
+                    place(e - A, prod,
+                          "const cx ch" + std::to_string(s) + "_" + std::to_string(t) + "_" + std::to_string(j) +
+                              " = ld(B, " + std::to_string(XOFF(c, t)) + ");",
+                          true);
+                }
+            }
+        }
+        o << "  __device__ static __forceinline__ void s1(char *L, uint32_t, uint32_t vbase, int trk, int, const SeqBw *, int) {\n"
+          << "    double2 *B = (double2 *)(L + vbase);\n"
+          << "    cx ibl = mk(0, 0);\n";
+        for (int e = 0; e < S; ++e) {
+            const int s = S - 1 - e;
+            bool fenced = false;
+            for (const Rd &r : reads[e]) {
+                if (r.cross && !fenced) { o << "    xfence();\n"; fenced = true; }
+                o << "    " << r.text << "\n";
+            }
+            unsigned rmask = 0;
+            for (int t = 0; t < T; ++t) {
+                const int k = cell(s, t);
+                if (k >= 0 && ts.bw_reset[k]) rmask |= 1u << t;
+            }
+            o << "    { cx a = ibl;";
+            if (rmask == (1u << T) - 1) o << " a = mk(0, 0);";
+            else if (rmask) o << " if ((" << rmask << "u >> trk) & 1u) a = mk(0, 0);";
+            o << " cx x = cadd(a, il" << s << ");";
+            for (int t = 0; t < T; ++t) {
+                const int k = cell(s, t);
+                if (k < 0 || ts.children[k].empty()) continue;
+                const std::string pre = "ch" + std::to_string(s) + "_" + std::to_string(t) + "_";
+                o << " { cx tsum = " << pre << "0;";
+                for (size_t j = 1; j < ts.children[k].size(); ++j) o << " tsum = cadd(tsum, " << pre << j << ");";
+                o << " if (trk == " << t << ") x = cadd(cadd(tsum, a), il" << s << "); }";
+            }
+            if (ts.active[s] == all_tracks) o << " st(B, " << OFF(s) << ", x);";
+            else o << " if ((" << ts.active[s] << "u >> trk) & 1u) st(B, " << OFF(s) << ", x);";
+            o << " ibl = x; }\n" << sbar;
+        }
+        o << "  }\n";
     }
-    o << "  }\n";
     o << "};\n}  // namespace fpf\n"
       << "extern \"C\" __global__ __launch_bounds__(" << sp.nt << ", " << sp.min_waves << ") void fpf_rtc_tiled(fpf::FeederDev f, int B, "
       << "const double *__restrict__ pq, fpf::OutDev o) {\n"

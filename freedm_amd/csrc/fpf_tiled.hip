@@ -43,40 +43,13 @@ namespace {
 int threads_for(const FeederDev &f, int tile) { return tiled_threads(f, tile); }
 }  // namespace
 
-// Geometry of the specialised build.  The sequential stages cost ~45 cycles per
-// row per wave whatever the number of active lanes (each LDS wave-instruction
-// has a fixed issue cost), so one sequential wave should carry as many
-// scenarios as possible: up to 16 scenarios (48 lanes) per workgroup, two tasks
-// per lane, 1024 threads at <= 128 VGPRs -- one workgroup per CU, and a
-// 4096-scenario batch is exactly one wave of workgroups on 256 CUs.
-int rtc_tile(const FeederDev &f, int *nt, int *maxt) {
-    const int nb = f.nn - 1;
-    int m = 2, n = 1024;
-    int t = std::min(MAX_SEQ_TILE, n * m / nb);
-    if (t == 0) return 0;
-    // diagnostic override of the geometry: FPF_RTC_GEOM="nt,maxt[,min_waves]"
-    if (const char *g = getenv("FPF_RTC_GEOM")) {
-        int gn = 0, gm = 0;
-        if (sscanf(g, "%d,%d", &gn, &gm) == 2 && (gn == 256 || gn == 512 || gn == 1024) && gm >= 1 && gm <= 4) {
-            n = gn;
-            m = gm;
-            t = std::min(MAX_SEQ_TILE, n * m / nb);
-        }
-    }
-    while (t > 0 && tiled_lds_bytes_rtc(f, t) > 160 * 1024) --t;
-    // small feeders: the fewest threads that hold the tile's tasks
-    while (n > 256 && t * nb <= (n / 2) * m) n /= 2;
-    *nt = n;
-    *maxt = m;
-    return t;
-}
-
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile) {
-    return sizeof(double2) * 3 * (size_t)tile * (size_t)(f.nn + 2 + f.n_taps + 2) + sizeof(Flags);
+    const size_t slot = f.slot_bytes > 0 ? (size_t)f.slot_bytes : sizeof(double2) * 3 * (size_t)tile;
+    return slot * (size_t)f.n_slots + sizeof(Flags);
 }
 
 size_t tiled_lds_bytes(const FeederDev &f, int tile) {
-    const size_t state = tiled_lds_bytes_rtc(f, tile);
+    const size_t state = sizeof(double2) * 3 * (size_t)tile * (size_t)(f.nn + 2 + f.n_taps + 2) + sizeof(Flags);
     const size_t progs = sizeof(SeqBw) * (size_t)f.n_seq_bw + sizeof(SeqFw) * (size_t)f.n_seq_fw;
     return f.prog_lds ? state + progs : state;
 }
@@ -85,7 +58,9 @@ int tiled_max_tile(const FeederDev &f) {
     const int nb = f.nn - 1;
     int t = std::min(MAX_SEQ_TILE, (512 * AOT_MAXT) / nb);
     if (t == 0) t = std::min(MAX_SEQ_TILE, (1024 * AOT_MAXT) / nb);
-    while (t > 0 && tiled_lds_bytes_rtc(f, t) > 160 * 1024) --t;
+    FeederDev g = f;
+    g.prog_lds = 0;
+    while (t > 0 && tiled_lds_bytes(g, t) > 160 * 1024) --t;
     return t;
 }
 

@@ -3,13 +3,14 @@
 // One workgroup owns a tile of TILE scenarios for the whole solve; their state
 // lives in LDS for all sweeps, so HBM only sees the loads in and the results
 // out.  One LDS slot per (node k, phase p, scenario s) -- byte offset
-// k*3*TILE*16 + (p*TILE + s)*16, a complex fp64 -- holds, in turn within a sweep:
+// slot(k)*3*TILE*16 + (p*TILE + s)*16, a complex fp64 -- holds, in turn within a sweep:
 //     V(k)  --P1-->  IL(k-1)  --S1-->  Ib(k-1)  --P2-->  drop(k)  --S2-->  V(k)
-// Slot 0 keeps the constant V0 (the substation, DPF_return7.cpp:84-96).
+// The substation's V0 (DPF_return7.cpp:84-96) sits in slot 0 (slots 0..T-1 in
+// the multi-track layout), never overwritten.
 //
 //   P1 (parallel, one task per (s,k), 3 phases per lane):  IL = conj(Sld/V)   :106-130
-//   S1 (sequential, one lane per (s,p)): the backward program in row order     :134-160
-//      with tap accumulators in LDS, then the substation convergence test     :199-210
+//   S1 (sequential): the backward program in row order                        :134-160
+//      then the substation convergence test                                   :199-210
 //   P2 (parallel): drop(k) = lng*(Ib(k-1) . Zl)  (TEMP table, ZGEMM order)    :163-178
 //   S2 (sequential): V(dst) = V(src) - drop(dst), phase zeroing               :169-195
 //   (a scenario retires after its last sweep; its state stays frozen)
@@ -19,13 +20,15 @@
 // is bit-identical to the sequential program (and to the oracle).
 //
 // The parallel stages carry the divisions and the 3x3 products; the sequential
-// stages are 1-2 dependent complex adds per row, three lanes (phases) per
-// scenario on one wave per SIMD.  Their programs (fpf_internal.h: separators
-// folded into branch ops, LDS byte offsets baked in, zero/dummy slots instead
-// of branches) sit in LDS and run in chunks of SEQ_CHUNK ops: a chunk's
-// descriptors and all its LDS operands are loaded first, so the dependent chain
-// waits on the adds, not on LDS latency.  A lane keeps Sld, IL and Ib of its
-// tasks in VGPRs across the sweep.
+// stages are 1-2 dependent complex adds per row.  Their lanes are
+// (phase p, track t, scenario s), lane = (p*T + t)*NS + s: a Prog with T tracks
+// runs T independent chains of the feeder's block tree side by side in one
+// instruction stream (fpf_rtc.cpp), NS scenarios per wave, 3*T*NS <= 64.  The
+// specialised layout pads the phase and slot strides so those lanes hit
+// distinct LDS banks (fpf_api.cpp: bank_layout).  RuntimeProg (T = 1)
+// interprets LDS-staged op programs (fpf_internal.h: SeqBw/SeqFw) in chunks of
+// SEQ_CHUNK ops, all of a chunk's LDS operands loaded before its dependent adds.
+// A lane keeps Sld, IL and Ib of its tasks in VGPRs across the sweep.
 #pragma once
 #include "fpf_internal.h"
 #include "fpf_math.hpp"
@@ -83,15 +86,24 @@ __device__ __forceinline__ double2 emit_node(const OutDev &o, double s3, int nn,
 
 // Sequential stages from the LDS-staged op programs (fpf_internal.h: SeqBw/SeqFw),
 // executed in chunks of SEQ_CHUNK ops with all of a chunk's LDS operands
-// loaded before its dependent arithmetic.
+// loaded before its dependent arithmetic.  Layout: slot k = node k, slot nn a
+// permanent zero, slot nn+1 a dummy sink, then the tap accumulators.
 struct RuntimeProg {
     static constexpr int kTile = 0;
     static constexpr int kNN = 0;
+    static constexpr int kTracks = 1;
+    static constexpr int kNs = 21;
+    static constexpr int kSlots = 0;       // runtime: nn + 2
+    static constexpr int kSlotBytes = 0;   // runtime: 3*TILE*16
+    static constexpr int kPhaseBytes = 0;  // runtime: TILE*16
+    static constexpr bool kKeepIb = true;  // Ib of the last sweep kept for PQb
     static constexpr bool kLdsProgram = true;
     static constexpr bool kLdsTaps = true;
 
-    __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, const SeqBw *pbw, int nbw, cx &ibl) {
+    __device__ static __forceinline__ void s1(char *L, uint32_t lane_off, uint32_t, int, int, const SeqBw *pbw,
+                                              int nbw) {
         auto at = [&](uint32_t off) -> double2 * { return (double2 *)(L + off); };
+        cx ibl = mk(0, 0);
         for (int q0 = 0; q0 < nbw; q0 += U) {
             SeqBw e[U];
             cx vil[U], va[U], vt[U];
@@ -122,7 +134,8 @@ struct RuntimeProg {
         }
     }
 
-    __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, const SeqFw *pfw, int nfw, int qp) {
+    __device__ static __forceinline__ void s2(char *L, uint32_t lane_off, uint32_t, int, int qp, const SeqFw *pfw,
+                                              int nfw) {
         auto at = [&](uint32_t off) -> double2 * { return (double2 *)(L + off); };
         cx vprev = mk(0, 0);
         for (int q0 = 0; q0 < nfw; q0 += U) {
@@ -155,22 +168,28 @@ struct RuntimeProg {
 
 }  // namespace
 
-// The kernel body.  Prog supplies the two sequential stages: RuntimeProg runs
-// the LDS-staged op programs (any well-formed feeder); the hipRTC path
-// (fpf_rtc.cpp) generates a Prog whose stages are the feeder's programs as
-// straight-line code with constant LDS offsets and a compile-time tile.
+// The kernel body.  Prog supplies the two sequential stages and the LDS layout:
+// RuntimeProg runs the LDS-staged op programs (any well-formed feeder); the
+// hipRTC path (fpf_rtc.cpp) generates a Prog whose stages are the feeder's
+// multi-track schedule as straight-line code with constant LDS offsets and a
+// compile-time tile.
 template <int NT, int MAXT, class Prog>
 __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const double *__restrict__ pq,
                                            const OutDev &o) {
     extern __shared__ double2 lds[];
     constexpr int NW = NT / 64;
+    constexpr int T = Prog::kTracks, NS = Prog::kNs;
+    static_assert(3 * T * NS <= 64, "sequential lanes exceed a wave");
     const int TILE = Prog::kTile > 0 ? Prog::kTile : f.tile;
     const int nn = Prog::kNN > 0 ? Prog::kNN : f.nn, nb = nn - 1, nl = f.nl;
     const int nbw = f.n_seq_bw, nfw = f.n_seq_fw;
-    const uint32_t slot = 3u * (uint32_t)TILE * 16u;           // bytes per node slot
+    const uint32_t slot = Prog::kSlotBytes > 0 ? (uint32_t)Prog::kSlotBytes : 3u * (uint32_t)TILE * 16u;
+    const uint32_t psb = Prog::kPhaseBytes > 0 ? (uint32_t)Prog::kPhaseBytes : (uint32_t)TILE * 16u;
     char *const L = (char *)lds;
-    const uint32_t w_bytes = (uint32_t)(nn + 2) * slot;
-    const uint32_t t_bytes = (uint32_t)(f.n_taps + 2) * slot;
+    const int n_w = Prog::kSlots > 0 ? Prog::kSlots : nn + 2;   // state slots
+    const int zero_from = Prog::kSlots > 0 ? Prog::kSlots : nn; // slots >= this start at zero
+    const uint32_t w_bytes = (uint32_t)n_w * slot;
+    const uint32_t t_bytes = Prog::kLdsTaps ? (uint32_t)(f.n_taps + 2) * slot : 0u;
     Flags *fl = (Flags *)(L + w_bytes + t_bytes);
     const bool plds = Prog::kLdsProgram && f.prog_lds;
     SeqBw *pbw = plds ? (SeqBw *)(fl + 1) : (SeqBw *)f.seq_bw;
@@ -184,13 +203,15 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
     const cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
     STAMP(0);
 
-    // ---- init: V slots = V0 (:92-96), zero/dummy slots 0, taps 0, flags, programs
-    for (int i = tid; i < (nn + 2) * 3 * TILE; i += NT) {
-        const int p = (i / TILE) % 3;
-        const cx v = i >= nn * 3 * TILE ? mk(0, 0) : (p == 0 ? v0[0] : (p == 1 ? v0[1] : v0[2]));
-        lds_st(lds, i, v);
+    // ---- init: state slots = V0 (:92-96), zero/dummy slots 0, taps 0, flags, programs
+    for (int i = tid; i < n_w * 3 * TILE; i += NT) {
+        const int j = i / (3 * TILE), p = (i / TILE) % 3, s = i % TILE;
+        const cx v = j >= zero_from ? mk(0, 0) : (p == 0 ? v0[0] : (p == 1 ? v0[1] : v0[2]));
+        const double2 w = make_double2(v.re, v.im);
+        *(double2 *)(L + (uint32_t)j * slot + (uint32_t)p * psb + (uint32_t)s * 16u) = w;
     }
-    for (int i = tid; i < (f.n_taps + 2) * 3 * TILE; i += NT) lds_st((double2 *)(L + w_bytes), i, mk(0, 0));
+    if (Prog::kLdsTaps)
+        for (int i = tid; i < (f.n_taps + 2) * 3 * TILE; i += NT) lds_st((double2 *)(L + w_bytes), i, mk(0, 0));
     if (plds) {
         for (int i = tid; i < nbw; i += NT) pbw[i] = f.seq_bw[i];
         for (int i = tid; i < nfw; i += NT) pfw[i] = f.seq_fw[i];
@@ -205,6 +226,7 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
     const double *tz[MAXT];
     uint32_t woff[MAXT];
     int tsc[MAXT];                                   // scenario of the task, -1 = none
+    unsigned rr_ok = 0;                              // bit j: task j's Sld in dv_in_range
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
         const int t = tid + j * NT;
@@ -215,7 +237,7 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
         if (t < ntask && s < ns) {
             const NodeOp nd = f.node_ops[k];
             tz[j] = f.tz + 18 * (size_t)nd.fw;
-            woff[j] = (uint32_t)k * slot + (uint32_t)s * 16u;
+            woff[j] = (uint32_t)nd.slot * slot + (uint32_t)s * 16u;
             tsc[j] = s;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
@@ -223,21 +245,28 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
                                  pq[((size_t)(2 * p + 1) * nl + nd.row) * B + s0 + s]);
                 sld[j][p] = cdiv(sl, mk(f.s3, 0.0));
             }
+            bool ok = true;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ok = ok && dv_in_range(sld[j][p].re) && dv_in_range(sld[j][p].im);
+            rr_ok |= (ok ? 1u : 0u) << j;
         }
 #pragma unroll
         for (int p = 0; p < 3; ++p) { il[j][p] = mk(0, 0); ib[j][p] = mk(0, 0); }
     }
 
-    // sequential lanes: the stages are latency-bound chains, so a tile uses as
-    // few waves as fit it (21 scenarios x 3 phases per wave); scenario s runs on
-    // wave s % NWS, lanes 3*(s/NWS) + p
-    const int NWS = (TILE + 20) / 21 < NW ? (TILE + 20) / 21 : NW;
+    // sequential lanes (track qt, phase qp, scenario qs): NS scenarios per wave,
+    // scenario s on wave s / NS; the stages are latency-bound chains, so a tile
+    // uses as few waves as hold it
+    const int NWS = (TILE + NS - 1) / NS < NW ? (TILE + NS - 1) / NS : NW;
     const int wv = tid >> 6, ln = tid & 63;
-    const int qj = ln / 3, qp = ln - 3 * qj;
-    const int qs = qj * NWS + wv;
-    const bool qlane = wv < NWS && qj < 21 && qs < ns;
-    const int gbase = qj * 3;
-    const uint32_t lane_off = qlane ? ((uint32_t)qp * TILE + qs) * 16u : 0u;
+    const int qp = ln / (T * NS), qt = (ln / NS) % T, qsl = ln % NS;
+    const int qs = wv * NS + qsl;
+    const bool qlane = wv < NWS && ln < 3 * T * NS && qs < ns;
+    const bool qlead = qlane && qt == 0;               // one chain per (scenario, phase) does the tests
+    const int gbase = qt * NS + qsl;                   // lane of phase 0 of this (track, scenario)
+    const uint32_t lane_off = qlane ? (uint32_t)qp * psb + (uint32_t)qs * 16u : 0u;
+    const uint32_t vbase = lane_off + (uint32_t)qt * slot;
+    const uint32_t n1_off = (uint32_t)f.node_ops[1].slot * slot;   // Ib(0) lives in node 1's slot
     cx ibo = mk(0, 0);
     __syncthreads();
     STAMP(1);
@@ -248,12 +277,24 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
 #pragma unroll
         for (int j = 0; j < MAXT; ++j) {
             if (tsc[j] >= 0 && fl->active[tsc[j]]) {
+                double2 *w[3];
+                cx v[3];
+                bool rr = (rr_ok >> j) & 1;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    double2 *w = at(woff[j] + p * TILE * 16);
-                    il[j][p] = load_current(sld[j][p], mk(w->x, w->y));
-                    *w = make_double2(il[j][p].re, il[j][p].im);
+                    w[p] = at(woff[j] + p * psb);
+                    v[p] = mk(w[p]->x, w[p]->y);
+                    rr = rr && dv_in_range(v[p].re) && dv_in_range(v[p].im);
                 }
+                if (rr) {   // the shared-reciprocal division (same bits as the reference's)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) il[j][p] = load_current_rr(sld[j][p], v[p]);
+                } else {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) il[j][p] = load_current(sld[j][p], v[p]);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *w[p] = make_double2(il[j][p].re, il[j][p].im);
             }
         }
         __syncthreads();
@@ -261,23 +302,22 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
 
         // ---- S1: backward program + convergence
         if (qlane && fl->active[qs]) {
-            cx ibl = mk(0, 0);
-            Prog::s1(L, lane_off, pbw, nbw, ibl);
+            Prog::s1(L, lane_off, vbase, qt, qp, pbw, nbw);
             // reset this lane's tap accumulators for the next sweep
             if (Prog::kLdsTaps)
                 for (int tp = 0; tp < f.n_taps; ++tp) *at(w_bytes + tp * slot + lane_off) = make_double2(0, 0);
             // errmx = max_p |Ib(0,p) - Ibo(p)|  (first element, then strict '>')
-            const double2 b0 = *at(1 * slot + lane_off);
+            const double2 b0 = *at(n1_off + lane_off);
             const cx ib0 = mk(b0.x, b0.y);
             const cx d = csub(ib0, ibo);
             const double df = hypot(d.re, d.im);
-            const double d0 = __shfl(df, gbase + 0, 64), d1 = __shfl(df, gbase + 1, 64),
-                         d2 = __shfl(df, gbase + 2, 64);
+            const double d0 = __shfl(df, gbase + 0 * T * NS, 64), d1 = __shfl(df, gbase + 1 * T * NS, 64),
+                         d2 = __shfl(df, gbase + 2 * T * NS, 64);
             double errmx = d0;
             if (d1 > errmx) errmx = d1;
             if (d2 > errmx) errmx = d2;
             ibo = ib0;
-            if (qp == 0) {
+            if (qlead && qp == 0) {
                 fl->fin[qs] = errmx < f.eps ? 1 : (it == f.mxitr - 1 ? 2 : 0);
                 if (errmx < f.eps || it == f.mxitr - 1) {
                     if (o.iters) o.iters[s0 + qs] = it + 1;
@@ -292,13 +332,18 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
 #pragma unroll
         for (int j = 0; j < MAXT; ++j) {
             if (tsc[j] >= 0 && fl->active[tsc[j]]) {
-                double2 *w0 = at(woff[j]), *w1 = at(woff[j] + TILE * 16), *w2 = at(woff[j] + 2 * TILE * 16);
-                ib[j][0] = mk(w0->x, w0->y);
-                ib[j][1] = mk(w1->x, w1->y);
-                ib[j][2] = mk(w2->x, w2->y);
-                const cx d0 = drop_col(tz[j], ib[j][0], ib[j][1], ib[j][2], 0);
-                const cx d1 = drop_col(tz[j], ib[j][0], ib[j][1], ib[j][2], 1);
-                const cx d2 = drop_col(tz[j], ib[j][0], ib[j][1], ib[j][2], 2);
+                cx tm[9];
+                load_temp(tz[j], tm);
+                double2 *w0 = at(woff[j]), *w1 = at(woff[j] + psb), *w2 = at(woff[j] + 2 * psb);
+                const cx b0 = mk(w0->x, w0->y), b1 = mk(w1->x, w1->y), b2 = mk(w2->x, w2->y);
+                if (Prog::kKeepIb) {
+                    ib[j][0] = b0;
+                    ib[j][1] = b1;
+                    ib[j][2] = b2;
+                }
+                const cx d0 = drop_col_r(tm, b0, b1, b2, 0);
+                const cx d1 = drop_col_r(tm, b0, b1, b2, 1);
+                const cx d2 = drop_col_r(tm, b0, b1, b2, 2);
                 *w0 = make_double2(d0.re, d0.im);
                 *w1 = make_double2(d1.re, d1.im);
                 *w2 = make_double2(d2.re, d2.im);
@@ -311,8 +356,9 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
         // (its state -- V in LDS, IL/Ib in the task registers, Ib(0) in ibo -- is
         // then frozen until the epilogue)
         if (qlane && fl->active[qs]) {
-            Prog::s2(L, lane_off, pfw, nfw, qp);
-            if (qp == 0 && fl->fin[qs]) fl->active[qs] = 0;
+            Prog::s2(L, lane_off, vbase, qt, qp, pfw, nfw);
+            // every lane of the scenario is on this wave and past s2 here
+            if (qlead && qp == 0 && fl->fin[qs]) fl->active[qs] = 0;
         }
         __syncthreads();
         STAMP(5 + it * 5);
@@ -330,13 +376,14 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
             const size_t gs = (size_t)s0 + s;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                double2 *w = at(woff[j] + p * TILE * 16);
-                *w = emit_node(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p], ib[j][p]);
+                double2 *w = at(woff[j] + p * psb);
+                *w = emit_node(o, f.s3, nn, B, k, p, gs, mk(w->x, w->y), il[j][p],
+                               Prog::kKeepIb ? ib[j][p] : mk(0, 0));   // !kKeepIb: no PQb requested
             }
         }
     }
     __syncthreads();
-    if (qlane) {
+    if (qlead) {
         const int gs = s0 + qs;
         // substation row 0: V0, Ib(0) (= ibo, the last sweep's), IL(nn-1) = 0
         const cx v = qp == 0 ? v0[0] : (qp == 1 ? v0[1] : v0[2]);
@@ -354,7 +401,8 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
         for (int k0 = 1; k0 < nn; k0 += 8) {
             double2 r[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) r[u] = k0 + u < nn ? *at((k0 + u) * slot + lane_off) : make_double2(0, 0);
+            for (int u = 0; u < 8; ++u)
+                r[u] = k0 + u < nn ? *at((uint32_t)f.node_ops[k0 + u].slot * slot + lane_off) : make_double2(0, 0);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 if (k0 + u < nn) {
@@ -365,9 +413,12 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
         }
         if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
         const double x = sb.re - (acc1 + acc2);
-        const double x0 = __shfl(x, gbase + 0, 64), x1 = __shfl(x, gbase + 1, 64), x2 = __shfl(x, gbase + 2, 64);
-        const double n0 = __shfl(mn, gbase + 0, 64), n1 = __shfl(mn, gbase + 1, 64), n2 = __shfl(mn, gbase + 2, 64);
-        const double m0 = __shfl(mx, gbase + 0, 64), m1 = __shfl(mx, gbase + 1, 64), m2 = __shfl(mx, gbase + 2, 64);
+        const double x0 = __shfl(x, gbase + 0 * T * NS, 64), x1 = __shfl(x, gbase + 1 * T * NS, 64),
+                     x2 = __shfl(x, gbase + 2 * T * NS, 64);
+        const double n0 = __shfl(mn, gbase + 0 * T * NS, 64), n1 = __shfl(mn, gbase + 1 * T * NS, 64),
+                     n2 = __shfl(mn, gbase + 2 * T * NS, 64);
+        const double m0 = __shfl(mx, gbase + 0 * T * NS, 64), m1 = __shfl(mx, gbase + 1 * T * NS, 64),
+                     m2 = __shfl(mx, gbase + 2 * T * NS, 64);
         if (qp == 0) {
             double vmin = n0, vmax = m0;
             if (n1 < vmin) vmin = n1;

@@ -173,6 +173,12 @@ int         fpf_aggregate_device(fpf_feeder *feeder, int n_scen, const signed ch
                                  const double *d_loss, const double *d_vmin, const double *d_vmax,
                                  double *d_agg, void *stream);
 
+/* Diagnostics: on-device check, over n seeded operand sets, that the
+ * shared-reciprocal division the tiled kernel uses gives the same bits as the
+ * compiler's a / b and as the libgcc __divdc3 complex division.  Returns the
+ * number of mismatching results (0 expected) or FPF_ERR_*. */
+long        fpf_selftest_division(int device, long n, unsigned long seed);
+
 #ifdef __cplusplus
 }
 #endif

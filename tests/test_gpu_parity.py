@@ -211,3 +211,29 @@ def test_hosting_shards_are_invariant():
     hi = pf.solve(F.hosting_loads(f, np.arange(256, 512)))
     np.testing.assert_array_equal(np.concatenate([lo["V_re"], hi["V_re"]], axis=2), full["V_re"])
     np.testing.assert_array_equal(np.concatenate([lo["loss"], hi["loss"]]), full["loss"])
+
+
+def test_shared_reciprocal_division_is_bit_exact():
+    """The tiled kernel's dv_div / cdiv_rr (fpf_math.hpp) against the compiler's
+    a / b and libgcc's __divdc3, bit for bit, on 2^26 seeded operand sets over
+    the guarded exponent range, zeros and signs included."""
+    from freedm_amd import _lib
+    assert _lib.load().fpf_selftest_division(0, 1 << 26, 20261016) == 0
+
+
+@pytest.mark.parametrize("tracks", [1, 2, 3, 4])
+def test_track_counts_are_bit_identical(tracks, monkeypatch):
+    """Every multi-track schedule of the specialised kernel (fpf_api.cpp:
+    schedule_tracks) gives the reference's bits: V, PQb, PQL, loss, iterations."""
+    monkeypatch.setenv("FPF_RTC_TRACKS", str(tracks))
+    for name in ("g1_demo_batch", "g2_dlnew", "g3_123bus", "g5_nonconv", "g6_missing_phase"):
+        g = load_golden(name)
+        pf = _pf(g["Dl"], g["Z"], kernel="tiled", specialize=True)
+        assert pf.info["specialized"] == 1, pf.rtc_error
+        r = pf.solve(g["pq"])
+        assert (r["iters"] == g["iters"]).all() and (r["status"] == g["status"]).all(), name
+        np.testing.assert_array_equal(r["V_re"], g["V_re"], err_msg=name)
+        np.testing.assert_array_equal(r["V_im"], g["V_im"], err_msg=name)
+        np.testing.assert_array_equal(r["PQb"][:, :, :4], g["PQb"], err_msg=name)
+        np.testing.assert_array_equal(r["PQL"][:, :, :4], g["PQL"], err_msg=name)
+        np.testing.assert_array_equal(r["loss"], g["loss"], err_msg=name)

@@ -23,8 +23,10 @@ def _hiprtc():
 OPTS = [b"--offload-arch=gfx950", b"-O3", b"-ffp-contract=off", b"-std=c++17"]
 
 
-@pytest.mark.parametrize("nn", [9, 123])
-def test_rtc_source_compiles(nn):
+@pytest.mark.parametrize("nn,tracks", [(9, 0), (123, 0), (123, 1), (123, 2), (123, 4)])
+def test_rtc_source_compiles(nn, tracks, monkeypatch):
+    if tracks:
+        monkeypatch.setenv("FPF_RTC_TRACKS", str(tracks))
     from rtc_dump import rtc_source
     from freedm_amd import demo_feeder, synthetic_feeder
     f = demo_feeder() if nn == 9 else synthetic_feeder(nn, nn)
