@@ -7,7 +7,8 @@ Workload = BASELINE config 2: synthetic 123-bus feeder (seed 123), a batch of
 4096 seeded load/DER scenarios per GPU (weak scaling; scenario ids are global,
 rank r solves ids [r*4096, (r+1)*4096)).  One step = one pass of the hot path
 over that batch: libfreedm_pf's tiled DPF kernel (all sweeps, fused loss/Vmin/
-Vmax) plus the deterministic batch aggregate, inputs resident in HBM.  After
+Vmax, and the deterministic batch aggregate in the same launch), inputs
+resident in HBM.  After
 the K timed steps the per-GPU aggregates are combined once by an RCCL
 all-reduce (the only collective of the path).  value = converged scenarios of
 all ranks / max-over-ranks wall time of the timed region.
@@ -95,6 +96,7 @@ def main():
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-specialize", action="store_true")
+    ap.add_argument("--exact", type=int, default=0, help="1: the reference's roundings (bit-identical mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -114,7 +116,8 @@ def main():
     from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
 
     feeder = synthetic_feeder(FEEDER_NODES, FEEDER_SEED)
-    pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize)
+    pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize,
+                   exact=args.exact)
     B = args.scenarios
     pf.reserve(B)
     ids = np.arange(rank * B, (rank + 1) * B)
@@ -134,10 +137,11 @@ def main():
     def step(i, ev0=None, ev1=None):
         if ev0 is not None:
             ev0.record(stream)
-        solve()                      # the DPF kernel: all sweeps + fused loss / Vmin / Vmax
+        # the DPF kernel: all sweeps, fused loss / Vmin / Vmax per scenario and the
+        # deterministic batch aggregate (8 doubles per step, last-workgroup reduction)
+        solve(agg_ptr[i])
         if ev1 is not None:
             ev1.record(stream)
-        aggregate(agg_ptr[i])        # deterministic batch aggregate (8 doubles per step)
 
     def combine(a):
         return torch.cat([a[:, 0].sum().view(1), a[:, 1].min().view(1), a[:, 2].max().view(1), a[:, 3:].sum(0)])
@@ -148,7 +152,11 @@ def main():
     torch.cuda.synchronize(dev)
     conv_per_step = int((out["status"] == 0).sum().item())
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events around every ev_every-th launch (an event pair costs the stream a
+    # few microseconds, so they bracket a sample of the launches, not all of them)
+    ev_every = max(1, args.steps // 8)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if i % ev_every == 0
+           else (None, None) for i in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -172,7 +180,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs if e0 is not None]
     avg_kern_s = float(np.mean(kern_ms)) / 1e3
     tot = total.cpu().numpy()
     n_conv_all = float(tot[3])
@@ -198,7 +206,8 @@ def main():
             "data": "synthetic (seeded 123-bus radial feeder + seeded load/PV scenarios)",
             "config": {"workload": f"BASELINE config 2: 123-bus feeder, {B} scenarios per GPU per step",
                        "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
-                       "tile": pf.info["tile"], "specialized": pf.info["specialized"], "parallelism": f"scenario shards x{world}"},
+                       "tile": pf.info["tile"], "specialized": pf.info["specialized"], "exact": bool(args.exact),
+                       "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "dpf_tiled_kernel" if pf.kernel == "tiled" else "dpf_generic_kernel",
@@ -209,6 +218,7 @@ def main():
             "converged_per_step_rank0": conv_per_step,
             "host_submit_ms_per_step": t_submit / args.steps * 1e3,
             "kernel_ms_min_max": [float(np.min(kern_ms)), float(np.max(kern_ms))],
+            "kernel_launches_timed": len(kern_ms),
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(feeder, seconds=args.cpu_seconds)

@@ -52,6 +52,10 @@ struct fpf_feeder {
     size_t stage_bytes = 0;
     void *d_stage = nullptr;
     double *d_agg = nullptr;
+    // fused aggregate of the specialised kernel: per-tile partials + arrival ticket
+    double *d_partials = nullptr;
+    size_t partials_cap = 0;      // tiles
+    unsigned *d_ticket = nullptr;
     // topology-specialised tiled kernel (hipRTC), if built
     bool rtc = false;
     RtcKernel rtc_kernel{};      // without the PQb output (no Ib kept in registers)
@@ -87,6 +91,7 @@ extern "C" void fpf_opts_default(fpf_opts *o) {
     o->ub_v = 1.05;             // load_system_data.cpp:24
     o->tile = 0;
     o->specialize = 1;
+    o->exact = 0;
 }
 
 extern "C" int fpf_ctx_create(int device, fpf_ctx **out) {
@@ -412,7 +417,7 @@ bool wants_rtc(const HostFeeder &h, const fpf_opts &o) {
 // (DPF_return7.cpp:176-178) and, backward, a tap before the first node of each
 // child block (the separator's Ib(sbus(m+1)) += Ibl, :138-146).  Blocks are
 // placed highest bottom-level first on the track where they can start earliest.
-TrackSched schedule_tracks(const HostFeeder &h, int T, int D) {
+TrackSched schedule_tracks(const HostFeeder &h, int T, int D, unsigned seed = 0) {
     const int nl = h.nl, nn = h.nn;
     TrackSched ts;
     ts.T = T;
@@ -467,13 +472,21 @@ TrackSched schedule_tracks(const HostFeeder &h, int T, int D) {
     std::vector<char> done(nb, 0);
     ts.step.assign(nn, -1);
     ts.track.assign(nn, -1);
+    // seed 0: bottom level, ties to the earlier block; other seeds perturb the
+    // priorities (xorshift) so the caller can keep the shortest of many tries
+    std::vector<double> prio(nb);
+    unsigned x = seed * 2654435761u + 12345u;
+    for (int b = 0; b < nb; ++b) {
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        prio[b] = bl[blk[b][0]] + (seed ? 0.999 * ((x & 0xffff) / 65536.0) * (1 + (seed % 4)) : -1e-6 * b);
+    }
     for (int n = 0; n < nb; ++n) {
         int best = -1;
         for (int b = 0; b < nb; ++b) {
             if (done[b]) continue;
             bool ready = true;
             for (int p : pred[b]) ready = ready && done[p];
-            if (ready && (best < 0 || bl[blk[b][0]] > bl[blk[best][0]])) best = b;
+            if (ready && (best < 0 || prio[b] > prio[best])) best = b;
         }
         int est = 0;
         for (size_t i = 0; i < blk[best].size(); ++i)
@@ -563,13 +576,14 @@ struct BankLayout { int ps = 0, sl = 0, s_deg = 99, p_deg = 99; };
 
 // Phase stride PS >= tile and slot stride SL >= 3*PS (16-byte units) that make
 // the sequential lanes (phase p, track t, scenario s -> lane (p*T + t)*NS + s,
-// at comb offsets base + t) conflict-free, then the parallel lanes (16
-// scenarios of each of 4 nodes per wave), then the least padding.
-BankLayout bank_layout(int T, int NS, int tile) {
+// at comb offsets base + t) conflict-free with the least padding, then the
+// fewest conflicts of the parallel lanes (16 scenarios of each of 4 nodes per
+// wave; compute-bound, so second).
+BankLayout bank_layout(int T, int NS, int tile, int max_sl = 1 << 30) {
     BankLayout best;
     int units[64];
     for (int ps = tile; ps <= tile + 8; ++ps)
-        for (int sl = 3 * ps; sl <= 3 * ps + 16; ++sl) {
+        for (int sl = 3 * ps; sl <= std::min(3 * ps + 16, max_sl); ++sl) {
             int sd = 1;
             for (int wv = 0; wv < 2; ++wv)
                 for (int base = 0; base < 4; ++base)
@@ -591,7 +605,7 @@ BankLayout bank_layout(int T, int NS, int tile) {
                     }
                     pd = std::max(pd, bank_degree(units, false));
                 }
-            if (sd < best.s_deg || (sd == best.s_deg && (pd < best.p_deg || (pd == best.p_deg && sl < best.sl)))) {
+            if (sd < best.s_deg || (sd == best.s_deg && (sl < best.sl || (sl == best.sl && pd < best.p_deg)))) {
                 best.ps = ps;
                 best.sl = sl;
                 best.s_deg = sd;
@@ -607,7 +621,7 @@ BankLayout bank_layout(int T, int NS, int tile) {
 // (steps x bank-conflict degree, sequential waves spread over the 4 SIMDs).
 struct RtcPlan {
     TrackSched ts;
-    int tile = 0, ns = 0, nt = 0, maxt = 0;
+    int tile = 0, ns = 0, nt = 0, maxt = 0, wpc = 1;
     BankLayout lay;
 };
 
@@ -620,14 +634,22 @@ bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
     for (int T = 1; T <= 4; ++T) {
         if (force_t && T != force_t) continue;
         for (int D = 1; D <= 4; ++D) {
-            TrackSched s = schedule_tracks(h, T, T == 1 ? 1 : D);
-            if (by_t[T].S == 0 || s.S <= by_t[T].S) by_t[T] = std::move(s);
+            for (unsigned seed = 0; seed < (T == 1 ? 1u : 64u); ++seed) {
+                TrackSched s = schedule_tracks(h, T, T == 1 ? 1 : D, seed);
+                if (by_t[T].S == 0 || s.S < by_t[T].S || (s.S == by_t[T].S && seed == 0)) by_t[T] = std::move(s);
+            }
             if (T == 1) break;
         }
         pack_slots(by_t[T], h.nn);
     }
     const int nb = h.nn - 1;
-    int tmax = std::min(MAX_TILE, (1024 * 2) / std::max(nb, 1));
+    // workgroups per CU: 2 lets one tile's latency-bound sequential stage overlap
+    // the other tile's parallel stages (each then gets half the LDS and 512 threads)
+    int wpc = 1;
+    if (const char *e = getenv("FPF_RTC_WPC")) wpc = std::max(1, std::min(2, atoi(e)));
+    // (two resident tiles: leave the allocation granularity some room)
+    const size_t lds_budget = (size_t)160 * 1024 / wpc - (wpc > 1 ? 2048 : 0);
+    int tmax = std::min(MAX_TILE, (1024 / wpc * 2) / std::max(nb, 1));
     if (o.tile > 0) tmax = std::min(tmax, o.tile);
     for (int tile = tmax; tile >= 1; --tile) {
         double best_cost = 1e30;
@@ -638,15 +660,29 @@ bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
             for (int w = 1; w <= 4; ++w) {
                 const int ns = (tile + w - 1) / w;   // NS scenarios per sequential wave, w waves
                 if (ns > nsmax || ns == tried) continue;
+                if (const char *e = getenv("FPF_RTC_NS"))
+                    if (atoi(e) > 0 && atoi(e) != ns) continue;
                 tried = ns;
-                const BankLayout lay = bank_layout(T, ns, tile);
+                // the largest slot stride that fits the LDS budget, then the layout
                 FeederDev probe{};
                 probe.n_slots = by_t[T].n_slots;
-                probe.slot_bytes = lay.sl * 16;
-                if (tiled_lds_bytes_rtc(probe, tile) > 160 * 1024) continue;
+                probe.n_fw = (int)h.fw.size();
+                probe.temp_lds = 1;
+                int max_sl = 0;
+                for (int sl = 3 * tile; sl <= 3 * tile + 40; ++sl) {
+                    probe.slot_bytes = sl * 16;
+                    if (tiled_lds_bytes_rtc(probe, tile) <= lds_budget) max_sl = sl;
+                }
+                if (max_sl == 0) continue;
+                const BankLayout lay = bank_layout(T, ns, tile, max_sl);
+                if (lay.sl == 0) continue;
                 const int nws = (tile + ns - 1) / ns;
-                const double cost = by_t[T].S * (double)std::max(lay.s_deg, 1) * (nws > 4 ? (nws + 3) / 4 : 1) +
-                                    0.01 * T + 0.001 * nws;
+                // cycles per step of one sequential wave vs the waves sharing the CU's
+                // LDS (MI355X, 123-bus, stamps of the whole stage: 2 waves ~81, 4 ~110;
+                // tools/ubench/gen_step.py: a bare step ~50 alone, ~80 with 4 waves)
+                static const double step_cyc[5] = {0, 60, 81, 100, 110};
+                const double cost = by_t[T].S * step_cyc[std::min(nws, 4)] * (double)std::max(lay.s_deg, 1) *
+                                        (nws > 4 ? (nws + 3) / 4 : 1) + 0.01 * T;
                 if (cost < best_cost) {
                     best_cost = cost;
                     out->ts = by_t[T];
@@ -657,7 +693,7 @@ bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
             }
         }
         if (best_cost < 1e30) {
-            int n = 1024, m = 2;
+            int n = 1024 / wpc, m = 2;
             if (const char *g = getenv("FPF_RTC_GEOM")) {
                 int gn = 0, gm = 0;
                 if (sscanf(g, "%d,%d", &gn, &gm) == 2 && (gn == 256 || gn == 512 || gn == 1024) && gm >= 1 && gm <= 4) {
@@ -670,20 +706,21 @@ bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
             if (tile * nb > n * m || (tile + out->ns - 1) / out->ns > n / 64) continue;
             out->nt = n;
             out->maxt = m;
+            out->wpc = wpc;
             return true;
         }
     }
     return false;
 }
 
-RtcSpec make_rtc_spec(const HostFeeder &h, const RtcPlan &pl) {
+RtcSpec make_rtc_spec(const HostFeeder &h, const RtcPlan &pl, const fpf_opts &o) {
     RtcSpec sp;
     sp.tile = pl.tile;
     sp.nn = h.nn;
     sp.n_taps = h.n_taps;
     sp.nt = pl.nt;
     sp.maxt = pl.maxt;
-    sp.min_waves = std::max(1, 4 * 256 / pl.nt);   // <= 128 VGPRs: 4 waves per SIMD
+    sp.min_waves = std::max(1, pl.wpc * pl.nt / 256);   // waves per SIMD of wpc resident tiles
     if (const char *g = getenv("FPF_RTC_GEOM")) {
         int n = 0, m = 0, w = 0;
         if (sscanf(g, "%d,%d,%d", &n, &m, &w) == 3 && w >= 1 && w <= 8) sp.min_waves = w;
@@ -693,6 +730,18 @@ RtcSpec make_rtc_spec(const HostFeeder &h, const RtcPlan &pl) {
     sp.ns = pl.ns;
     sp.ps = pl.lay.ps;
     sp.slot = pl.lay.sl;
+    sp.exact = o.exact != 0;
+    if (const char *e = getenv("FPF_RTC_TEMP_GLOBAL")) sp.temp_lds = atoi(e) == 0;
+    if (const char *g = getenv("FPF_RTC_STAGGER")) {
+        long c = 0;
+        int sh = 8;
+        if (sscanf(g, "%ld,%d", &c, &sh) >= 1) {
+            sp.stagger = std::max(0L, c);
+            sp.stagger_shift = std::max(0, std::min(20, sh));
+        }
+    }
+    sp.full_k = true;
+    for (int p = 0; p < 3; ++p) sp.full_k = sp.full_k && h.lnum[p] + 1 >= h.nn;
     return sp;
 }
 
@@ -777,6 +826,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     if (e == hipSuccess) e = hipMalloc(&f->d_tables, blob.size());
     if (e == hipSuccess) e = hipMemcpy(f->d_tables, blob.data(), blob.size(), hipMemcpyHostToDevice);
     e = e == hipSuccess ? hipMalloc(&f->d_agg, 8 * sizeof(double)) : e;
+    e = e == hipSuccess ? hipMalloc(&f->d_ticket, sizeof(unsigned)) : e;
+    e = e == hipSuccess ? hipMemset(f->d_ticket, 0, sizeof(unsigned)) : e;
     if (e != hipSuccess) {
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_HIP, std::string("feeder upload: ") + hipGetErrorString(e));
@@ -826,7 +877,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     }
     in.kernel = kern;
     if (kern == FPF_KERNEL_TILED && have_plan) {
-        const RtcSpec sp = make_rtc_spec(h, plan);
+        const RtcSpec sp = make_rtc_spec(h, plan, o);
         std::string err;
         RtcSpec sp0 = sp;
         sp0.keep_ib = false;
@@ -838,6 +889,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             d.n_slots = plan.ts.n_slots;
             d.slot_bytes = plan.lay.sl * 16;
             d.phase_bytes = plan.lay.ps * 16;
+            d.temp_lds = sp.temp_lds ? 1 : 0;
         } else {
             ctx->err = err;   // not fatal: the interpreted tiled kernel runs instead
         }
@@ -864,6 +916,8 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_vmax);
     (void)hipFree(f->d_stage);
     (void)hipFree(f->d_agg);
+    (void)hipFree(f->d_partials);
+    (void)hipFree(f->d_ticket);
     delete f;
 }
 
@@ -927,7 +981,27 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     o.loss = u.loss ? u.loss : f->d_loss;
     o.vmin = u.vmin ? u.vmin : f->d_vmin;
     o.vmax = u.vmax ? u.vmax : f->d_vmax;
+    o.agg = nullptr;
+    o.partials = nullptr;
+    o.ticket = nullptr;
     hipError_t e;
+    bool agg_done = false;
+    static const bool fused_agg = !getenv("FPF_FUSED_AGG") || atoi(getenv("FPF_FUSED_AGG")) != 0;
+    if (d_agg && fused_agg && f->info.kernel == FPF_KERNEL_TILED && f->rtc) {
+        // the specialised kernel reduces the batch aggregate in its last workgroup
+        const size_t tiles = ((size_t)n_scen + f->dev.tile - 1) / f->dev.tile;
+        if (tiles > f->partials_cap) {
+            (void)hipFree(f->d_partials);
+            f->d_partials = nullptr;
+            f->partials_cap = 0;
+            HIPCHK(ctx, hipMalloc(&f->d_partials, tiles * 8 * sizeof(double)));
+            f->partials_cap = tiles;
+        }
+        o.agg = d_agg;
+        o.partials = f->d_partials;
+        o.ticket = f->d_ticket;
+        agg_done = true;
+    }
     if (f->info.kernel == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {
             std::string err;
@@ -945,7 +1019,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         e = launch_generic(f->dev, n_scen, d_pq, f->d_scratch, f->scratch_ld, o, st);
     }
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("solve launch: ") + hipGetErrorString(e));
-    if (d_agg) {
+    if (d_agg && !agg_done) {
         e = launch_aggregate(n_scen, o.status, o.loss, o.vmin, o.vmax, f->dev.lb_v, f->dev.ub_v, d_agg, st);
         if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("aggregate launch: ") + hipGetErrorString(e));
     }
@@ -1040,7 +1114,7 @@ extern "C" long fpf_feeder_rtc_source(const double *dl, int nl, int ncols, const
     analyse_tiled(h);
     RtcPlan plan;
     if (!wants_rtc(h, o) || !plan_rtc(h, o, &plan)) return FPF_ERR_UNSUPPORTED;
-    RtcSpec sp = make_rtc_spec(h, plan);
+    RtcSpec sp = make_rtc_spec(h, plan, o);
     const char *kib = getenv("FPF_RTC_KEEP_IB");
     sp.keep_ib = kib && atoi(kib);   // default: the variant solves without PQb run
     const std::string src = rtc_source(sp);

@@ -101,6 +101,7 @@ struct FeederDev {
     int32_t n_slots;         // LDS state slots of the specialised (multi-track) layout
     int32_t slot_bytes;      // bytes per state slot of the specialised layout (padded, see fpf_api.cpp: bank_layout)
     int32_t phase_bytes;     // bytes between the phases of one slot (specialised layout)
+    int32_t temp_lds;        // specialised layout: TEMP blocks staged in LDS
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -109,6 +110,11 @@ struct OutDev {
     int32_t *iters;
     int8_t *status;
     double *loss, *vmin, *vmax;
+    // fused batch aggregate (specialised kernel): agg != NULL -> every workgroup
+    // publishes its tile's 8 partials, the last one to arrive combines them
+    double *agg;
+    double *partials;        // [grid][8]
+    unsigned *ticket;        // arrival counter, 0 between launches
 };
 
 #ifndef __HIPCC_RTC__
@@ -151,10 +157,15 @@ struct RtcSpec {
     int tile, nn, n_taps, nt;
     int maxt = 1;                         // tasks per lane
     int min_waves = 4;                    // __launch_bounds__ minimum waves per SIMD
-    int ahead = 8;                        // LDS operand lookahead of the sequential stages (steps)
+    int ahead = 2;                        // LDS operand lookahead of the sequential stages (steps; more costs registers)
     int ns = 21;                          // scenarios per sequential wave (3*T*ns <= 64)
     int ps = 0, slot = 0;                 // phase / slot strides of the state layout (16-byte units)
     bool keep_ib = true;                  // keep the last sweep's Ib for the PQb output
+    bool exact = false;                   // fpf_opts.exact: the reference's roundings
+    bool full_k = false;                  // every Lnum_p + 1 == nn: V_abc_list keeps all rows
+    bool temp_lds = true;                 // stage the TEMP blocks in LDS (else read from global)
+    long stagger = 0;                     // diagnostic (FPF_RTC_STAGGER=cycles,shift)
+    int stagger_shift = 8;
     TrackSched ts;
 };
 struct RtcKernel {

@@ -97,6 +97,34 @@ __host__ __device__ __forceinline__ cx load_current_rr(cx s, cx v) {
     return cconj(cdiv_rr(s, v));
 }
 
+// ---- fast mode (fpf_opts.exact = 0): the same quantities, fewer roundings -----
+// IL = conj(S/V) = (S.re V.re + S.im V.im, S.re V.im - S.im V.re) / |V|^2 with
+// one refined reciprocal; a few ulp from __divdc3.  |V|^2 outside
+// [2^-600, 2^600] takes the exact path.
+__host__ __device__ __forceinline__ cx load_current_fast(cx s, cx v) {
+    if (v.re == 0.0 && v.im == 0.0) return mk(0.0, 0.0);
+    const double d2 = fma(v.re, v.re, v.im * v.im);
+    if (!(d2 >= 0x1p-600 && d2 <= 0x1p600)) return cconj(cdiv(s, v));
+    const double r = dv_rcp(d2);
+    return mk(fma(s.re, v.re, s.im * v.im) * r, fma(s.re, v.im, -(s.im * v.re)) * r);
+}
+// column a of Ib(1x3) . TEMP(3x3) as fused complex multiply-adds
+__host__ __device__ __forceinline__ cx drop_col_fma(const cx tm[9], const cx ib0, const cx ib1, const cx ib2,
+                                                    int a) {
+    const cx t0 = tm[0 * 3 + a], t1 = tm[1 * 3 + a], t2 = tm[2 * 3 + a];
+    double re = fma(-t0.im, ib0.im, t0.re * ib0.re);
+    double im = fma(t0.im, ib0.re, t0.re * ib0.im);
+    re = fma(t1.re, ib1.re, re);
+    re = fma(-t1.im, ib1.im, re);
+    im = fma(t1.re, ib1.im, im);
+    im = fma(t1.im, ib1.re, im);
+    re = fma(t2.re, ib2.re, re);
+    re = fma(-t2.im, ib2.im, re);
+    im = fma(t2.re, ib2.im, im);
+    im = fma(t2.im, ib2.re, im);
+    return mk(re, im);
+}
+
 // Load current of one phase, DPF_return7.cpp:117-125:
 //   abs(v) == 0 ? 0 : conj(S / v)
 __host__ __device__ __forceinline__ cx load_current(cx s, cx v) {
@@ -139,6 +167,18 @@ __device__ __forceinline__ void load_temp(const double *t, cx tm[9]) {
         const double2 v = g[i];
         tm[i] = mk(v.x, v.y);
     }
+}
+
+// element i of a double2 table in global memory (global_load_dwordx4, see load_temp)
+__device__ __forceinline__ double2 ld_global2(const double *t, int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+    typedef const __attribute__((address_space(1))) double2 gd2;
+    const gd2 *g = (const gd2 *)t;
+    const double x = g[i].x, y = g[i].y;
+    return make_double2(x, y);
+#else
+    return ((const double2 *)t)[i];
+#endif
 }
 
 // drop_col on TEMP values held in registers, tm[L*3 + a] = TEMP(L, a)

@@ -86,6 +86,15 @@ std::string gen_program(const RtcSpec &sp) {
       << "  static constexpr int kSlotBytes = " << SL * 16 << ";\n"
       << "  static constexpr int kPhaseBytes = " << PS * 16 << ";\n"
       << "  static constexpr bool kKeepIb = " << (sp.keep_ib ? "true" : "false") << ";\n"
+      << "  static constexpr bool kExact = " << (sp.exact ? "true" : "false") << ";\n"
+      << "  static constexpr bool kTempLds = " << (sp.temp_lds ? "true" : "false") << ";\n"
+      << "  static constexpr bool kFullK = " << (sp.full_k ? "true" : "false") << ";\n"
+      << "  static constexpr long kStagger = " << sp.stagger << ";\n"
+      << "  static constexpr int kStaggerShift = " << sp.stagger_shift << ";\n"
+      << "  static constexpr short kSlotOf[" << sp.nn << "] = {";
+    for (int k = 0; k < sp.nn; ++k) o << (k ? ", " : "") << ts.slot(k);
+    o << "};\n"
+      << "  __device__ static __forceinline__ int node_slot(const FeederDev &, int k) { return kSlotOf[k]; }\n"
       << "  static constexpr bool kLdsProgram = false;\n"
       << "  static constexpr bool kLdsTaps = false;\n"
       << "  __device__ static __forceinline__ cx ld(const double2 *B, long i) { const double2 v = B[i]; return mk(v.x, v.y); }\n"

@@ -45,7 +45,10 @@ int threads_for(const FeederDev &f, int tile) { return tiled_threads(f, tile); }
 
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile) {
     const size_t slot = f.slot_bytes > 0 ? (size_t)f.slot_bytes : sizeof(double2) * 3 * (size_t)tile;
-    return slot * (size_t)f.n_slots + sizeof(Flags);
+    const size_t state = (slot * (size_t)f.n_slots + sizeof(Flags) + 15) & ~(size_t)15;
+    // + the TEMP blocks staged in LDS; after the sweeps the same bytes hold the
+    // tile's aggregate rows (8 doubles per scenario)
+    return state + std::max(f.temp_lds ? 144 * (size_t)f.n_fw : 0, (size_t)64 * MAX_SEQ_TILE);
 }
 
 size_t tiled_lds_bytes(const FeederDev &f, int tile) {

@@ -183,8 +183,10 @@ class PowerFlow:
         fs, fa = L.fpf_solve_batch_device, L.fpf_aggregate_device
         keep = (o,)
 
-        def solve():
-            rc = fs(h, B, pq_p, o_ref, None, st)
+        def solve(agg=None):
+            """One device solve; with agg (8 float64 on the device) the batch
+            aggregate is produced by the same launch (specialised kernel)."""
+            rc = fs(h, B, pq_p, o_ref, None if agg is None else C.c_void_p(_ptr(agg)), st)
             if rc < 0:
                 raise DPFError(rc, self.ctx.err())
 

@@ -85,7 +85,13 @@ typedef struct fpf_opts {
     int    tile;       /* scenarios per workgroup for the tiled kernel, 0 = auto */
     int    specialize; /* 1 (default): compile the tiled kernel for the feeder's topology
                           with hipRTC at fpf_feeder_create; 0: interpret its programs */
-    int    reserved[6];
+    int    exact;      /* 1: the specialised kernel repeats the reference's roundings
+                          (complex divide as libgcc __divdc3, no FMA): V, PQb, PQL, loss
+                          bit-identical to the oracle.  0 (default): load currents as
+                          conj(S)V/|V|^2 and the branch products with FMA -- within a few
+                          ulp (north-star bar: 1e-10 relative on V, same iteration counts).
+                          The generic and interpreted kernels are always exact. */
+    int    reserved[5];
 } fpf_opts;
 
 typedef struct fpf_feeder_info {
