@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--exact", type=int, default=0, help="1: the reference's roundings (bit-identical mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-v-out", action="store_true", help="diagnostic: do not request the V outputs")
     args = ap.parse_args()
 
     import torch
@@ -129,6 +130,8 @@ def main():
            "vmax": torch.zeros(B, dtype=torch.float64, device=dev),
            "v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
            "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
+    if args.no_v_out:
+        del out["v_re"], out["v_im"]
     stream = torch.cuda.current_stream(dev)
     agg_all = torch.zeros((max(args.steps, 1) + args.warmup, 8), dtype=torch.float64, device=dev)
     agg_ptr = [agg_all[i] for i in range(agg_all.shape[0])]
@@ -210,7 +213,8 @@ def main():
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "dpf_tiled_kernel" if pf.kernel == "tiled" else "dpf_generic_kernel",
+                         "kernel": {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
+                                    "wave": "dpf_wave_kernel", "generic": "dpf_generic_kernel"}[pf.kernel],
                          "bytes_alg_per_scenario": bpa, "kernel_ms": avg_kern_s * 1e3},
             "aggregate": {"loss_sum_kw": float(tot[0]), "vmin": float(tot[1]), "vmax": float(tot[2]),
                           "n_conv": int(tot[3]), "n_nonconv": int(tot[4]), "n_over": int(tot[5]),

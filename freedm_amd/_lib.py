@@ -15,8 +15,8 @@ LIB_PATH = os.path.join(HERE, "lib", "libfreedm_pf.so")
 
 FPF_OK, FPF_ERR_ARG, FPF_ERR_TOPOLOGY, FPF_ERR_HIP, FPF_ERR_NOMEM, FPF_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
 FPF_CONVERGED, FPF_NONCONVERGED = 0, 1
-FPF_KERNEL_AUTO, FPF_KERNEL_GENERIC, FPF_KERNEL_TILED = 0, 1, 2
-KERNELS = {"auto": FPF_KERNEL_AUTO, "generic": FPF_KERNEL_GENERIC, "tiled": FPF_KERNEL_TILED}
+FPF_KERNEL_AUTO, FPF_KERNEL_GENERIC, FPF_KERNEL_TILED, FPF_KERNEL_WAVE = 0, 1, 2, 3
+KERNELS = {"auto": FPF_KERNEL_AUTO, "generic": FPF_KERNEL_GENERIC, "tiled": FPF_KERNEL_TILED, "wave": FPF_KERNEL_WAVE}
 
 EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_destroy", "fpf_last_error",
            "fpf_feeder_create", "fpf_feeder_destroy", "fpf_feeder_get_info", "fpf_feeder_reserve",

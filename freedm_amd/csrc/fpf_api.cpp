@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -62,6 +63,9 @@ struct fpf_feeder {
     RtcKernel rtc_kernel_ib{};   // with PQb: built on the first solve that asks for it
     bool rtc_ib = false;
     RtcSpec rtc_spec;
+    // wave kernel (fast mode)
+    void *d_wave = nullptr;
+    WaveDev wdev{};
 };
 
 static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
@@ -353,6 +357,137 @@ void analyse_tiled(HostFeeder &h) {
     }
     h.depth = d;
     h.wf = true;
+}
+
+// Tables of the wave kernel (fpf_wave.hip).  Accepts well-formed feeders of at
+// most 256 branches whose backward chains are the feeder tree: a branch row
+// that follows another branch row starts at that row's receiving bus, so the
+// Ib the backward sweep hands up a block (DPF_return7.cpp:147-157) flows to the
+// node's forward source (:176-178) -- the sweep then computes subtree sums.
+struct WaveHost {
+    bool ok = false;
+    std::string why;
+    int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0;
+    std::vector<int32_t> row, node, info, mref, pairs;
+    std::vector<double> temp;
+};
+
+void analyse_wave(const HostFeeder &h, WaveHost &w) {
+    auto no = [&](const std::string &why) { w.ok = false; w.why = why; };
+    if (!h.wf) return no("not well formed: " + h.wf_why);
+    const int nl = h.nl, nn = h.nn, n = nn - 1;
+    int spw = 0, C = 0;
+    if (!wave_geometry(n, &spw, &C)) return no("more than 256 branches");
+    const int L = 64 / spw;
+    std::vector<int> par(nn, -1), chain(nn, -1);
+    std::vector<std::vector<int>> lat(nn);
+    for (int m = 0; m < nl; ++m) {
+        if (h.at(m, 0) == 0) continue;
+        const int k = (int)h.at(m, 2), src = m == 0 ? 0 : (int)h.at(m, 1);
+        par[k] = src;
+        if (m == 0) continue;
+        if (h.at(m - 1, 0) != 0) {
+            if ((int)h.at(m - 1, 2) != src)
+                return no("row " + std::to_string(m) + ": the backward chain leaves the feeder tree");
+            chain[src] = k;
+        } else {
+            lat[src].push_back(k);
+        }
+    }
+    // depth-first order, in-block child first: blocks and subtrees are contiguous
+    std::vector<int> pos(nn, -1), at, blk(nn, 0), size(nn, 1), bfirst;
+    std::vector<int> st = {1};
+    bfirst.push_back(1);
+    while (!st.empty()) {
+        const int k = st.back();
+        st.pop_back();
+        pos[k] = (int)at.size();
+        at.push_back(k);
+        for (int l : lat[k]) {
+            blk[l] = (int)bfirst.size();
+            bfirst.push_back(l);
+            st.push_back(l);
+        }
+        if (chain[k] >= 0) {
+            blk[chain[k]] = blk[k];
+            st.push_back(chain[k]);
+        }
+    }
+    if ((int)at.size() != n) return no("feeder tree does not reach every node from node 1");
+    for (int q = n - 1; q > 0; --q) size[par[at[q]]] += size[at[q]];
+    const int nblk = (int)bfirst.size();
+    if (nblk > 511) return no("too many blocks");
+    // nearest zeroed proper ancestor per (node, phase)
+    std::vector<std::array<int, 3>> mref(nn, {-1, -1, -1});
+    int has_rel = 0, has_mask = 0;
+    for (int k = 1; k < nn; ++k) {
+        if (h.node[k].mask & 7) has_mask = 1;
+        for (int p = 0; p < 3; ++p) {
+            if ((h.node[k].mask >> p) & 1) continue;
+            for (int a = par[k]; a >= 1; a = par[a])
+                if ((h.node[a].mask >> p) & 1) {
+                    mref[k][p] = a;
+                    has_rel = 1;
+                    break;
+                }
+        }
+    }
+    // positions whose scan values other slots gather: subtree ends (backward),
+    // taps and the positions before lateral blocks (forward), zeroed ancestors
+    std::vector<int> comp(n, -1);
+    int ncomp = 0;
+    auto need = [&](int q) { if (comp[q] < 0) comp[q] = ncomp++; };
+    for (int q = 0; q < n; ++q) need(q + size[at[q]] - 1);
+    for (int b = 1; b < nblk; ++b) {
+        need(pos[par[bfirst[b]]]);
+        need(pos[bfirst[b]] - 1);
+    }
+    for (int k = 1; k < nn; ++k)
+        for (int p = 0; p < 3; ++p)
+            if (mref[k][p] >= 1) need(pos[mref[k][p]]);
+    if (ncomp > 510) return no("too many gathered positions");
+    // off(b) = sum over b's block-ancestor chain of Ginc[tap] - Ginc[first - 1]
+    std::vector<std::vector<std::pair<int, int>>> chainp(nblk);
+    int bdepth = 0;
+    for (int b = 1; b < nblk; ++b) {
+        for (int j = b; j != 0; j = blk[par[bfirst[j]]])
+            chainp[b].push_back({comp[pos[par[bfirst[j]]]], comp[pos[bfirst[j]] - 1]});
+        bdepth = std::max(bdepth, (int)chainp[b].size());
+    }
+    w.pairs.assign((size_t)std::max(bdepth, 1) * 2 * nblk, ncomp);
+    for (int b = 1; b < nblk; ++b)
+        for (size_t j = 0; j < chainp[b].size(); ++j) {
+            w.pairs[(2 * j) * nblk + b] = chainp[b][j].first;
+            w.pairs[(2 * j + 1) * nblk + b] = chainp[b][j].second;
+        }
+    const size_t S = (size_t)C * L;
+    w.row.assign(S, -1);
+    w.node.assign(S, -1);
+    w.info.assign(S, (ncomp << 13));   // empty slot: gathers the zero entry, block 0
+    w.mref.assign(3 * S, -1);
+    w.temp.assign(9 * S * 2, 0.0);
+    for (int q = 0; q < n; ++q) {
+        const int k = at[q], c = q % C, lane = q / C, i = c * L + lane;
+        const NodeOp &nd = h.node[k];
+        w.row[i] = nd.row;
+        w.node[i] = k;
+        w.info[i] = (nd.mask & 7) | 8 | ((comp[q] + 1) << 4) | (comp[q + size[k] - 1] << 13) | (blk[k] << 22);
+        for (int p = 0; p < 3; ++p)
+            if (mref[k][p] >= 1) w.mref[(p * C + c) * L + lane] = comp[pos[mref[k][p]]];
+        for (int j = 0; j < 9; ++j) {
+            w.temp[((j * C + c) * L + lane) * 2 + 0] = h.tz[(size_t)nd.fw * 18 + 2 * j];
+            w.temp[((j * C + c) * L + lane) * 2 + 1] = h.tz[(size_t)nd.fw * 18 + 2 * j + 1];
+        }
+    }
+    w.n = n;
+    w.spw = spw;
+    w.C = C;
+    w.nblk = nblk;
+    w.bdepth = bdepth;
+    w.ncomp = ncomp;
+    w.has_rel = has_rel;
+    w.has_mask = has_mask;
+    w.ok = true;
 }
 
 // Chunked sequential programs for one tile size (see fpf_internal.h).
@@ -780,8 +915,17 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     if (why.empty()) why = build_lnum(h, z, z_rows, o);
     if (!why.empty()) return fail(ctx, FPF_ERR_TOPOLOGY, "feeder rejected (the reference would throw): " + why);
     analyse_tiled(h);
+    WaveHost wh;
+    analyse_wave(h, wh);
+    // kernel choice: the wave kernel for fast mode, the tiled kernel for exact
+    // mode (or a feeder the wave kernel refuses), the generic kernel otherwise
+    int kern = o.kernel;
+    if (kern == FPF_KERNEL_AUTO && !o.exact && wh.ok) kern = FPF_KERNEL_WAVE;
+    if (kern == FPF_KERNEL_WAVE && (!wh.ok || o.exact))
+        return fail(ctx, FPF_ERR_UNSUPPORTED,
+                    o.exact ? "wave kernel: fast mode only (exact = 0)" : "wave kernel: " + wh.why);
     RtcPlan plan;
-    const bool have_plan = wants_rtc(h, o) && plan_rtc(h, o, &plan);
+    const bool have_plan = kern != FPF_KERNEL_WAVE && wants_rtc(h, o) && plan_rtc(h, o, &plan);
     if (have_plan) {
         h.ts = plan.ts;
         h.node_rtc = node_table_rtc(h, plan.ts);
@@ -867,8 +1011,48 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     d.prog_lds = 1;
     if (tile >= 1 && tiled_lds_bytes(d, tile) > 160 * 1024) d.prog_lds = 0;   // programs stay in HBM/L2
 
-    // kernel choice
-    int kern = o.kernel;
+    if (kern == FPF_KERNEL_WAVE) {
+        WaveDev &w = f->wdev;
+        std::vector<char> wb;
+        const size_t o_row = push_blob(wb, wh.row), o_node = push_blob(wb, wh.node), o_info = push_blob(wb, wh.info);
+        const size_t o_mref = push_blob(wb, wh.mref);
+        const size_t o_tmp = push_blob(wb, wh.temp), o_pairs = push_blob(wb, wh.pairs);
+        e = hipMalloc(&f->d_wave, wb.size());
+        if (e == hipSuccess) e = hipMemcpy(f->d_wave, wb.data(), wb.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            fpf_feeder_destroy(f);
+            return fail(ctx, FPF_ERR_HIP, std::string("wave tables upload: ") + hipGetErrorString(e));
+        }
+        char *wbase = (char *)f->d_wave;
+        w.n = wh.n;
+        w.nn = h.nn;
+        w.nl = nl;
+        w.spw = wh.spw;
+        w.C = wh.C;
+        w.nblk = wh.nblk;
+        w.bdepth = wh.bdepth;
+        w.ncomp = wh.ncomp;
+        w.has_rel = wh.has_rel;
+        w.has_mask = wh.has_mask;
+        w.dbg = getenv("FPF_WAVE_DBG") ? atoi(getenv("FPF_WAVE_DBG")) : 0;
+        w.mxitr = o.mxitr;
+        for (int p = 0; p < 3; ++p) w.K[p] = d.K[p];
+        for (int i = 0; i < 6; ++i) w.V0[i] = d.V0[i];
+        w.s3 = d.s3;
+        w.eps = d.eps;
+        w.lb_v = d.lb_v;
+        w.ub_v = d.ub_v;
+        w.slot_row = (const int32_t *)(wbase + o_row);
+        w.slot_node = (const int32_t *)(wbase + o_node);
+        w.slot_info = (const int32_t *)(wbase + o_info);
+        w.slot_mref = (const int32_t *)(wbase + o_mref);
+        w.slot_temp = (const double *)(wbase + o_tmp);
+        w.blk_pairs = (const int32_t *)(wbase + o_pairs);
+        if (wave_lds_bytes(w) > 160 * 1024) {
+            fpf_feeder_destroy(f);
+            return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
+        }
+    }
     if (kern == FPF_KERNEL_AUTO) kern = (h.wf && (tile >= 1 || have_plan)) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
     if (kern == FPF_KERNEL_TILED && (!h.wf || (tile < 1 && !have_plan))) {
         fpf_feeder_destroy(f);
@@ -898,7 +1082,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_UNSUPPORTED, "specialised kernel failed and the interpreted one does not fit: " + ctx->err);
     }
-    in.tile = kern == FPF_KERNEL_TILED ? d.tile : 0;
+    in.tile = kern == FPF_KERNEL_TILED ? d.tile : (kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : 0);
     in.specialized = f->rtc ? 1 : 0;
     *out = f;
     return FPF_OK;
@@ -918,6 +1102,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_agg);
     (void)hipFree(f->d_partials);
     (void)hipFree(f->d_ticket);
+    (void)hipFree(f->d_wave);
     delete f;
 }
 
@@ -987,9 +1172,11 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     hipError_t e;
     bool agg_done = false;
     static const bool fused_agg = !getenv("FPF_FUSED_AGG") || atoi(getenv("FPF_FUSED_AGG")) != 0;
-    if (d_agg && fused_agg && f->info.kernel == FPF_KERNEL_TILED && f->rtc) {
-        // the specialised kernel reduces the batch aggregate in its last workgroup
-        const size_t tiles = ((size_t)n_scen + f->dev.tile - 1) / f->dev.tile;
+    const bool fuses_agg = (f->info.kernel == FPF_KERNEL_TILED && f->rtc) || f->info.kernel == FPF_KERNEL_WAVE;
+    if (d_agg && fused_agg && fuses_agg) {
+        // the specialised and wave kernels reduce the batch aggregate in their last workgroup
+        const int per = f->info.kernel == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : f->dev.tile;
+        const size_t tiles = ((size_t)n_scen + per - 1) / per;
         if (tiles > f->partials_cap) {
             (void)hipFree(f->d_partials);
             f->d_partials = nullptr;
@@ -1002,7 +1189,9 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         o.ticket = f->d_ticket;
         agg_done = true;
     }
-    if (f->info.kernel == FPF_KERNEL_TILED) {
+    if (f->info.kernel == FPF_KERNEL_WAVE) {
+        e = launch_wave(f->wdev, n_scen, d_pq, o, st);
+    } else if (f->info.kernel == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {
             std::string err;
             if (rtc_build(ctx->device, f->rtc_spec, &f->rtc_kernel_ib, &err) != 0)

@@ -104,6 +104,34 @@ struct FeederDev {
     int32_t temp_lds;        // specialised layout: TEMP blocks staged in LDS
 };
 
+// Wave kernel (fpf_wave.hip, fast mode): SPW scenarios per wavefront, one
+// segment of L = 64/SPW lanes per scenario, state in registers, both sweeps as
+// segment-wide prefix scans over a depth-first order of the feeder tree in
+// which every block (Dl row run between separators) is contiguous.  Node at
+// position q (0..n-1) lives in slot c = q % C of segment lane q / C; per-slot
+// tables are segment-lane-major, index (field*C + c)*L + lane.  Only the scan
+// values other slots read (subtree ends, taps, zeroed ancestors) go through
+// LDS, at a compact index.
+struct WaveDev {
+    int32_t n, nn, nl;       // branches (= nodes - 1), nodes, Dl rows
+    int32_t spw, C;          // scenarios per wave, slots per lane
+    int32_t nblk, bdepth;    // blocks, block-ancestor pairs of the deepest block
+    int32_t ncomp;           // gathered positions (compact scan array; entry ncomp = 0)
+    int32_t has_rel;         // some unmasked (node, phase) below a zeroed ancestor
+    int32_t has_mask;        // some (node, phase) zeroed
+    int32_t mxitr;
+    int32_t K[3];            // Lnum_p + 1 (V_abc_list.cpp:12-17)
+    int32_t dbg;             // diagnostic ablations (FPF_WAVE_DBG; results are wrong when set)
+    double V0[6], s3, eps, lb_v, ub_v;
+    const int32_t *slot_row;    // [C][L] Dl row of the slot's node (-1: empty slot)
+    const int32_t *slot_node;   // [C][L] node id
+    const int32_t *slot_info;   // [C][L] bits 0-2 zero mask, 3 valid, 4-12 compact index + 1,
+                                //        13-21 compact index of the subtree's last node, 22-30 block
+    const int32_t *slot_mref;   // [3][C][L] compact index of the nearest zeroed proper ancestor, -1 none
+    const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch
+    const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) compact indices; pad = ncomp (zero)
+};
+
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
 struct OutDev {
     double *vpolar, *pqb, *pql, *v_re, *v_im;
@@ -125,6 +153,10 @@ hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const 
 hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss,
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
                             double *d_agg, hipStream_t st);
+hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+size_t wave_lds_bytes(const WaveDev &w);
+bool wave_geometry(int n, int *spw, int *c);
+int wave_scenarios_per_block(const WaveDev &w);
 size_t tiled_lds_bytes(const FeederDev &f, int tile);
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile);
 int tiled_max_tile(const FeederDev &f);

@@ -1,0 +1,669 @@
+// fpf_wave.hip -- the wave kernel (fast mode, fpf_opts.exact = 0): every sweep
+// of DPF_return7 (Broker/src/vvc/DPF_return7.cpp:104-217) as data-parallel work
+// over a segment of L = 64/SPW lanes per scenario, SPW scenarios per wavefront.
+//
+// The feeder tree (node k's parent = sbus of its row; for the feeders this
+// kernel accepts this is also the node that receives Ib(k) in the backward
+// sweep, :134-160) is laid out in a depth-first order that visits a node's
+// in-block child before its laterals, so
+//   * every subtree is a contiguous range of positions  -> the backward sweep
+//       Ib(k) = sum of IL over the subtree of k = Einc[last(k)] - Eexc[pos(k)]
+//     is one segment-wide prefix scan E of IL plus one gather;
+//   * every block (Dl row run between separator rows) is a contiguous range
+//     -> the forward sweep V(k) = V(src) - drop(k) (:163-195), i.e.
+//       V(k) = V0 - A(k), A(k) = sum of drops on the path 1..k,
+//     is one prefix scan G of the drops: A(k) = Ginc[pos(k)] + off(block(k)),
+//     off(b) = sum over b's block-ancestor chain of (Ginc[tap] - Ginc[first-1]),
+//     resolved by one lane per block.
+// Phase zeroing (:180-192): V(k,p) = 0 on a zeroed phase, and below a zeroed
+// ancestor m the path restarts from 0: V(k,p) = A(m) - A(k).
+//
+// Node at position q lives in slot c = q % C of segment lane q / C; its state
+// (Sld, V, IL, Ib) stays in registers for the whole solve.  LDS holds, per
+// scenario, the scan array (X, [3][L*C+1] complex, slot-major so a lane's
+// stores are conflict-free; entry L*C is a permanent zero) and the block
+// offsets, and once per workgroup the TEMP blocks (lng * Z/Zb, 9 complex per
+// branch) and the block-chain table.  Scans are DPP row shifts (+ row
+// broadcasts for L = 32, 64) on the fp64 halves; segments never read each
+// other's lanes.  A scenario's outputs are written in the sweep it converges
+// in (or its 20th); its lanes then idle along until the wave's last scenario
+// is done.
+//
+// Arithmetic: the quantities of the reference with a different association
+// (prefix sums instead of the sequential chains, FMA products, one-reciprocal
+// division, Sld scaled by 1/(bkva/3)): a few ulp per operation, checked at the
+// north-star bar (1e-10 relative on V, identical iteration counts) in
+// tests/test_gpu_parity.py.  Voltages are per-unit: |V|^2 must stay a normal
+// double (a solve that diverges past 1e+-150 p.u. gets non-finite values; its
+// status is NONCONVERGED either way).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+
+namespace fpf {
+
+// diagnostic ablation build (make ablate): FPF_WAVE_DBG bits switch pieces off;
+// results are wrong when set.  Compiled out of the product.
+#ifdef FPF_WAVE_ABLATE
+#define DBG(bit) (f.dbg & (bit))
+#else
+#define DBG(bit) 0
+#endif
+
+#ifdef FPF_STAMPS
+// diagnostic build only: lane 0 of each of the first 64 wavefronts records
+// s_memtime at stage boundaries (never read by the kernel itself)
+__device__ unsigned long long *fpf_wave_stamp_buf = nullptr;
+#define WSTAMP(idx)                                                                                   \
+    do {                                                                                              \
+        const int gw_ = blockIdx.x * WPB + (threadIdx.x >> 6);                                         \
+        if (fpf_wave_stamp_buf && (threadIdx.x & 63) == 0 && gw_ < 64 && (idx) < 64)                   \
+            fpf_wave_stamp_buf[gw_ * 64 + (idx)] = __builtin_amdgcn_s_memtime();                        \
+    } while (0)
+extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr) {
+    unsigned long long *p = (unsigned long long *)dptr;
+    return hipMemcpyToSymbol(HIP_SYMBOL(fpf_wave_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#else
+#define WSTAMP(idx) ((void)0)
+#endif
+
+namespace {
+
+// DPP move of one fp64 value (two 32-bit halves); lanes without a source read 0
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_d(double x) {
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, true);
+    const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, BM, true);
+    return __hiloint2double(h2, l2);
+}
+
+// inclusive scan within segments of L lanes: row_shr 1, 2, 4, 8 within rows of
+// 16, then row_bcast:15 (rows 1, 3) for L >= 32 and row_bcast:31 (rows 2, 3) for L = 64
+template <int L>
+__device__ __forceinline__ double seg_incl(double x) {
+    x += dpp_d<0x111, 0xf, 0xf>(x);
+    x += dpp_d<0x112, 0xf, 0xf>(x);
+    x += dpp_d<0x114, 0xf, 0xf>(x);
+    x += dpp_d<0x118, 0xf, 0xf>(x);
+    if (L >= 32) x += dpp_d<0x142, 0xa, 0xf>(x);
+    if (L >= 64) x += dpp_d<0x143, 0xc, 0xf>(x);
+    return x;
+}
+
+// the value of the segment's last lane
+template <int L>
+__device__ __forceinline__ double seg_last(double x, int seg) {
+    if (L == 64) {
+        const int lo = __builtin_amdgcn_readlane(__double2loint(x), 63);
+        const int hi = __builtin_amdgcn_readlane(__double2hiint(x), 63);
+        return __hiloint2double(hi, lo);
+    }
+    return __shfl(x, seg * L + L - 1, 64);
+}
+
+template <int L>
+__device__ __forceinline__ double seg_sum(double x) {
+#pragma unroll
+    for (int m = L / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+template <int L>
+__device__ __forceinline__ double seg_min(double x) {
+#pragma unroll
+    for (int m = L / 2; m >= 1; m >>= 1) x = fmin(x, __shfl_xor(x, m, 64));
+    return x;
+}
+template <int L>
+__device__ __forceinline__ double seg_max(double x) {
+#pragma unroll
+    for (int m = L / 2; m >= 1; m >>= 1) x = fmax(x, __shfl_xor(x, m, 64));
+    return x;
+}
+
+// LDS ordering between the lanes of one wave: a wave's DS operations execute in
+// order; the fence keeps the compiler from moving them across
+__device__ __forceinline__ void wfence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+__device__ __forceinline__ cx ldx(const double2 *X, int i) {
+    const double2 v = X[i];
+    return mk(v.x, v.y);
+}
+__device__ __forceinline__ void stx(double2 *X, int i, cx v) { X[i] = make_double2(v.re, v.im); }
+
+// IL = conj(S/V) = conj(S) V / |V|^2 with one refined reciprocal; 0 when V == 0
+// (:117-125) -- a voltage is exactly 0 only on a zeroed phase, so feeders
+// without zeroed phases (ZERO = false) skip the test
+template <bool ZERO>
+__device__ __forceinline__ cx il_fast(cx s, cx v) {
+    const double d2 = fma(v.re, v.re, v.im * v.im);
+    double r = dv_rcp(d2);
+    if (ZERO) r = d2 == 0.0 ? 0.0 : r;
+    return mk(fma(s.re, v.re, s.im * v.im) * r, fma(s.re, v.im, -(s.im * v.re)) * r);
+}
+
+// Outputs of node k, phase p (DPF_return7.cpp:222-253); returns (Re SL, |V|)
+__device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn, int B, int k, int p, size_t s, cx v,
+                                             cx il, cx ib) {
+    const cx sv = cmul(v, mk(s3, 0.0));
+    const cx sl = cmul(sv, cconj(il));
+    const cx sb = cmul(sv, cconj(ib));
+    const double mag = sqrt(fma(v.re, v.re, v.im * v.im));
+    const size_t o6 = ((size_t)(2 * p) * nn + k) * B + s, o6i = o6 + (size_t)nn * B;
+    if (o.vpolar) { o.vpolar[o6] = mag; o.vpolar[o6i] = polar_angle(v, p); }
+    if (o.pqb) { o.pqb[o6] = sb.re; o.pqb[o6i] = sb.im; }
+    if (o.pql) { o.pql[o6] = sl.re; o.pql[o6i] = sl.im; }
+    if (o.v_re) o.v_re[((size_t)p * nn + k) * B + s] = v.re;
+    if (o.v_im) o.v_im[((size_t)p * nn + k) * B + s] = v.im;
+    return make_double2(sl.re, mag);
+}
+}  // namespace
+
+// packed per-slot info (fpf_api.cpp: analyse_wave)
+__device__ __forceinline__ int si_mask(int x) { return x & 7; }
+__device__ __forceinline__ bool si_valid(int x) { return (x >> 3) & 1; }
+__device__ __forceinline__ int si_comp(int x) { return ((x >> 4) & 511) - 1; }   // -1: not gathered
+__device__ __forceinline__ int si_last(int x) { return (x >> 13) & 511; }
+__device__ __forceinline__ int si_blk(int x) { return (x >> 22) & 511; }
+
+template <int SPW, int C>
+struct WaveGeom {
+    static constexpr int L = 64 / SPW;                 // lanes per scenario
+    static constexpr int WPB = SPW * C <= 2 ? 16 : 8;  // wavefronts per workgroup
+    static constexpr int MINW = SPW * C <= 2 ? 4 : 2;  // waves per SIMD the registers allow
+    static constexpr int SPB = WPB * SPW;              // scenarios per workgroup
+};
+
+// segment-wide reductions by the DPP scan pattern; the segment's last lane holds
+// the result.  Lanes without a source keep +inf (bound_ctrl off, old = +inf).
+template <int CT>
+__device__ __forceinline__ double dpp_min_step(double v) {
+    constexpr int RM = CT == 0x142 ? 0xa : (CT == 0x143 ? 0xc : 0xf);
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CT, RM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0x7ff00000, __double2hiint(v), CT, RM, 0xf, false);
+    return fmin(v, __hiloint2double(hi, lo));
+}
+template <int L>
+__device__ __forceinline__ double seg_reduce_min(double x) {
+    x = dpp_min_step<0x111>(x);
+    x = dpp_min_step<0x112>(x);
+    x = dpp_min_step<0x114>(x);
+    x = dpp_min_step<0x118>(x);
+    if (L >= 32) x = dpp_min_step<0x142>(x);
+    if (L >= 64) x = dpp_min_step<0x143>(x);
+    return x;
+}
+template <int L>
+__device__ __forceinline__ double seg_reduce_max(double x) { return -seg_reduce_min<L>(-x); }
+
+template <int SPW, int C, bool FULL>
+__global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
+    WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
+    constexpr int L = WaveGeom<SPW, C>::L, WPB = WaveGeom<SPW, C>::WPB, SPB = WaveGeom<SPW, C>::SPB;
+    constexpr int NT = WPB * 64;
+    extern __shared__ double2 lds[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int seg = lane / L, li = lane % L;
+    const int sc = wv * SPW + seg;                 // scenario within the workgroup
+    const int s0 = blockIdx.x * SPB, s = s0 + sc;
+    const int nsb = min(SPB, B - s0);              // scenarios of this workgroup
+    const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
+    // LDS: per workgroup the TEMP blocks and the block-chain table; per scenario
+    // Sld (later V in node order), the gathered scan values X ([3][XC], entry XC-1
+    // = 0) and the block offsets
+    double2 *const tl = lds;                                          // [9][C][L]
+    int *const pairs = (int *)(tl + 9 * C * L);                       // [bdepth][2][nblk]
+    const int pair_n = (2 * bdepth * nblk + 3) & ~3;
+    double2 *const reg0 = (double2 *)(pairs + pair_n);               // per-scenario regions
+    const int RS = 3 * C * L + 3 * XC + 3 * nblk;                    // double2 per region
+    double2 *const SL = reg0 + sc * RS;
+    double2 *const X = SL + 3 * C * L;
+    double2 *const OFF = X + 3 * XC;
+    const bool live = sc < nsb;
+
+    // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced, staged over the
+    // per-scenario regions; then each slot picks its row
+    {
+        double *stage = (double *)reg0;   // [6][nl][SPB]
+        for (int i = threadIdx.x; i < 9 * C * L; i += NT) tl[i] = ld_global2(f.slot_temp, i);
+        for (int i = threadIdx.x; i < 2 * bdepth * nblk; i += NT) pairs[i] = f.blk_pairs[i];
+        for (int i = threadIdx.x; i < (DBG(256) ? 0 : 6 * nl * SPB); i += NT) {
+            const int j = i % SPB, fr = i / SPB;
+            stage[i] = j < nsb ? __builtin_nontemporal_load(pq + (size_t)fr * B + s0 + j) : 0.0;
+        }
+    }
+    __syncthreads();
+    const double inv_s3 = 1.0 / f.s3;
+    int si[C];
+    double2 sld_in[C][3];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int i = c * L + li;
+        const int row = f.slot_row[i];
+        si[c] = f.slot_info[i];
+        const double *stage = (const double *)reg0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            // Sld = (P + jQ) / (bkva/3)  (:46-50)
+            sld_in[c][p] = make_double2(0.0, 0.0);
+            if (row >= 0)
+                sld_in[c][p] = make_double2(stage[((2 * p) * nl + row) * SPB + sc] * inv_s3,
+                                            stage[((2 * p + 1) * nl + row) * SPB + sc] * inv_s3);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) SL[(p * C + c) * L + li] = sld_in[c][p];
+    if (li < 3) X[li * XC + XC - 1] = make_double2(0.0, 0.0);
+    // per-scenario results for the workgroup aggregate: [sc][loss, vmin, vmax, status]
+    __shared__ double res[SPB][4];
+
+    const cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+    cx v[C][3];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
+
+    // A scenario's results are recorded in its last sweep (converged, or the
+    // mxitr-th); its lanes then sweep along without storing until the wave's
+    // last scenario is done.
+    cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    bool done = !live;
+    for (int it = 0; __ballot(!done) != 0; ++it) {
+        // ---- load currents (:106-130)
+        cx il[C][3], ib[C][3];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(SL, (p * C + c) * L + li), v[c][p]);
+
+        // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of IL;
+        // Einc is gathered at subtree ends only (leaves)
+        cx tot[3], exl[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = il[0][p];
+            ib[0][p] = acc;
+#pragma unroll
+            for (int c = 1; c < C; ++c) { acc = cadd(acc, il[c][p]); ib[c][p] = acc; }
+            const cx inc = mk(seg_incl<L>(acc.re), seg_incl<L>(acc.im));
+            tot[p] = mk(seg_last<L>(inc.re, seg), seg_last<L>(inc.im, seg));
+            exl[p] = csub(inc, acc);   // the lane's exclusive prefix
+#pragma unroll
+            for (int c = 0; c < C; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // Einc at this slot
+        }
+        wfence();
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int ci = si_comp(si[c]);
+            if (ci >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
+            }
+        }
+        wfence();
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            // Ib = Einc[last] - Eexc; Eexc of slot c = Einc of slot c-1, of slot 0 the lane's prefix
+            cx eprev = exl[p];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const cx e = ib[c][p];
+                ib[c][p] = csub(ldx(X, p * XC + si_last(si[c])), eprev);
+                eprev = e;
+            }
+        }
+
+        // ---- convergence on the substation branch (:199-217): Ib(0) = the segment total;
+        // max_p |Ib(0,p) - Ibo(p)| < eps compared as squares
+        double err2 = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const double dr = tot[p].re - ibo[p].re, di = tot[p].im - ibo[p].im;
+            err2 = fmax(err2, fma(dr, dr, di * di));
+            ibo[p] = tot[p];
+        }
+        const bool conv = err2 < f.eps * f.eps;
+        const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
+
+        // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
+        // Also Re(drop . conj(Ib)) per phase: on a feeder without zeroed phases
+        // PQb(0).re - sum_k PQL(k).re = s3 sum_a Re(drop_a conj(Ib_a)) exactly
+        // (V_k = V0 - A_k, sum_k A_k conj(IL_k) = sum_a drop_a conj(Ib_a)), so the
+        // VVC loss needs neither IL nor Ib after this point
+        cx g[C][3];
+        double lp[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                cx tm[9];
+#pragma unroll
+                for (int l = 0; l < 3; ++l) tm[l * 3 + a] = ldx(tl, ((l * 3 + a) * C + c) * L + li);
+                g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
+                lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = g[0][p];
+#pragma unroll
+            for (int c = 1; c < C; ++c) { acc = cadd(acc, g[c][p]); g[c][p] = acc; }
+            const cx inc = mk(seg_incl<L>(acc.re), seg_incl<L>(acc.im));
+            const cx ex = csub(inc, acc);
+#pragma unroll
+            for (int c = 0; c < C; ++c) g[c][p] = cadd(ex, g[c][p]);   // Ginc at this slot
+        }
+        wfence();
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int ci = si_comp(si[c]);
+            if (ci >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+            }
+        }
+        wfence();
+        // block offsets, one lane per block (block 0, node 1's chain, has none)
+        for (int b = li; b < nblk; b += L) {
+            cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+            for (int j = 0; j < bdepth; ++j) {
+                const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, of[p]);
+        }
+        wfence();
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                g[c][p] = cadd(g[c][p], ldx(OFF, p * nblk + si_blk(si[c])));   // A(k)
+                v[c][p] = csub(v0[p], g[c][p]);
+                if (FULL && ((si_mask(si[c]) >> p) & 1)) v[c][p] = mk(0.0, 0.0);
+            }
+        if (FULL && f.has_rel) {
+            // below a zeroed ancestor m: V(k,p) = A(m) - A(k)
+            wfence();
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int ci = si_comp(si[c]);
+                if (ci >= 0) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+                }
+            }
+            wfence();
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const int mr = f.slot_mref[(p * C + c) * L + li];
+                    if (mr >= 0 && !((si_mask(si[c]) >> p) & 1)) v[c][p] = csub(ldx(X, p * XC + mr), g[c][p]);
+                }
+        }
+        wfence();
+
+        if (fin && !DBG(128)) {
+            // ---- a scenario's last sweep: V in node order into its region (Sld is
+            // not needed again; the workgroup writes V out after the loop), loss
+            // (VoltVarCtrl.cpp:1152-1161), Vmin/Vmax (V_abc_list.cpp:7-81,
+            // VoltVarCtrl.cpp:1201-1207); whole segments
+            double mn = INFINITY, mx = -INFINITY, x;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (si_valid(si[c])) {
+                    int k = f.slot_node[c * L + li];
+                    asm volatile("" : "+v"(k));   // keeps the output addressing inside this block
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        stx(SL, p * nn + k, v[c][p]);
+                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                        const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
+                        mn = fmin(mn, m2);
+                        mx = fmax(mx, m2);
+                    }
+                }
+            }
+            if (li == 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    // substation row 0: V0, Ib(0) = this sweep's total, no load
+                    stx(SL, p * nn + 0, v0[p]);
+                    if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0[p], mk(0, 0), ibo[p]);
+                    const double m2 = fma(v0[p].re, v0[p].re, v0[p].im * v0[p].im);
+                    mn = fmin(mn, m2);
+                    mx = fmax(mx, m2);
+                }
+            }
+            if (!FULL || !f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
+                // every Lnum_p + 1 = Nn: V_abc_list keeps every row, so the extremes are
+                // plain min/max; loss = s3 sum Re(drop conj(Ib))
+                // (|V|^2 compared, one sqrt each at the end: sqrt is monotonic)
+                x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
+                mn = sqrt(seg_reduce_min<L>(mn));
+                mx = sqrt(seg_reduce_max<L>(mx));
+            } else {
+                // general V_abc_list: per phase the first K_p nonzero |V| in row order,
+                // zero padded; loss from PQb(0) and PQL as the reference sums them
+                wfence();
+                double sl = 0.0;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        if (si_valid(si[c])) sl += f.s3 * (v[c][p].re * il[c][p].re + v[c][p].im * il[c][p].im);
+                sl = seg_incl<L>(sl);
+                x = 0.0;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) x += cmul(cmul(v0[p], mk(f.s3, 0.0)), cconj(ibo[p])).re;
+                x -= sl;
+                mn = INFINITY;
+                mx = -INFINITY;
+                const unsigned long long segbits = L == 64 ? ~0ull : ((1ull << L) - 1ull) << (seg * L);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const int K = f.K[p];
+                    int cnt = 0;
+                    for (int k0 = 0; k0 < nn; k0 += L) {
+                        const int k = k0 + li;
+                        double m = 0.0;
+                        if (k < nn) {
+                            const cx vv = ldx(SL, p * nn + k);
+                            m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
+                        }
+                        const bool nz = k < nn && m != 0.0;
+                        const unsigned long long bal = __ballot(nz) & segbits;
+                        const int rank = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+                        if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
+                        cnt += __popcll(bal);
+                    }
+                    if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+                }
+                mn = seg_reduce_min<L>(mn);
+                mx = seg_reduce_max<L>(mx);
+            }
+            if (li == L - 1) {
+                if (o.iters) o.iters[s] = it + 1;
+                if (o.status) o.status[s] = conv ? 0 : 1;
+                if (o.loss) o.loss[s] = x;
+                if (o.vmin) o.vmin[s] = mn;
+                if (o.vmax) o.vmax[s] = mx;
+                res[sc][0] = x;
+                res[sc][1] = mn;
+                res[sc][2] = mx;
+                res[sc][3] = conv ? 0.0 : 1.0;
+            }
+            wfence();
+        }
+        done = done || fin;
+    }
+
+    // ---- fused batch aggregate [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over,
+    // n_under, n_scen] over converged scenarios: the workgroup's partial in
+    // scenario order, published with agent-scope stores; one ticket per
+    // workgroup; the last to arrive folds the partials in workgroup order
+    // (deterministic) -- the hand-off of MI355X_MICROARCH.md "Valid forms".
+    // Published before the V stores, so the ticket does not wait for them.
+    __syncthreads();
+    __shared__ int last_wg;
+    const bool agg = o.agg && !DBG(2048);
+    if (agg && threadIdx.x == 0) {
+        double ls = 0, mn = INFINITY, mx = -INFINITY, nc = 0, nnc = 0, no = 0, nu = 0;
+        for (int j = 0; j < nsb; ++j) {
+            if (res[j][3] == 0.0) {
+                ls += res[j][0];
+                mn = fmin(mn, res[j][1]);
+                mx = fmax(mx, res[j][2]);
+                nc += 1;
+                if (res[j][2] > f.ub_v) no += 1;
+                if (res[j][1] < f.lb_v) nu += 1;
+            } else {
+                nnc += 1;
+            }
+        }
+        const double part[8] = {ls, mn, mx, nc, nnc, no, nu, (double)nsb};
+        double *dst = o.partials + 8 * (size_t)blockIdx.x;
+        for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_wg = t == gridDim.x - 1;
+    }
+    // ---- the workgroup's V, coalesced: consecutive scenarios of one (phase, node)
+    if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
+        for (int i = threadIdx.x; i < 3 * nn * SPB; i += NT) {
+            const int j = i % SPB, r = i / SPB;   // r = p*nn + k
+            if (j < nsb) {
+                const double2 vv = reg0[j * RS + r];
+                if (o.v_re) __builtin_nontemporal_store(vv.x, o.v_re + (size_t)r * B + s0 + j);
+                if (o.v_im) __builtin_nontemporal_store(vv.y, o.v_im + (size_t)r * B + s0 + j);
+            }
+        }
+    }
+    if (agg) {
+        __syncthreads();
+        if (last_wg) {
+            // thread i folds workgroups i, i + NT, ... in order, then a fixed tree
+            double a[8] = {0, INFINITY, -INFINITY, 0, 0, 0, 0, 0};
+            for (unsigned b = threadIdx.x; b < gridDim.x; b += NT) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const double r = __hip_atomic_load(o.partials + 8 * (size_t)b + q, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                    a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
+                }
+            }
+            double *sh = (double *)reg0;   // [8][NT] (the regions are dead)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sh[q * NT + threadIdx.x] = a[q];
+            __syncthreads();
+            for (int w = NT / 2; w > 0; w >>= 1) {
+                if ((int)threadIdx.x < w) {
+                    const int t = threadIdx.x;
+                    sh[0 * NT + t] += sh[0 * NT + t + w];
+                    sh[1 * NT + t] = fmin(sh[1 * NT + t], sh[1 * NT + t + w]);
+                    sh[2 * NT + t] = fmax(sh[2 * NT + t], sh[2 * NT + t + w]);
+#pragma unroll
+                    for (int q = 3; q < 8; ++q) sh[q * NT + t] += sh[q * NT + t + w];
+                }
+                __syncthreads();
+            }
+            if (threadIdx.x < 8) o.agg[threadIdx.x] = sh[threadIdx.x * NT];
+            if (threadIdx.x == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+namespace {
+int wave_wpb(const WaveDev &w) { return w.spw * w.C <= 2 ? 16 : 8; }   // = WaveGeom::WPB
+}  // namespace
+
+size_t wave_lds_bytes(const WaveDev &w) {
+    const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)wave_wpb(w) * w.spw;
+    const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4;
+    const size_t regions = 16 * spb * (3 * w.C * L + 3 * xc + 3 * (size_t)w.nblk);
+    const size_t stage = 8 * 6 * (size_t)w.nl * spb;                 // the loads, staged over the regions
+    const size_t agg = 8 * 8 * (size_t)wave_wpb(w) * 64;               // the last workgroup's fold
+    return 16 * (9 * (size_t)w.C * L) + pairs + std::max(regions, std::max(stage, agg));
+}
+
+int wave_scenarios_per_block(const WaveDev &w) { return wave_wpb(w) * w.spw; }
+
+namespace {
+typedef void (*WaveKernel)(WaveDev, int, const double *, OutDev);
+template <int SPW, int C>
+WaveKernel pick(bool full) {
+    return full ? dpf_wave_kernel<SPW, C, true> : dpf_wave_kernel<SPW, C, false>;
+}
+}  // namespace
+
+hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
+    const int per_block = wave_scenarios_per_block(w);
+    const unsigned grid = (unsigned)((n_scen + per_block - 1) / per_block);
+    const size_t lds = wave_lds_bytes(w);
+    // FULL keeps IL and Ib of the last sweep for Vpolar/PQb/PQL, and for the
+    // loss of a feeder with zeroed phases (reference formula over PQL)
+    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
+    WaveKernel k = nullptr;
+    int id = -1;
+    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full); id = 0; }
+    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full); id = 1; }
+    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full); id = 2; }
+    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full); id = 3; }
+    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full); id = 4; }
+    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full); id = 5; }
+    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full); id = 6; }
+    if (!k) return hipErrorInvalidValue;
+    static bool attr[7][2] = {};
+    if (!attr[id][full]) {   // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the static part)
+        hipFuncAttributes fa{};
+        hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024 - (int)fa.sharedSizeBytes);
+        if (e != hipSuccess) return e;
+        attr[id][full] = true;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(wave_wpb(w) * 64), lds, st, w, n_scen, pq, o);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess && getenv("FPF_DEBUG")) {
+        hipFuncAttributes fa{};
+        (void)hipFuncGetAttributes(&fa, (const void *)k);
+        fprintf(stderr, "launch_wave: %s grid %u block %d dyn lds %zu static %zu maxdyn %d regs %d local %zu\n",
+                hipGetErrorString(e), grid, wave_wpb(w) * 64, lds, fa.sharedSizeBytes, fa.maxDynamicSharedSizeBytes,
+                fa.numRegs, fa.localSizeBytes);
+    }
+    return e;
+}
+
+// the (scenarios per wave, slots per lane) geometry for n branches
+bool wave_geometry(int n, int *spw, int *c) {
+    static const int cfg[5][2] = {{4, 1}, {4, 2}, {2, 2}, {2, 4}, {1, 4}};
+    if (const char *e = getenv("FPF_WAVE_GEOM")) {   // experiments: "spw,c"
+        int a = 0, b = 0;
+        if (sscanf(e, "%d,%d", &a, &b) == 2 && n <= (64 / std::max(a, 1)) * b) {
+            *spw = a;
+            *c = b;
+            return true;
+        }
+    }
+    for (const auto &g : cfg)
+        if (n <= (64 / g[0]) * g[1]) {
+            *spw = g[0];
+            *c = g[1];
+            return true;
+        }
+    return false;
+}
+
+}  // namespace fpf

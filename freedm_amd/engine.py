@@ -107,7 +107,7 @@ class PowerFlow:
         L.fpf_feeder_get_info(h, C.byref(info))
         self.info = info.as_dict()
         self.nl, self.nn = self.info["nl"], self.info["nn"]
-        self.kernel = {1: "generic", 2: "tiled"}[self.info["kernel"]]
+        self.kernel = {1: "generic", 2: "tiled", 3: "wave"}[self.info["kernel"]]
         # a hipRTC failure is not fatal (the interpreted tiled kernel runs); keep why
         self.rtc_error = self.ctx.err() if (self.kernel == "tiled" and specialize
                                             and not self.info["specialized"]) else ""

@@ -66,9 +66,12 @@ extern "C" {
                                  /* state after the last sweep                            */
 
 /* kernel selection */
-#define FPF_KERNEL_AUTO      0   /* tiled if the feeder is well formed, else generic      */
+#define FPF_KERNEL_AUTO      0   /* fast mode: wave if the feeder allows it; then tiled   */
+                                 /* if the feeder is well formed, else generic            */
 #define FPF_KERNEL_GENERIC   1   /* one lane per scenario, state streamed through HBM     */
 #define FPF_KERNEL_TILED     2   /* one workgroup per scenario tile, state in LDS         */
+#define FPF_KERNEL_WAVE      3   /* one wavefront per scenario, sweeps as prefix scans;   */
+                                 /* fast mode, well-formed feeders of <= 256 branches     */
 
 typedef struct fpf_ctx fpf_ctx;
 typedef struct fpf_feeder fpf_feeder;

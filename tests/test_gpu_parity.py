@@ -38,7 +38,7 @@ def _vrel(a_re, a_im, b_re, b_im):
     return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))
 
 
-KERNELS = [("generic", False, 1), ("tiled", False, 1), ("tiled", True, 1), ("tiled", True, 0)]
+KERNELS = [("generic", False, 1), ("tiled", False, 1), ("tiled", True, 1), ("tiled", True, 0), ("wave", False, 0)]
 
 
 def _close(a, b, rtol):
@@ -47,12 +47,14 @@ def _close(a, b, rtol):
     assert float(np.max(np.abs(a - b))) <= rtol * scale, (float(np.max(np.abs(a - b))), scale)
 
 
-@pytest.mark.parametrize("kernel,spec,exact", KERNELS, ids=["generic", "tiled", "tiled-rtc", "tiled-rtc-fast"])
+@pytest.mark.parametrize("kernel,spec,exact", KERNELS, ids=["generic", "tiled", "tiled-rtc", "tiled-rtc-fast", "wave"])
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_matches_golden(name, kernel, spec, exact):
     g = load_golden(name)
     if kernel == "tiled" and name == "g4_2048bus" and spec:
         pytest.skip("2048-bus: above the hipRTC size limit, covered by the interpreted tiled kernel")
+    if kernel == "wave" and name == "g4_2048bus":
+        pytest.skip("2048-bus: above the wave kernel's 256 branches")
     pf = _pf(g["Dl"], g["Z"], kernel=kernel, specialize=spec, exact=exact)
     assert pf.kernel == kernel
     if kernel == "tiled":
@@ -90,7 +92,10 @@ def test_matches_golden(name, kernel, spec, exact):
 
 def test_auto_kernel_choice():
     g = load_golden("g3_123bus")
-    assert _pf(g["Dl"], g["Z"]).kernel == "tiled"
+    assert _pf(g["Dl"], g["Z"]).kernel == "wave"            # fast mode (default)
+    assert _pf(g["Dl"], g["Z"], exact=1).kernel == "tiled"  # the reference's roundings
+    g4 = load_golden("g4_2048bus")
+    assert _pf(g4["Dl"], g4["Z"]).kernel == "tiled"         # above the wave kernel's size
     f = F.demo_feeder()
     Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # 2->3 before 1->2: legal for the reference, not well formed
     pf = _pf(Dl, f.Z)
@@ -98,6 +103,10 @@ def test_auto_kernel_choice():
     from freedm_amd import DPFError
     with pytest.raises(DPFError):
         _pf(Dl, f.Z, kernel="tiled")
+    with pytest.raises(DPFError):
+        _pf(Dl, f.Z, kernel="wave")
+    with pytest.raises(DPFError):
+        _pf(g["Dl"], g["Z"], kernel="wave", exact=1)
 
 
 def test_malformed_order_matches_oracle():
@@ -205,14 +214,18 @@ def test_full_config2_properties():
     np.testing.assert_array_equal(a["iters"][idx], c["iters"])
 
 
-def test_fast_mode_full_batches_against_oracle():
-    """The default (fast) specialised kernel against the oracle on whole batches:
-    config 2 (4096 scenarios) and a 32768-scenario slice of the config-4 hosting
-    study -- identical iteration counts and status everywhere, V within 1e-10."""
+@pytest.mark.parametrize("kernel", ["wave", "tiled"])
+def test_fast_mode_full_batches_against_oracle(kernel):
+    """The fast-mode kernels (the wave kernel is the default) against the oracle
+    on whole batches: config 2 (4096 scenarios) and a 32768-scenario slice of the
+    config-4 hosting study -- identical iteration counts and status everywhere,
+    V within 1e-10."""
     from oracle import oracle as O
     f = F.synthetic_feeder(123, 123)
-    pf = _pf(f.Dl, f.Z)
-    assert pf.info["specialized"] == 1, pf.rtc_error
+    pf = _pf(f.Dl, f.Z, kernel=kernel)
+    assert pf.kernel == kernel
+    if kernel == "tiled":
+        assert pf.info["specialized"] == 1, pf.rtc_error
     for pq in (F.scenario_loads(f, np.arange(4096)), F.hosting_loads(f, np.arange(32768))):
         r = pf.solve(pq)
         c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=16)
