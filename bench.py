@@ -6,12 +6,13 @@
 Workload = BASELINE config 2: synthetic 123-bus feeder (seed 123), a batch of
 4096 seeded load/DER scenarios per GPU (weak scaling; scenario ids are global,
 rank r solves ids [r*4096, (r+1)*4096)).  One step = one pass of the hot path
-over that batch: libfreedm_pf's tiled DPF kernel (all sweeps, fused loss/Vmin/
-Vmax, and the deterministic batch aggregate in the same launch), inputs
-resident in HBM.  After
-the K timed steps the per-GPU aggregates are combined once by an RCCL
-all-reduce (the only collective of the path).  value = converged scenarios of
-all ranks / max-over-ranks wall time of the timed region.
+over that batch: one launch of libfreedm_pf's DPF kernel (the wave kernel in
+the default fast mode: all sweeps, V, per-scenario loss / Vmin / Vmax /
+iterations), inputs resident in HBM, per-scenario results kept for every
+step.  After the K timed steps the study aggregate over all K x 4096 results
+is reduced once on each GPU (deterministic) and combined across GPUs by one
+RCCL all-reduce (the only collective of the path), inside the timed region.
+value = converged scenarios of all ranks / max-over-ranks wall time.
 
 Also reported: the roofline of the dominant kernel (algorithmic bytes per
 SURVEY.md 8(d) / its HIP-event time), and the CPU oracle (oracle/ref_dpf.c,
@@ -123,51 +124,52 @@ def main():
     pf.reserve(B)
     ids = np.arange(rank * B, (rank + 1) * B)
     d_pq = torch.from_numpy(scenario_loads(feeder, ids, seed=SCEN_SEED)).to(dev)
-    out = {"iters": torch.zeros(B, dtype=torch.int32, device=dev),
-           "status": torch.zeros(B, dtype=torch.int8, device=dev),
-           "loss": torch.zeros(B, dtype=torch.float64, device=dev),
-           "vmin": torch.zeros(B, dtype=torch.float64, device=dev),
-           "vmax": torch.zeros(B, dtype=torch.float64, device=dev),
-           "v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
-           "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
-    if args.no_v_out:
-        del out["v_re"], out["v_im"]
+    # per-scenario outputs of every timed step (the study's results); V is
+    # overwritten step after step
+    K = max(args.steps, 1)
+    res = {"iters": torch.zeros((K, B), dtype=torch.int32, device=dev),
+           "status": torch.zeros((K, B), dtype=torch.int8, device=dev),
+           "loss": torch.zeros((K, B), dtype=torch.float64, device=dev),
+           "vmin": torch.zeros((K, B), dtype=torch.float64, device=dev),
+           "vmax": torch.zeros((K, B), dtype=torch.float64, device=dev)}
+    v_out = {} if args.no_v_out else {"v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
+                                      "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
     stream = torch.cuda.current_stream(dev)
-    agg_all = torch.zeros((max(args.steps, 1) + args.warmup, 8), dtype=torch.float64, device=dev)
-    agg_ptr = [agg_all[i] for i in range(agg_all.shape[0])]
-    solve, aggregate = pf.bind_device(d_pq, out, stream=stream)
+    solves = [pf.bind_device(d_pq, dict(v_out, **{k: t[i] for k, t in res.items()}), stream=stream)[0]
+              for i in range(K)]
+    flat = {k: t.view(-1) for k, t in res.items()}
+    agg = torch.zeros(8, dtype=torch.float64, device=dev)
 
-    def step(i, ev0=None, ev1=None):
-        if ev0 is not None:
-            ev0.record(stream)
-        # the DPF kernel: all sweeps, fused loss / Vmin / Vmax per scenario and the
-        # deterministic batch aggregate (8 doubles per step, last-workgroup reduction)
-        solve(agg_ptr[i])
-        if ev1 is not None:
-            ev1.record(stream)
+    def step(i):
+        # one batch: the DPF kernel -- all sweeps, V, loss / Vmin / Vmax / iterations
+        # per scenario
+        solves[i]()
 
-    def combine(a):
-        return torch.cat([a[:, 0].sum().view(1), a[:, 1].min().view(1), a[:, 2].max().view(1), a[:, 3:].sum(0)])
+    def study_aggregate():
+        # once per study: [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over, n_under,
+        # n_scen] over every scenario solved (deterministic reduction)
+        pf.aggregate_device(flat, agg, n_scen=K * B, stream=stream)
+        return agg
 
     for i in range(args.warmup):
-        step(args.steps + i)
-    combine(agg_all[args.steps:])            # warm torch's reduction kernels (lazy code-object load)
+        step(i % K)
+    study_aggregate()
     torch.cuda.synchronize(dev)
-    conv_per_step = int((out["status"] == 0).sum().item())
+    conv_per_step = int((res["status"][0] == 0).sum().item())
 
-    # HIP events around every ev_every-th launch (an event pair costs the stream a
-    # few microseconds, so they bracket a sample of the launches, not all of them)
-    ev_every = max(1, args.steps // 8)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if i % ev_every == 0
-           else (None, None) for i in range(args.steps)]
+    # HIP events on the launch stream bracket the K back-to-back launches of the
+    # timed region: average kernel time = their elapsed time / K
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        step(i, *evs[i])
+        step(i)
+    ev1.record(stream)
     t_submit = time.perf_counter() - t0
-    total = combine(agg_all[:args.steps])
+    total = study_aggregate().clone()
     if world > 1:
         # the one collective: combine the per-GPU study aggregates over RCCL/xGMI
         mm = torch.stack([total[1], -total[2]])
@@ -183,8 +185,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs if e0 is not None]
-    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    avg_kern_s = ev0.elapsed_time(ev1) / args.steps / 1e3
     tot = total.cpu().numpy()
     n_conv_all = float(tot[3])
     value = n_conv_all / elapsed
@@ -221,8 +222,6 @@ def main():
                           "n_under": int(tot[6]), "n_scen": int(tot[7])},
             "converged_per_step_rank0": conv_per_step,
             "host_submit_ms_per_step": t_submit / args.steps * 1e3,
-            "kernel_ms_min_max": [float(np.min(kern_ms)), float(np.max(kern_ms))],
-            "kernel_launches_timed": len(kern_ms),
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(feeder, seconds=args.cpu_seconds)

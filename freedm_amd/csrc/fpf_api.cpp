@@ -1209,7 +1209,8 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     }
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("solve launch: ") + hipGetErrorString(e));
     if (d_agg && !agg_done) {
-        e = launch_aggregate(n_scen, o.status, o.loss, o.vmin, o.vmax, f->dev.lb_v, f->dev.ub_v, d_agg, st);
+        e = launch_aggregate(n_scen, o.status, o.loss, o.vmin, o.vmax, f->dev.lb_v, f->dev.ub_v, d_agg, nullptr,
+                             nullptr, st);
         if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("aggregate launch: ") + hipGetErrorString(e));
     }
     return FPF_OK;
@@ -1222,8 +1223,15 @@ extern "C" int fpf_aggregate_device(fpf_feeder *f, int n_scen, const signed char
     fpf_ctx *ctx = f->ctx;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    if (f->partials_cap < 256) {   // scratch of the multi-block form (shared with the fused aggregates)
+        (void)hipFree(f->d_partials);
+        f->d_partials = nullptr;
+        f->partials_cap = 0;
+        HIPCHK(ctx, hipMalloc(&f->d_partials, 256 * 8 * sizeof(double)));
+        f->partials_cap = 256;
+    }
     hipError_t e = launch_aggregate(n_scen, (const int8_t *)d_status, d_loss, d_vmin, d_vmax, f->dev.lb_v, f->dev.ub_v,
-                                    d_agg, st);
+                                    d_agg, f->d_partials, f->d_ticket, st);
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("aggregate launch: ") + hipGetErrorString(e));
     return FPF_OK;
 }

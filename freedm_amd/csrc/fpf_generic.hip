@@ -160,16 +160,22 @@ hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, doub
 }
 
 // Deterministic batch aggregate (fixed thread->scenario map and fixed tree):
-// [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over, n_under, n_scen]
-__global__ __launch_bounds__(1024) void dpf_aggregate_kernel(int B, const int8_t *__restrict__ status,
+// [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over, n_under, n_scen].  Block g
+// reduces scenarios [g*chunk, (g+1)*chunk); with several blocks each publishes
+// its partial (agent-scope stores), takes a ticket, and the last one folds the
+// partials in block order.
+__global__ __launch_bounds__(1024) void dpf_aggregate_kernel(int B, int chunk, const int8_t *__restrict__ status,
                                                              const double *__restrict__ loss,
                                                              const double *__restrict__ vmin,
                                                              const double *__restrict__ vmax,
-                                                             double lb_v, double ub_v, double *agg) {
+                                                             double lb_v, double ub_v, double *agg, double *partials,
+                                                             unsigned *ticket) {
     __shared__ double sh[8][1024];
+    __shared__ int last;
     const int t = threadIdx.x;
+    const int lo = blockIdx.x * chunk, hi = min(B, lo + chunk);
     double ls = 0, mn = INFINITY, mx = -INFINITY, nc = 0, nnc = 0, no = 0, nu = 0;
-    for (int s = t; s < B; s += blockDim.x) {
+    for (int s = lo + t; s < hi; s += blockDim.x) {
         if (status[s] == 0) {
             ls += loss[s];
             mn = fmin(mn, vmin[s]);
@@ -181,28 +187,66 @@ __global__ __launch_bounds__(1024) void dpf_aggregate_kernel(int B, const int8_t
             nnc += 1;
         }
     }
-    sh[0][t] = ls; sh[1][t] = mn; sh[2][t] = mx; sh[3][t] = nc;
-    sh[4][t] = nnc; sh[5][t] = no; sh[6][t] = nu;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (t < w) {
-            sh[0][t] += sh[0][t + w];
-            sh[1][t] = fmin(sh[1][t], sh[1][t + w]);
-            sh[2][t] = fmax(sh[2][t], sh[2][t + w]);
-            for (int q = 3; q < 7; ++q) sh[q][t] += sh[q][t + w];
-        }
+    auto tree = [&]() {
         __syncthreads();
+        for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+            if (t < w) {
+                sh[0][t] += sh[0][t + w];
+                sh[1][t] = fmin(sh[1][t], sh[1][t + w]);
+                sh[2][t] = fmax(sh[2][t], sh[2][t + w]);
+                for (int q = 3; q < 8; ++q) sh[q][t] += sh[q][t + w];
+            }
+            __syncthreads();
+        }
+    };
+    sh[0][t] = ls; sh[1][t] = mn; sh[2][t] = mx; sh[3][t] = nc;
+    sh[4][t] = nnc; sh[5][t] = no; sh[6][t] = nu; sh[7][t] = 0;
+    tree();
+    if (gridDim.x == 1) {
+        if (t < 7) agg[t] = sh[t][0];
+        if (t == 0) agg[7] = (double)B;
+        return;
     }
     if (t == 0) {
-        for (int q = 0; q < 7; ++q) agg[q] = sh[q][0];
+        for (int q = 0; q < 7; ++q)
+            __hip_atomic_store(partials + 8 * (size_t)blockIdx.x + q, sh[q][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    double a[8] = {0, INFINITY, -INFINITY, 0, 0, 0, 0, 0};
+    for (unsigned g = t; g < gridDim.x; g += blockDim.x) {
+        for (int q = 0; q < 7; ++q) {
+            const double r = __hip_atomic_load(partials + 8 * (size_t)g + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
+        }
+    }
+    for (int q = 0; q < 8; ++q) sh[q][t] = a[q];
+    tree();
+    if (t < 7) agg[t] = sh[t][0];
+    if (t == 0) {
         agg[7] = (double)B;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
+// partials: [>= 256][8] scratch and ticket (0 between launches) for the
+// multi-block form; NULL = one block
 hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss, const double *vmin,
-                            const double *vmax, double lb_v, double ub_v, double *d_agg, hipStream_t st) {
-    hipLaunchKernelGGL(dpf_aggregate_kernel, dim3(1), dim3(1024), 0, st, n_scen, status, loss, vmin, vmax,
-                       lb_v, ub_v, d_agg);
+                            const double *vmax, double lb_v, double ub_v, double *d_agg, double *partials,
+                            unsigned *ticket, hipStream_t st) {
+    int grid = 1, chunk = n_scen;
+    if (partials && ticket && n_scen > 8192) {
+        chunk = 4096;
+        grid = (n_scen + chunk - 1) / chunk;
+        if (grid > 256) {
+            grid = 256;
+            chunk = (n_scen + grid - 1) / grid;
+        }
+    }
+    hipLaunchKernelGGL(dpf_aggregate_kernel, dim3(grid), dim3(1024), 0, st, n_scen, chunk, status, loss, vmin, vmax,
+                       lb_v, ub_v, d_agg, partials, ticket);
     return hipGetLastError();
 }
 

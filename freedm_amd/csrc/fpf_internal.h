@@ -152,7 +152,7 @@ hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, doub
 hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss,
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
-                            double *d_agg, hipStream_t st);
+                            double *d_agg, double *partials, unsigned *ticket, hipStream_t st);
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wave_lds_bytes(const WaveDev &w);
 bool wave_geometry(int n, int *spw, int *c);

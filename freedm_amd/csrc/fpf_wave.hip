@@ -171,6 +171,8 @@ __device__ __forceinline__ int si_comp(int x) { return ((x >> 4) & 511) - 1; }  
 __device__ __forceinline__ int si_last(int x) { return (x >> 13) & 511; }
 __device__ __forceinline__ int si_blk(int x) { return (x >> 22) & 511; }
 
+constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
+
 template <int SPW, int C>
 struct WaveGeom {
     static constexpr int L = 64 / SPW;                 // lanes per scenario
@@ -219,41 +221,68 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
     double2 *const tl = lds;                                          // [9][C][L]
     int *const pairs = (int *)(tl + 9 * C * L);                       // [bdepth][2][nblk]
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
-    double2 *const reg0 = (double2 *)(pairs + pair_n);               // per-scenario regions
+    int *const knode = pairs + pair_n;                                // [C][L] node of each slot
+    double2 *const reg0 = (double2 *)(knode + C * L);                 // per-scenario regions
     const int RS = 3 * C * L + 3 * XC + 3 * nblk;                    // double2 per region
     double2 *const SL = reg0 + sc * RS;
     double2 *const X = SL + 3 * C * L;
     double2 *const OFF = X + 3 * XC;
     const bool live = sc < nsb;
+    int si[C], row[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        row[c] = f.slot_row[c * L + li];
+        si[c] = f.slot_info[c * L + li];
+    }
 
-    // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced, staged over the
+    // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced (16 scenarios = one
+    // 128-byte line per row), U loads in flight per thread, staged over the
     // per-scenario regions; then each slot picks its row
     {
         double *stage = (double *)reg0;   // [6][nl][SPB]
+        constexpr int U = 8;
+        const int total = DBG(256) ? 0 : 6 * nl * SPB;
+        for (int i0 = 0; i0 < total; i0 += U * NT) {
+            double r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                const int j = i % SPB, fr = i / SPB;
+                const bool ok = i < total && j < nsb;
+                r[u] = __builtin_nontemporal_load(pq + (ok ? (size_t)fr * B + s0 + j : 0));
+                r[u] = ok ? r[u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                if (i < total) stage[i] = r[u];
+            }
+        }
         for (int i = threadIdx.x; i < 9 * C * L; i += NT) tl[i] = ld_global2(f.slot_temp, i);
         for (int i = threadIdx.x; i < 2 * bdepth * nblk; i += NT) pairs[i] = f.blk_pairs[i];
-        for (int i = threadIdx.x; i < (DBG(256) ? 0 : 6 * nl * SPB); i += NT) {
-            const int j = i % SPB, fr = i / SPB;
-            stage[i] = j < nsb ? __builtin_nontemporal_load(pq + (size_t)fr * B + s0 + j) : 0.0;
-        }
+        for (int i = threadIdx.x; i < C * L; i += NT) knode[i] = f.slot_node[i];
     }
     __syncthreads();
+    // this lane's block chain (lane b < nblk resolves block b), padded with the zero entry
+    int bp[2 * WAVE_BD];
+#pragma unroll
+    for (int j = 0; j < WAVE_BD; ++j) {
+        const bool ok = j < bdepth && li < nblk;
+        bp[2 * j] = ok ? pairs[(2 * j) * nblk + li] : XC - 1;
+        bp[2 * j + 1] = ok ? pairs[(2 * j + 1) * nblk + li] : XC - 1;
+    }
     const double inv_s3 = 1.0 / f.s3;
-    int si[C];
     double2 sld_in[C][3];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        const int i = c * L + li;
-        const int row = f.slot_row[i];
-        si[c] = f.slot_info[i];
         const double *stage = (const double *)reg0;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             // Sld = (P + jQ) / (bkva/3)  (:46-50)
             sld_in[c][p] = make_double2(0.0, 0.0);
-            if (row >= 0)
-                sld_in[c][p] = make_double2(stage[((2 * p) * nl + row) * SPB + sc] * inv_s3,
-                                            stage[((2 * p + 1) * nl + row) * SPB + sc] * inv_s3);
+            if (row[c] >= 0)
+                sld_in[c][p] = make_double2(stage[((2 * p) * nl + row[c]) * SPB + sc] * inv_s3,
+                                            stage[((2 * p + 1) * nl + row[c]) * SPB + sc] * inv_s3);
         }
     }
     __syncthreads();
@@ -295,7 +324,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
 #pragma unroll
             for (int c = 1; c < C; ++c) { acc = cadd(acc, il[c][p]); ib[c][p] = acc; }
             const cx inc = mk(seg_incl<L>(acc.re), seg_incl<L>(acc.im));
-            tot[p] = mk(seg_last<L>(inc.re, seg), seg_last<L>(inc.im, seg));
+            tot[p] = inc;   // the segment total in its last lane
             exl[p] = csub(inc, acc);   // the lane's exclusive prefix
 #pragma unroll
             for (int c = 0; c < C; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // Einc at this slot
@@ -331,7 +360,9 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
             err2 = fmax(err2, fma(dr, dr, di * di));
             ibo[p] = tot[p];
         }
-        const bool conv = err2 < f.eps * f.eps;
+        // decided in the segment's last lane, broadcast by ballot
+        const unsigned long long cbits = __ballot(li == L - 1 && err2 < f.eps * f.eps);
+        const bool conv = (cbits >> (seg * L + L - 1)) & 1;
         const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
 
         // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
@@ -372,16 +403,30 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
             }
         }
         wfence();
-        // block offsets, one lane per block (block 0, node 1's chain, has none)
-        for (int b = li; b < nblk; b += L) {
-            cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
-            for (int j = 0; j < bdepth; ++j) {
-                const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
+        // block offsets, one lane per block (block 0, node 1's chain, has none);
+        // the chain's index pairs sit in registers (bp), all its reads issue together
+        if (nblk <= L && bdepth <= WAVE_BD) {
+            if (li < nblk) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
 #pragma unroll
-                for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
+                for (int j = 0; j < WAVE_BD; ++j) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + bp[2 * j]), ldx(X, p * XC + bp[2 * j + 1])));
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + li, of[p]);
             }
+        } else {
+            for (int b = li; b < nblk; b += L) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+                for (int j = 0; j < bdepth; ++j) {
+                    const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, of[p]);
+                    for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, of[p]);
+            }
         }
         wfence();
 #pragma unroll
@@ -423,8 +468,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (si_valid(si[c])) {
-                    int k = f.slot_node[c * L + li];
-                    asm volatile("" : "+v"(k));   // keeps the output addressing inside this block
+                    const int k = knode[c * L + li];
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         stx(SL, p * nn + k, v[c][p]);
@@ -435,7 +479,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
                     }
                 }
             }
-            if (li == 0) {
+            if (li == L - 1) {   // the lane holding Ib(0)
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     // substation row 0: V0, Ib(0) = this sweep's total, no load
@@ -590,7 +634,7 @@ int wave_wpb(const WaveDev &w) { return w.spw * w.C <= 2 ? 16 : 8; }   // = Wave
 
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)wave_wpb(w) * w.spw;
-    const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4;
+    const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
     const size_t regions = 16 * spb * (3 * w.C * L + 3 * xc + 3 * (size_t)w.nblk);
     const size_t stage = 8 * 6 * (size_t)w.nl * spb;                 // the loads, staged over the regions
     const size_t agg = 8 * 8 * (size_t)wave_wpb(w) * 64;               // the last workgroup's fold

@@ -136,8 +136,12 @@ def test_empty_and_single():
     pf = _pf(g["Dl"], g["Z"])
     r0 = pf.solve(np.zeros((6, pf.nl, 0)))
     assert r0["iters"].size == 0 and r0["n_nonconv"] == 0
-    r1 = pf.solve(g["pq"])
-    np.testing.assert_array_equal(r1["V_re"], g["V_re"])
+    r1 = pf.solve(g["pq"])   # default: the fast-mode wave kernel
+    assert pf.kernel == "wave"
+    assert _vrel(r1["V_re"], r1["V_im"], g["V_re"], g["V_im"]) <= 1e-10
+    assert (r1["iters"] == g["iters"]).all()
+    r2 = _pf(g["Dl"], g["Z"], exact=1).solve(g["pq"])   # the reference's roundings
+    np.testing.assert_array_equal(r2["V_re"], g["V_re"])
 
 
 def test_dpf_return7_dropin():
