@@ -122,7 +122,9 @@ def main():
                    exact=args.exact)
     B = args.scenarios
     pf.reserve(B)
-    ids = np.arange(rank * B, (rank + 1) * B)
+    from freedm_amd import dist as D
+    lo, hi = D.shard_range(rank, world, world * B)   # weak scaling: B global ids per GPU
+    ids = np.arange(lo, hi)
     d_pq = torch.from_numpy(scenario_loads(feeder, ids, seed=SCEN_SEED)).to(dev)
     # per-scenario outputs of every timed step (the study's results); V is
     # overwritten step after step
@@ -170,12 +172,8 @@ def main():
     ev1.record(stream)
     t_submit = time.perf_counter() - t0
     total = study_aggregate().clone()
-    if world > 1:
-        # the one collective: combine the per-GPU study aggregates over RCCL/xGMI
-        mm = torch.stack([total[1], -total[2]])
-        dist.all_reduce(total, op=dist.ReduceOp.SUM)
-        dist.all_reduce(mm, op=dist.ReduceOp.MIN)
-        total[1], total[2] = mm[0], -mm[1]
+    # the one collective: combine the per-GPU study aggregates over RCCL/xGMI
+    D.combine_aggregates(total)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

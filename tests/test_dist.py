@@ -1,0 +1,78 @@
+"""Multi-process (world_size 2, gloo on CPU) coverage of the sharded study
+(freedm_amd/dist.py): shard assignment, shard invariance of the
+scenario inputs, and the one collective -- the all-reduce of the study
+aggregates -- against the single-process aggregate of the same scenarios.
+The per-shard solves use the CPU oracle here (test infrastructure, no GPU in
+this container); on the GPU box bench.py runs the same path over RCCL."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from freedm_amd import dist as D
+from freedm_amd import feeder as F
+
+N_STUDY = 96
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    f = F.synthetic_feeder(123, 123)
+    lo, hi = D.shard_range(rank, world, N_STUDY)
+    rows = []
+    for a, b in D.batches(lo, hi, 20):
+        r = O.dpf_batch(f.Dl, f.Z, F.hosting_loads(f, np.arange(a, b)), nthreads=2, want_full=False)
+        rows.append(D.aggregate_results(r["status"], r["loss"], r["vmin"], r["vmax"]))
+    agg = torch.from_numpy(D.fold_aggregates(rows))
+    D.combine_aggregates(agg)
+    np.save(os.path.join(out_dir, f"agg{rank}.npy"), agg.numpy())
+    dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 96, 1 << 20):
+        for world in (1, 2, 3, 8):
+            parts = [D.shard_range(r, world, n) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in parts]
+            assert max(sizes) - min(sizes) <= 1
+    assert list(D.batches(5, 17, 5)) == [(5, 10), (10, 15), (15, 17)]
+    with pytest.raises(ValueError):
+        D.shard_range(2, 2, 10)
+
+
+def test_inputs_are_shard_invariant():
+    f = F.synthetic_feeder(123, 123)
+    full = F.hosting_loads(f, np.arange(N_STUDY))
+    lo, hi = D.shard_range(1, 2, N_STUDY)
+    np.testing.assert_array_equal(F.hosting_loads(f, np.arange(lo, hi)), full[:, :, lo:hi])
+
+
+def test_world2_gloo_study_aggregate():
+    from oracle import oracle as O
+    f = F.synthetic_feeder(123, 123)
+    r = O.dpf_batch(f.Dl, f.Z, F.hosting_loads(f, np.arange(N_STUDY)), nthreads=4, want_full=False)
+    ref = D.aggregate_results(r["status"], r["loss"], r["vmin"], r["vmax"])
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rank_main, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
+        got = [np.load(os.path.join(d, f"agg{k}.npy")) for k in range(2)]
+    for g in got:   # every rank holds the study aggregate
+        np.testing.assert_array_equal(g[1:], ref[1:])
+        assert g[0] == pytest.approx(ref[0], rel=1e-13)
+    assert got[0][7] == N_STUDY and got[0][3] + got[0][4] == N_STUDY
