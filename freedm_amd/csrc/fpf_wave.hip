@@ -142,7 +142,10 @@ __device__ __forceinline__ void stx(double2 *X, int i, cx v) { X[i] = make_doubl
 template <bool ZERO>
 __device__ __forceinline__ cx il_fast(cx s, cx v) {
     const double d2 = fma(v.re, v.re, v.im * v.im);
-    double r = dv_rcp(d2);
+    // v_rcp_f64 and one Newton step (the hardware reciprocal is good to ~2^-26,
+    // one step squares the error)
+    double r = __builtin_amdgcn_rcp(d2);
+    r = fma(r, fma(-d2, r, 1.0), r);
     if (ZERO) r = d2 == 0.0 ? 0.0 : r;
     return mk(fma(s.re, v.re, s.im * v.im) * r, fma(s.re, v.im, -(s.im * v.re)) * r);
 }
@@ -209,6 +212,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
     constexpr int L = WaveGeom<SPW, C>::L, WPB = WaveGeom<SPW, C>::WPB, SPB = WaveGeom<SPW, C>::SPB;
     constexpr int NT = WPB * 64;
     extern __shared__ double2 lds[];
+    if (DBG(4096)) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int seg = lane / L, li = lane % L;
     const int sc = wv * SPW + seg;                 // scenario within the workgroup
@@ -258,11 +262,28 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
                 if (i < total) stage[i] = r[u];
             }
         }
-        for (int i = threadIdx.x; i < 9 * C * L; i += NT) tl[i] = ld_global2(f.slot_temp, i);
-        for (int i = threadIdx.x; i < 2 * bdepth * nblk; i += NT) pairs[i] = f.blk_pairs[i];
-        for (int i = threadIdx.x; i < C * L; i += NT) knode[i] = f.slot_node[i];
+        // the feeder tables: all loads in flight before the LDS stores
+        constexpr int UT = (9 * C * L + NT - 1) / NT;
+        double2 t[UT];
+#pragma unroll
+        for (int u = 0; u < UT; ++u) {
+            const int i = u * NT + (int)threadIdx.x;
+            t[u] = ld_global2(f.slot_temp, i < 9 * C * L ? i : 0);
+        }
+        const int np2 = 2 * bdepth * nblk;
+        const int pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
+        const int kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
+#pragma unroll
+        for (int u = 0; u < UT; ++u) {
+            const int i = u * NT + (int)threadIdx.x;
+            if (i < 9 * C * L) tl[i] = t[u];
+        }
+        if ((int)threadIdx.x < np2) pairs[threadIdx.x] = pv;
+        for (int i = threadIdx.x + NT; i < np2; i += NT) pairs[i] = f.blk_pairs[i];
+        if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
     }
     __syncthreads();
+    if (DBG(8192)) return;
     // this lane's block chain (lane b < nblk resolves block b), padded with the zero entry
     int bp[2 * WAVE_BD];
 #pragma unroll
@@ -410,8 +431,11 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
                 cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
 #pragma unroll
                 for (int j = 0; j < WAVE_BD; ++j) {
+                    if (j < bdepth) {   // uniform
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + bp[2 * j]), ldx(X, p * XC + bp[2 * j + 1])));
+                        for (int p = 0; p < 3; ++p)
+                            of[p] = cadd(of[p], csub(ldx(X, p * XC + bp[2 * j]), ldx(X, p * XC + bp[2 * j + 1])));
+                    }
                 }
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + li, of[p]);
@@ -585,12 +609,23 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
     }
     // ---- the workgroup's V, coalesced: consecutive scenarios of one (phase, node)
     if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
-        for (int i = threadIdx.x; i < 3 * nn * SPB; i += NT) {
-            const int j = i % SPB, r = i / SPB;   // r = p*nn + k
-            if (j < nsb) {
-                const double2 vv = reg0[j * RS + r];
-                if (o.v_re) __builtin_nontemporal_store(vv.x, o.v_re + (size_t)r * B + s0 + j);
-                if (o.v_im) __builtin_nontemporal_store(vv.y, o.v_im + (size_t)r * B + s0 + j);
+        constexpr int UV = 4;
+        const int total = 3 * nn * SPB;
+        for (int i0 = 0; i0 < total; i0 += UV * NT) {
+            double2 vv[UV];
+#pragma unroll
+            for (int u = 0; u < UV; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                vv[u] = i < total ? reg0[(i % SPB) * RS + i / SPB] : make_double2(0.0, 0.0);
+            }
+#pragma unroll
+            for (int u = 0; u < UV; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                const int j = i % SPB, r = i / SPB;   // r = p*nn + k
+                if (i < total && j < nsb) {
+                    if (o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + (size_t)r * B + s0 + j);
+                    if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + (size_t)r * B + s0 + j);
+                }
             }
         }
     }
