@@ -21,7 +21,7 @@ KERNELS = {"auto": FPF_KERNEL_AUTO, "generic": FPF_KERNEL_GENERIC, "tiled": FPF_
 EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_destroy", "fpf_last_error",
            "fpf_feeder_create", "fpf_feeder_destroy", "fpf_feeder_get_info", "fpf_feeder_reserve",
            "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source",
-           "fpf_selftest_division"]
+           "fpf_selftest_division", "fpf_vvc_line_search"]
 
 
 class FpfOpts(C.Structure):
@@ -58,6 +58,11 @@ class FpfAggregate(C.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class FpfLineSearch(C.Structure):
+    _fields_ = [("stop", C.c_int), ("reverse", C.c_int), ("first_nonconv", C.c_int), ("reserved", C.c_int),
+                ("loss", C.c_void_p), ("vmin", C.c_void_p), ("vmax", C.c_void_p)]
 
 
 _lib = None
@@ -104,6 +109,9 @@ def load(path: str | None = None):
     L.fpf_feeder_rtc_source.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
                                         C.c_char_p, C.c_size_t]
     L.fpf_feeder_rtc_source.restype = C.c_long
+    L.fpf_vvc_line_search.argtypes = [vp, _dp, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int), C.c_int, C.c_double,
+                                      C.c_double, C.c_int, C.c_double, C.POINTER(FpfLineSearch)]
+    L.fpf_vvc_line_search.restype = C.c_int
     L.fpf_selftest_division.argtypes = [C.c_int, C.c_long, C.c_ulong]
     L.fpf_selftest_division.restype = C.c_long
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",

@@ -1106,6 +1106,9 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     delete f;
 }
 
+// the options the feeder was created with (fpf_vvc.cpp)
+double fpf_feeder_bkva(const fpf_feeder *f) { return f->opts.bkva; }
+
 extern "C" int fpf_feeder_get_info(const fpf_feeder *f, fpf_feeder_info *info) {
     if (!f || !info) return FPF_ERR_ARG;
     *info = f->info;

@@ -210,6 +210,39 @@ class PowerFlow:
         if rc < 0:
             raise DPFError(rc, self.ctx.err())
 
+    # ------------------------------------------------------------------ VVC step-size search
+    def vvc_line_search(self, ctrl_dl: np.ndarray, g, load_nodes, c0: float, alpha: float = 1.1,
+                        m_max: int = 100, ploss_orig: float = np.inf) -> dict:
+        """The VVC step-size search as one batch (fpf_vvc_line_search,
+        VoltVarCtrl.cpp:1316-1542; reversed search :1544-1762 = negative c0).
+        g, load_nodes: three sequences (phases a, b, c) of per-load gradients
+        g_vq_x and load node numbers Load_x.  Returns stop (the kept m, -1 =
+        none), reverse, first_nonconv, and loss / vmin / vmax per candidate m."""
+        L = _lib.load()
+        ctrl = np.asfortranarray(ctrl_dl, dtype=np.float64)
+        if ctrl.shape[0] != self.nl:
+            raise ValueError("ctrl_dl rows differ from the feeder's")
+        ld = max(1, max(len(x) for x in g))
+        G = np.zeros((3, ld))
+        N = np.zeros((3, ld))
+        n = (C.c_int * 3)()
+        for x in range(3):
+            if len(g[x]) != len(load_nodes[x]):
+                raise ValueError("g and load_nodes differ in length")
+            G[x, :len(g[x])] = g[x]
+            N[x, :len(load_nodes[x])] = load_nodes[x]
+            n[x] = len(g[x])
+        M = m_max + 1
+        r = {"loss": np.zeros(M), "vmin": np.zeros(M), "vmax": np.zeros(M)}
+        res = _lib.FpfLineSearch(0, 0, 0, 0, r["loss"].ctypes.data, r["vmin"].ctypes.data, r["vmax"].ctypes.data)
+        rc = L.fpf_vvc_line_search(self.h, ctrl.ctypes.data_as(_lib._dp), ctrl.shape[0], ctrl.shape[1],
+                                   G.ctypes.data_as(_lib._dp), N.ctypes.data_as(_lib._dp), n, ld, float(c0),
+                                   float(alpha), int(m_max), float(ploss_orig), C.byref(res))
+        if rc < 0:
+            raise DPFError(rc, self.ctx.err())
+        r.update(stop=res.stop, reverse=res.reverse, first_nonconv=res.first_nonconv, n_nonconv=rc)
+        return r
+
     # ------------------------------------------------------------------ reference call
     def dpf_return7(self, Dl: np.ndarray) -> VPQ:
         Dl = np.asarray(Dl, dtype=np.float64)

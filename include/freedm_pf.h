@@ -182,6 +182,35 @@ int         fpf_aggregate_device(fpf_feeder *feeder, int n_scen, const signed ch
                                  const double *d_loss, const double *d_vmin, const double *d_vmax,
                                  double *d_agg, void *stream);
 
+/* Batched VVC step-size search: the reference's line search over the step
+ * sizes of one gradient (VoltVarCtrl.cpp:1316-1542; the reversed search
+ * :1544-1762 is the same call with a negative c0), as ONE batch.  Candidate m
+ * is the control ctrl_dl with, for every load i of phase x (x = a, b, c) and
+ * every row whose rbus == load_nodes[x][i] (:1334-1372),
+ *     Dl(row, 7 + 2x) = ctrl_dl(row, 7 + 2x) - g[x][i] * (bkva/3) * c_m,
+ *     c_0 = c0, c_{m+1} = alpha * c_m                      (:1321-1323, :1420-1422)
+ * for m = 0 .. m_max.  The stop rule is the reference's: the first m with
+ * loss(c_{m+1}) > loss(c_m) (:1484); on the way the direction flag drops when a
+ * kept loss exceeds ploss_orig (:1530-1536).  The reference calls DPF_return7
+ * 2 m + 1 times sequentially and throws on a non-converged solve. */
+typedef struct fpf_line_search {
+    int     stop;          /* the m whose candidate is kept (Dl_osize), -1: none within m_max */
+    int     reverse;       /* 1: the reference reverses the gradient direction (flag = false) */
+    int     first_nonconv; /* first m that does not converge (the reference throws), -1: none */
+    int     reserved;
+    double *loss;          /* [m_max + 1] caller-owned: loss at c_m (kW), required            */
+    double *vmin;          /* [m_max + 1] caller-owned or NULL                                */
+    double *vmax;          /* [m_max + 1] caller-owned or NULL                                */
+} fpf_line_search;
+
+/* g, load_nodes: [3][ld] row-major (phase-major), n_loads[3] <= ld entries used
+ * per phase; ctrl_dl: Nl x ncols column-major with the feeder's topology.
+ * Returns >= 0 (non-converged candidates) or FPF_ERR_*. */
+int         fpf_vvc_line_search(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
+                                const double *g, const double *load_nodes, const int *n_loads, int ld,
+                                double c0, double alpha, int m_max, double ploss_orig,
+                                fpf_line_search *res);
+
 /* Diagnostics: on-device check, over n seeded operand sets, that the
  * shared-reciprocal division the tiled kernel uses gives the same bits as the
  * compiler's a / b and as the libgcc __divdc3 complex division.  Returns the

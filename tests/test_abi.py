@@ -53,13 +53,14 @@ def test_header_is_c89_and_cxx98_clean(cmd, tmp_path):
 def test_struct_layouts_match_ctypes(tmp_path):
     from freedm_amd import _lib
     src = tmp_path / "sz.c"
-    src.write_text('#include <stdio.h>\n#include "freedm_pf.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
-                   ' sizeof(fpf_opts), sizeof(fpf_feeder_info), sizeof(fpf_outputs), sizeof(fpf_aggregate)); return 0;}\n')
+    src.write_text('#include <stdio.h>\n#include "freedm_pf.h"\nint main(void){printf("%zu %zu %zu %zu %zu\\n",'
+                   ' sizeof(fpf_opts), sizeof(fpf_feeder_info), sizeof(fpf_outputs), sizeof(fpf_aggregate),'
+                   ' sizeof(fpf_line_search)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     assert got == [ctypes.sizeof(_lib.FpfOpts), ctypes.sizeof(_lib.FpfFeederInfo),
-                   ctypes.sizeof(_lib.FpfOutputs), ctypes.sizeof(_lib.FpfAggregate)]
+                   ctypes.sizeof(_lib.FpfOutputs), ctypes.sizeof(_lib.FpfAggregate), ctypes.sizeof(_lib.FpfLineSearch)]
 
 
 def test_product_path_never_touches_the_oracle():
