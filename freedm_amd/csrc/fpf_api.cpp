@@ -364,10 +364,12 @@ void analyse_tiled(HostFeeder &h) {
 // that follows another branch row starts at that row's receiving bus, so the
 // Ib the backward sweep hands up a block (DPF_return7.cpp:147-157) flows to the
 // node's forward source (:176-178) -- the sweep then computes subtree sums.
+constexpr size_t WAVE_LDS_BUDGET = 159 * 1024;   // 160 KiB per CU minus the kernel's static LDS
+
 struct WaveHost {
     bool ok = false;
     std::string why;
-    int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0;
+    int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0, half = 0;
     std::vector<int32_t> row, node, info, mref, pairs;
     std::vector<double> temp;
 };
@@ -487,6 +489,20 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     w.ncomp = ncomp;
     w.has_rel = has_rel;
     w.has_mask = has_mask;
+    // LDS: the full workgroup, else half of it (static LDS ~1 KB aside)
+    WaveDev probe{};
+    probe.spw = spw;
+    probe.C = C;
+    probe.nl = nl;
+    probe.nblk = nblk;
+    probe.bdepth = bdepth;
+    probe.ncomp = ncomp;
+    w.half = 0;
+    if (wave_lds_bytes(probe) > WAVE_LDS_BUDGET) {
+        probe.half = 1;
+        if (wave_lds_bytes(probe) > WAVE_LDS_BUDGET) return no("per-scenario LDS above the budget");
+        w.half = 1;
+    }
     w.ok = true;
 }
 
@@ -1034,6 +1050,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.ncomp = wh.ncomp;
         w.has_rel = wh.has_rel;
         w.has_mask = wh.has_mask;
+        w.half = wh.half;
         w.dbg = getenv("FPF_WAVE_DBG") ? atoi(getenv("FPF_WAVE_DBG")) : 0;
         w.mxitr = o.mxitr;
         for (int p = 0; p < 3; ++p) w.K[p] = d.K[p];
@@ -1048,7 +1065,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.slot_mref = (const int32_t *)(wbase + o_mref);
         w.slot_temp = (const double *)(wbase + o_tmp);
         w.blk_pairs = (const int32_t *)(wbase + o_pairs);
-        if (wave_lds_bytes(w) > 160 * 1024) {
+        if (wave_lds_bytes(w) > WAVE_LDS_BUDGET) {
             fpf_feeder_destroy(f);
             return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
         }

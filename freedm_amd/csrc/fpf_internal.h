@@ -122,6 +122,7 @@ struct WaveDev {
     int32_t mxitr;
     int32_t K[3];            // Lnum_p + 1 (V_abc_list.cpp:12-17)
     int32_t dbg;             // diagnostic ablations (FPF_WAVE_DBG; results are wrong when set)
+    int32_t half;            // 1: half the wavefronts per workgroup (LDS-heavy feeders)
     double V0[6], s3, eps, lb_v, ub_v;
     const int32_t *slot_row;    // [C][L] Dl row of the slot's node (-1: empty slot)
     const int32_t *slot_node;   // [C][L] node id

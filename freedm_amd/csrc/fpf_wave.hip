@@ -176,10 +176,11 @@ __device__ __forceinline__ int si_blk(int x) { return (x >> 22) & 511; }
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
 
-template <int SPW, int C>
+template <int SPW, int C, bool HALF = false>
 struct WaveGeom {
     static constexpr int L = 64 / SPW;                 // lanes per scenario
-    static constexpr int WPB = SPW * C <= 2 ? 16 : 8;  // wavefronts per workgroup
+    // wavefronts per workgroup (halved for feeders whose per-scenario LDS is large)
+    static constexpr int WPB = (SPW * C <= 2 ? 16 : 8) >> (HALF ? 1 : 0);
     static constexpr int MINW = SPW * C <= 2 ? 4 : 2;  // waves per SIMD the registers allow
     static constexpr int SPB = WPB * SPW;              // scenarios per workgroup
 };
@@ -206,10 +207,10 @@ __device__ __forceinline__ double seg_reduce_min(double x) {
 template <int L>
 __device__ __forceinline__ double seg_reduce_max(double x) { return -seg_reduce_min<L>(-x); }
 
-template <int SPW, int C, bool FULL>
-__global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
+template <int SPW, int C, bool FULL, bool HALF>
+__global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, C, HALF>::MINW)) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
-    constexpr int L = WaveGeom<SPW, C>::L, WPB = WaveGeom<SPW, C>::WPB, SPB = WaveGeom<SPW, C>::SPB;
+    constexpr int L = WaveGeom<SPW, C, HALF>::L, WPB = WaveGeom<SPW, C, HALF>::WPB, SPB = WaveGeom<SPW, C, HALF>::SPB;
     constexpr int NT = WPB * 64;
     extern __shared__ double2 lds[];
     if (DBG(4096)) return;
@@ -664,7 +665,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C>::WPB * 64), (WaveGeom<SPW, C>::MI
 }
 
 namespace {
-int wave_wpb(const WaveDev &w) { return w.spw * w.C <= 2 ? 16 : 8; }   // = WaveGeom::WPB
+int wave_wpb(const WaveDev &w) { return (w.spw * w.C <= 2 ? 16 : 8) >> (w.half ? 1 : 0); }   // = WaveGeom::WPB
 }  // namespace
 
 size_t wave_lds_bytes(const WaveDev &w) {
@@ -681,8 +682,9 @@ int wave_scenarios_per_block(const WaveDev &w) { return wave_wpb(w) * w.spw; }
 namespace {
 typedef void (*WaveKernel)(WaveDev, int, const double *, OutDev);
 template <int SPW, int C>
-WaveKernel pick(bool full) {
-    return full ? dpf_wave_kernel<SPW, C, true> : dpf_wave_kernel<SPW, C, false>;
+WaveKernel pick(bool full, bool half) {
+    return half ? (full ? dpf_wave_kernel<SPW, C, true, true> : dpf_wave_kernel<SPW, C, false, true>)
+                : (full ? dpf_wave_kernel<SPW, C, true, false> : dpf_wave_kernel<SPW, C, false, false>);
 }
 }  // namespace
 
@@ -695,23 +697,23 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
     WaveKernel k = nullptr;
     int id = -1;
-    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full); id = 0; }
-    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full); id = 1; }
-    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full); id = 2; }
-    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full); id = 3; }
-    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full); id = 4; }
-    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full); id = 5; }
-    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full); id = 6; }
+    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, w.half); id = 0; }
+    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full, w.half); id = 1; }
+    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full, w.half); id = 2; }
+    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full, w.half); id = 3; }
+    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full, w.half); id = 4; }
+    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, w.half); id = 5; }
+    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, w.half); id = 6; }
     if (!k) return hipErrorInvalidValue;
-    static bool attr[7][2] = {};
-    if (!attr[id][full]) {   // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the static part)
+    static bool attr[7][2][2] = {};
+    if (!attr[id][full][w.half]) {   // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the static part)
         hipFuncAttributes fa{};
         hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
         if (e == hipSuccess)
             e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024 - (int)fa.sharedSizeBytes);
         if (e != hipSuccess) return e;
-        attr[id][full] = true;
+        attr[id][full][w.half] = true;
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(wave_wpb(w) * 64), lds, st, w, n_scen, pq, o);
     const hipError_t e = hipGetLastError();
