@@ -228,7 +228,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
     int *const knode = pairs + pair_n;                                // [C][L] node of each slot
     double2 *const reg0 = (double2 *)(knode + C * L);                 // per-scenario regions
-    const int RS = 3 * C * L + 3 * XC + 3 * nblk;                    // double2 per region
+    const int RS = (3 * C * L + 3 * XC + 3 * nblk) | 1;              // double2 per region (odd: V read-out banks)
     double2 *const SL = reg0 + sc * RS;
     double2 *const X = SL + 3 * C * L;
     double2 *const OFF = X + 3 * XC;
@@ -244,7 +244,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
     // 128-byte line per row), U loads in flight per thread, staged over the
     // per-scenario regions; then each slot picks its row
     {
-        double *stage = (double *)reg0;   // [6][nl][SPB]
+        double *stage = (double *)reg0;   // [6][nl][SPB + 1]: the pad spreads a slot's rows over the banks
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
         for (int i0 = 0; i0 < total; i0 += U * NT) {
@@ -260,7 +260,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + u * NT + (int)threadIdx.x;
-                if (i < total) stage[i] = r[u];
+                if (i < total) stage[(i / SPB) * (SPB + 1) + i % SPB] = r[u];
             }
         }
         // the feeder tables: all loads in flight before the LDS stores
@@ -303,8 +303,8 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             // Sld = (P + jQ) / (bkva/3)  (:46-50)
             sld_in[c][p] = make_double2(0.0, 0.0);
             if (row[c] >= 0)
-                sld_in[c][p] = make_double2(stage[((2 * p) * nl + row[c]) * SPB + sc] * inv_s3,
-                                            stage[((2 * p + 1) * nl + row[c]) * SPB + sc] * inv_s3);
+                sld_in[c][p] = make_double2(stage[((2 * p) * nl + row[c]) * (SPB + 1) + sc] * inv_s3,
+                                            stage[((2 * p + 1) * nl + row[c]) * (SPB + 1) + sc] * inv_s3);
         }
     }
     __syncthreads();
@@ -671,8 +671,8 @@ int wave_wpb(const WaveDev &w) { return (w.spw * w.C <= 2 ? 16 : 8) >> (w.half ?
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)wave_wpb(w) * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * (3 * w.C * L + 3 * xc + 3 * (size_t)w.nblk);
-    const size_t stage = 8 * 6 * (size_t)w.nl * spb;                 // the loads, staged over the regions
+    const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + 3 * (size_t)w.nblk) | 1);
+    const size_t stage = 8 * 6 * (size_t)w.nl * (spb + 1);           // the loads, staged over the regions
     const size_t agg = 8 * 8 * (size_t)wave_wpb(w) * 64;               // the last workgroup's fold
     return 16 * (9 * (size_t)w.C * L) + pairs + std::max(regions, std::max(stage, agg));
 }
