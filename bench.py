@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector peak
 SCEN_PER_GPU = 4096
 FEEDER_NODES, FEEDER_SEED, SCEN_SEED = 123, 123, 4096
 
@@ -191,6 +192,11 @@ def main():
     bpa = bytes_alg_per_scenario(nb, nn)
     achieved = bpa * B / avg_kern_s / 1e9
     traffic = _pmc_traffic()
+    # algorithmic fp64 flops per scenario = 123 Nb k_s + 60 Nn, over
+    # the timed launches, against the 78.6 TFLOP/s fp64 vector peak
+    k_sum = float(res["iters"][:args.steps].sum().item())
+    flops = 123.0 * nb * k_sum + 60.0 * nn * B * args.steps
+    fp64_tflops = flops / (avg_kern_s * args.steps) / 1e12
 
     if rank == 0:
         res = {
@@ -214,7 +220,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
                                     "wave": "dpf_wave_kernel", "generic": "dpf_generic_kernel"}[pf.kernel],
-                         "bytes_alg_per_scenario": bpa, "kernel_ms": avg_kern_s * 1e3},
+                         "bytes_alg_per_scenario": bpa, "kernel_ms": avg_kern_s * 1e3,
+                         "fp64": {"achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": fp64_tflops / FP64_PEAK_TFLOPS,
+                                  "mean_sweeps": k_sum / (B * args.steps)}},
             "aggregate": {"loss_sum_kw": float(tot[0]), "vmin": float(tot[1]), "vmax": float(tot[2]),
                           "n_conv": int(tot[3]), "n_nonconv": int(tot[4]), "n_over": int(tot[5]),
                           "n_under": int(tot[6]), "n_scen": int(tot[7])},

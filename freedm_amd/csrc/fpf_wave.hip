@@ -96,6 +96,27 @@ __device__ __forceinline__ double seg_incl(double x) {
     return x;
 }
 
+// N independent scans step by step, so their DPP/add chains interleave
+template <int L, int N>
+__device__ __forceinline__ void seg_incl_n(double (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] += dpp_d<0x111, 0xf, 0xf>(x[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] += dpp_d<0x112, 0xf, 0xf>(x[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] += dpp_d<0x114, 0xf, 0xf>(x[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] += dpp_d<0x118, 0xf, 0xf>(x[i]);
+    if (L >= 32) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) x[i] += dpp_d<0x142, 0xa, 0xf>(x[i]);
+    }
+    if (L >= 64) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) x[i] += dpp_d<0x143, 0xc, 0xf>(x[i]);
+    }
+}
+
 // the value of the segment's last lane
 template <int L>
 __device__ __forceinline__ double seg_last(double x, int seg) {
@@ -214,6 +235,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
     constexpr int NT = WPB * 64;
     extern __shared__ double2 lds[];
     if (DBG(4096)) return;
+    WSTAMP(0);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int seg = lane / L, li = lane % L;
     const int sc = wv * SPW + seg;                 // scenario within the workgroup
@@ -284,6 +306,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
         if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
     }
     __syncthreads();
+    WSTAMP(1);
     if (DBG(8192)) return;
     // this lane's block chain (lane b < nblk resolves block b), padded with the zero entry
     int bp[2 * WAVE_BD];
@@ -328,26 +351,34 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
     // last scenario is done.
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     bool done = !live;
+    WSTAMP(2);
     for (int it = 0; __ballot(!done) != 0; ++it) {
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(SL, (p * C + c) * L + li), v[c][p]);
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(SL, (p * C + c) * L + li), v[c][p]);
 
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of IL;
         // Einc is gathered at subtree ends only (leaves)
         cx tot[3], exl[3];
+        double sc6[6];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             cx acc = il[0][p];
             ib[0][p] = acc;
 #pragma unroll
             for (int c = 1; c < C; ++c) { acc = cadd(acc, il[c][p]); ib[c][p] = acc; }
-            const cx inc = mk(seg_incl<L>(acc.re), seg_incl<L>(acc.im));
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<L>(sc6);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx inc = mk(sc6[2 * p], sc6[2 * p + 1]);
             tot[p] = inc;   // the segment total in its last lane
-            exl[p] = csub(inc, acc);   // the lane's exclusive prefix
+            exl[p] = csub(inc, ib[C - 1][p]);   // the lane's exclusive prefix
 #pragma unroll
             for (int c = 0; c < C; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // Einc at this slot
         }
@@ -355,7 +386,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             const int ci = si_comp(si[c]);
-            if (ci >= 0) {
+            if (ci >= 0 && !DBG(32)) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
             }
@@ -400,7 +431,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             for (int a = 0; a < 3; ++a) {
                 cx tm[9];
 #pragma unroll
-                for (int l = 0; l < 3; ++l) tm[l * 3 + a] = ldx(tl, ((l * 3 + a) * C + c) * L + li);
+                for (int l = 0; l < 3; ++l) tm[l * 3 + a] = DBG(1) ? mk(0.001 * l, 0.002 * a) : ldx(tl, ((l * 3 + a) * C + c) * L + li);
                 g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
                 lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
             }
@@ -410,8 +441,13 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             cx acc = g[0][p];
 #pragma unroll
             for (int c = 1; c < C; ++c) { acc = cadd(acc, g[c][p]); g[c][p] = acc; }
-            const cx inc = mk(seg_incl<L>(acc.re), seg_incl<L>(acc.im));
-            const cx ex = csub(inc, acc);
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<L>(sc6);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx ex = csub(mk(sc6[2 * p], sc6[2 * p + 1]), g[C - 1][p]);
 #pragma unroll
             for (int c = 0; c < C; ++c) g[c][p] = cadd(ex, g[c][p]);   // Ginc at this slot
         }
@@ -419,7 +455,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             const int ci = si_comp(si[c]);
-            if (ci >= 0) {
+            if (ci >= 0 && !DBG(64)) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
             }
@@ -427,7 +463,8 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
         wfence();
         // block offsets, one lane per block (block 0, node 1's chain, has none);
         // the chain's index pairs sit in registers (bp), all its reads issue together
-        if (nblk <= L && bdepth <= WAVE_BD) {
+        if (DBG(8)) {
+        } else if (nblk <= L && bdepth <= WAVE_BD) {
             if (li < nblk) {
                 cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
 #pragma unroll
@@ -576,7 +613,9 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             wfence();
         }
         done = done || fin;
+        WSTAMP(3 + it);
     }
+    WSTAMP(40);
 
     // ---- fused batch aggregate [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over,
     // n_under, n_scen] over converged scenarios: the workgroup's partial in
@@ -630,6 +669,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             }
         }
     }
+    WSTAMP(41);
     if (agg) {
         __syncthreads();
         if (last_wg) {

@@ -2,6 +2,9 @@
 (freedm_amd/lib/libfreedm_pf_stamps.so, `make -C freedm_amd/csrc stamps`).
 Shares only -- the stamp build's own timing is not quoted (cdna_hip_programming.md 7).
 
+Stamps (fpf_wave.hip WSTAMP): 0 entry, 1 loads/tables staged, 2 Sld set up,
+3 + it end of sweep it, 40 after the loop, 41 V written out.
+
     NN=123 B=4096 FPF_WAVE_GEOM=2,4 python tools/wave_stamps.py
 """
 import ctypes
@@ -19,8 +22,6 @@ import torch  # noqa: E402
 
 from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder, _lib  # noqa: E402
 
-STAGES = ["IL", "bw_scan", "bw_gather", "drop", "fw_scan", "fw_resolve_V"]
-
 
 def main():
     nn = int(os.environ.get("NN", "123"))
@@ -32,7 +33,9 @@ def main():
     pf = PowerFlow(f, kernel="wave")
     pq = torch.from_numpy(scenario_loads(f, np.arange(B))).cuda()
     out = {"loss": torch.zeros(B, dtype=torch.float64, device="cuda"),
-           "iters": torch.zeros(B, dtype=torch.int32, device="cuda")}
+           "iters": torch.zeros(B, dtype=torch.int32, device="cuda"),
+           "v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device="cuda"),
+           "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device="cuda")}
     for _ in range(3):
         pf.solve_device(pq, out)
     torch.cuda.synchronize()
@@ -43,25 +46,18 @@ def main():
     rows = []
     for w in range(64):
         s = st[w]
-        if s[0] == 0 or s[1] == 0:
+        if s[0] == 0 or s[41] == 0:
             continue
-        d = {"init": s[1] - s[0], "epi": 0}
-        it = 0
-        prev = s[1]
-        while it < 9 and s[2 + 6 * it] != 0 and s[7 + 6 * it] != 0:
-            for q, nme in enumerate(STAGES):
-                cur = s[2 + 6 * it + q]
-                d[nme] = d.get(nme, 0) + (cur - prev)
-                prev = cur
-            it += 1
-        d["sweeps"] = it
-        d["total"] = prev - s[0]
+        sw = [s[3 + i] for i in range(37) if s[3 + i] != 0]
+        d = {"staging": s[1] - s[0], "sld": s[2] - s[1], "sweeps": sw[-1] - s[2], "n_sweeps": len(sw),
+             "after_loop": s[40] - sw[-1], "v_out": s[41] - s[40], "total": s[41] - s[0]}
+        d["per_sweep"] = d["sweeps"] / len(sw)
         rows.append(d)
-    keys = ["init"] + STAGES + ["total"]
-    mean = {k: float(np.mean([r.get(k, 0) for r in rows])) for k in keys}
-    print(json.dumps({"nn": nn, "B": B, "geom": [pf.info["tile"]], "waves": len(rows),
-                      "sweeps": float(np.mean([r["sweeps"] for r in rows])),
-                      "mean_cycles": mean, "share": {k: mean[k] / mean["total"] for k in keys if k != "total"}}))
+    keys = ["staging", "sld", "sweeps", "after_loop", "v_out", "total", "per_sweep", "n_sweeps"]
+    mean = {k: float(np.mean([r[k] for r in rows])) for k in keys}
+    print(json.dumps({"nn": nn, "B": B, "tile": pf.info["tile"], "waves": len(rows), "mean_cycles": mean,
+                      "share": {k: mean[k] / mean["total"] for k in ("staging", "sld", "sweeps", "after_loop",
+                                                                      "v_out")}}))
 
 
 if __name__ == "__main__":
