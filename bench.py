@@ -35,12 +35,25 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector peak
 SCEN_PER_GPU = 4096
 FEEDER_NODES, FEEDER_SEED, SCEN_SEED = 123, 123, 4096
+# BASELINE.json configs measurable on one GPU: (nodes, feeder seed, scenarios per GPU,
+# scenario seed, load model).  Config 2 is the bench line; 3 and 4 are diagnostics
+# (--config 3|4) for the roofline at throughput-sized batches.
+CONFIGS = {2: (123, 123, 4096, 4096, "scenario"),
+           3: (2048, 2048, 65536, 65536, "scenario"),
+           4: (123, 123, 131072, 1 << 20, "hosting")}
 
 
 def bytes_alg_per_scenario(nb: int, nn: int) -> int:
     """S in (48 B per branch) + V out (48 B per node) + iters,
     loss, Vmin, Vmax (28 B); state-resident model (state stays in LDS)."""
     return 48 * nb + 48 * nn + 28
+
+
+def bytes_alg_streaming(nb: int, nn: int, k_sum: float, n_scen: int) -> float:
+    """SURVEY.md 8(d) config 3 (Nb = 2047): the per-scenario state cannot stay
+    on chip, so each sweep also moves V and Ib once each way (192 B per branch
+    per sweep) on top of the compulsory bytes."""
+    return bytes_alg_per_scenario(nb, nn) * n_scen + 192.0 * nb * k_sum
 
 
 def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
@@ -94,7 +107,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scenarios", type=int, default=SCEN_PER_GPU, help="scenarios per GPU per step")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE config: 2 (the bench line), 3 (2048-bus x 65536), 4 (hosting study shard)")
+    ap.add_argument("--scenarios", type=int, default=0, help="scenarios per GPU per step (0: the config's)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-specialize", action="store_true")
@@ -116,17 +131,22 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
+    from freedm_amd import PowerFlow, hosting_loads, scenario_loads, synthetic_feeder
 
-    feeder = synthetic_feeder(FEEDER_NODES, FEEDER_SEED)
+    n_nodes, f_seed, b_cfg, s_seed, model = CONFIGS[args.config]
+    loads = {"scenario": scenario_loads, "hosting": hosting_loads}[model]
+    feeder = synthetic_feeder(n_nodes, f_seed)
     pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize,
                    exact=args.exact)
-    B = args.scenarios
+    B = args.scenarios or b_cfg
     pf.reserve(B)
     from freedm_amd import dist as D
     lo, hi = D.shard_range(rank, world, world * B)   # weak scaling: B global ids per GPU
-    ids = np.arange(lo, hi)
-    d_pq = torch.from_numpy(scenario_loads(feeder, ids, seed=SCEN_SEED)).to(dev)
+    # generated in chunks of 8192 scenarios (host memory), scenario-fastest on the GPU
+    d_pq = torch.empty((6, feeder.nl, B), dtype=torch.float64, device=dev)
+    for c in range(lo, hi, 8192):
+        e = min(hi, c + 8192)
+        d_pq[:, :, c - lo:e - lo] = torch.from_numpy(loads(feeder, np.arange(c, e), seed=s_seed)).to(dev)
     # per-scenario outputs of every timed step (the study's results); V is
     # overwritten step after step
     K = max(args.steps, 1)
@@ -190,17 +210,21 @@ def main():
     value = n_conv_all / elapsed
     nb, nn = pf.info["nb"], pf.nn
     bpa = bytes_alg_per_scenario(nb, nn)
-    achieved = bpa * B / avg_kern_s / 1e9
-    traffic = _pmc_traffic()
+    k_sum = float(res["iters"][:args.steps].sum().item())
+    if args.config == 3:
+        bytes_launch = bytes_alg_streaming(nb, nn, k_sum / args.steps, B)
+    else:
+        bytes_launch = bpa * B
+    achieved = bytes_launch / avg_kern_s / 1e9
+    traffic = _pmc_traffic() if (args.config == 2 and B == SCEN_PER_GPU) else None
     # algorithmic fp64 flops per scenario = 123 Nb k_s + 60 Nn, over
     # the timed launches, against the 78.6 TFLOP/s fp64 vector peak
-    k_sum = float(res["iters"][:args.steps].sum().item())
     flops = 123.0 * nb * k_sum + 60.0 * nn * B * args.steps
     fp64_tflops = flops / (avg_kern_s * args.steps) / 1e12
 
     if rank == 0:
         res = {
-            "metric": "converged power-flow scenarios/sec, 123-bus feeder",
+            "metric": "converged power-flow scenarios/sec, %d-bus feeder" % n_nodes,
             "value": value,
             "unit": "scenarios/s",
             "n_gpus": world,
@@ -211,8 +235,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64 (complex fp64)",
-            "data": "synthetic (seeded 123-bus radial feeder + seeded load/PV scenarios)",
-            "config": {"workload": f"BASELINE config 2: 123-bus feeder, {B} scenarios per GPU per step",
+            "data": f"synthetic (seeded {n_nodes}-bus radial feeder + seeded {model} load/PV scenarios)",
+            "config": {"workload": f"BASELINE config {args.config}: {n_nodes}-bus feeder, {B} scenarios per GPU per step",
                        "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
                        "tile": pf.info["tile"], "specialized": pf.info["specialized"], "exact": bool(args.exact),
                        "parallelism": f"scenario shards x{world}"},
@@ -220,7 +244,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
                                     "wave": "dpf_wave_kernel", "generic": "dpf_generic_kernel"}[pf.kernel],
-                         "bytes_alg_per_scenario": bpa, "kernel_ms": avg_kern_s * 1e3,
+                         "bytes_alg_per_scenario": bytes_launch / B, "kernel_ms": avg_kern_s * 1e3,
                          "fp64": {"achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": fp64_tflops / FP64_PEAK_TFLOPS,
                                   "mean_sweeps": k_sum / (B * args.steps)}},
@@ -230,7 +254,7 @@ def main():
             "converged_per_step_rank0": conv_per_step,
             "host_submit_ms_per_step": t_submit / args.steps * 1e3,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(feeder, seconds=args.cpu_seconds)
             res["speedup_vs_cpu"] = value / res["cpu_baseline"]["value"]
         print(json.dumps(res), flush=True)
