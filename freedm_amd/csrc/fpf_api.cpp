@@ -846,6 +846,7 @@ struct RtcPlan {
 };
 
 constexpr int MAX_TILE = 16;   // = MAX_SEQ_TILE of fpf_tiled_body.h (flag arrays)
+constexpr int AUTO_MIN_TILE = 4;   // smallest interpreted tile the auto choice prefers to the generic kernel
 
 bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
     int force_t = 0;
@@ -1045,8 +1046,27 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     std::vector<char> blob;
     const size_t o_tz = push_blob(blob, h.tz);
     const size_t o_il = push_blob(blob, h.il);
-    const size_t o_bw = push_blob(blob, h.bw);
-    const size_t o_fw = push_blob(blob, h.fw);
+    // generic kernel: flag (kind | 2) the first op touching each Ib slot in a
+    // sweep, so it starts from the constant 0 instead of re-zeroing and
+    // re-reading the slot (slots no op touches are zeroed once per launch)
+    std::vector<BwOp> bw_dev = h.bw;
+    {
+        std::vector<char> touched(h.nn > 0 ? h.nn : 1, 0);
+        for (auto &op : bw_dev)
+            if (op.idx >= 0 && op.idx < (int)touched.size() && !touched[op.idx]) {
+                touched[op.idx] = 1;
+                op.kind |= 2;
+            }
+    }
+    const size_t o_bw = push_blob(blob, bw_dev);
+    // generic kernel: flag (pad | 1) a forward op whose source V is the one the
+    // previous op writes, so it is carried in registers
+    std::vector<FwOp> fw_dev = h.fw;
+    for (size_t q = 0; q < fw_dev.size(); ++q) {
+        fw_dev[q].pad = 0;
+        if (q > 0 && fw_dev[q].src >= 0 && fw_dev[q].src == fw_dev[q - 1].dst) fw_dev[q].pad = 1;
+    }
+    const size_t o_fw = push_blob(blob, fw_dev);
     const size_t o_node = push_blob(blob, h.node);
     const size_t o_node_rtc = push_blob(blob, h.node_rtc);
     const size_t o_sbw = push_blob(blob, h.seq_bw);
@@ -1139,7 +1159,11 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
         }
     }
-    if (kern == FPF_KERNEL_AUTO) kern = (h.wf && (tile >= 1 || have_plan)) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
+    // auto: the interpreted tiled kernel only pays with several scenarios per
+    // workgroup; below that (large feeders, e.g. 2048-bus at tile 1: 794 ms vs
+    // 112 ms per 65536-scenario batch, profiles/r01f) the generic kernel wins
+    if (kern == FPF_KERNEL_AUTO)
+        kern = (h.wf && (have_plan || tile >= AUTO_MIN_TILE)) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
     if (kern == FPF_KERNEL_TILED && (!h.wf || (tile < 1 && !have_plan))) {
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_UNSUPPORTED,

@@ -53,42 +53,90 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
             V.st(j * 3 + p, v0[p]);                                  // :92-96
         }
 
+    // IL and Ib are fresh zeros every sweep (:106, :134).  The load-current ops
+    // write the same IL slots every sweep and each Ib slot's first op reads the
+    // constant 0 (BwOp kind | 2), so only the slots no op writes need zeroing,
+    // and that once: they are never written afterwards
+    for (int k = 0; k < nn * 3; ++k) IL.st(k, mk(0, 0));
+    for (int k = 0; k < (nn - 1) * 3; ++k) Ib.st(k, mk(0, 0));
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     int iters = 0, status = 1;
     for (int it = 0; it < f.mxitr; ++it) {
         // load currents  :106-130
-        for (int k = 0; k < nn * 3; ++k) IL.st(k, mk(0, 0));
-        for (int q = 0; q < f.n_il; ++q) {
+        // 4 ops' loads issued before their stores (IL, Sld and V are disjoint
+        // slot ranges; the stores keep list order, so a repeated slot's last write wins)
+        int q = 0;
+        for (; q + 4 <= f.n_il; q += 4) {
+            IlOp op[4];
+            cx sl[4][3], vv[4][3];
+            for (int u = 0; u < 4; ++u) {
+                op[u] = f.il_ops[q + u];
+                for (int p = 0; p < 3; ++p) {
+                    sl[u][p] = Sld.ld_(op[u].row * 3 + p);
+                    vv[u][p] = V.ld_(op[u].ndr * 3 + p);
+                }
+            }
+            for (int u = 0; u < 4; ++u)
+                for (int p = 0; p < 3; ++p) IL.st((op[u].ndr - 1) * 3 + p, load_current(sl[u][p], vv[u][p]));
+        }
+        for (; q < f.n_il; ++q) {
             const IlOp op = f.il_ops[q];
             for (int p = 0; p < 3; ++p)
                 IL.st((op.ndr - 1) * 3 + p, load_current(Sld.ld_(op.row * 3 + p), V.ld_(op.ndr * 3 + p)));
         }
         // backward sweep  :134-160
-        for (int k = 0; k < (nn - 1) * 3; ++k) Ib.st(k, mk(0, 0));
         cx ibl[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
         for (int q = 0; q < f.n_bw; ++q) {
             const BwOp op = f.bw_ops[q];
-            if (op.kind == 1) {
-                for (int p = 0; p < 3; ++p) Ib.st(op.idx * 3 + p, cadd(Ib.ld_(op.idx * 3 + p), ibl[p]));
+            const bool first = op.kind & 2;    // wave-uniform
+            auto ib = [&](int p) { return first ? mk(0, 0) : Ib.ld_(op.idx * 3 + p); };
+            if (op.kind & 1) {
+                for (int p = 0; p < 3; ++p) Ib.st(op.idx * 3 + p, cadd(ib(p), ibl[p]));
                 for (int p = 0; p < 3; ++p) ibl[p] = mk(0, 0);
             } else {
                 for (int p = 0; p < 3; ++p) {
-                    const cx x = cadd(cadd(Ib.ld_(op.idx * 3 + p), ibl[p]), IL.ld_(op.idx * 3 + p));
+                    const cx x = cadd(cadd(ib(p), ibl[p]), IL.ld_(op.idx * 3 + p));
                     Ib.st(op.idx * 3 + p, x);
                     ibl[p] = x;
                 }
             }
         }
         // forward sweep  :163-195
-        for (int q = 0; q < f.n_fw; ++q) {
-            const FwOp op = f.fw_ops[q];
-            const double *t = f.tz + 18 * (size_t)q;
-            const cx b0 = Ib.ld_(op.ib * 3 + 0), b1 = Ib.ld_(op.ib * 3 + 1), b2 = Ib.ld_(op.ib * 3 + 2);
+        // software-pipelined: op q+1's Ib (not written here) and source V are
+        // loaded before op q stores; when op q+1 reads the V op q writes
+        // (FwOp.pad & 1, the chain case) the value comes from registers
+        if (f.n_fw > 0) {
+            FwOp op = f.fw_ops[0];
+            cx b[3], sv[3];
             for (int p = 0; p < 3; ++p) {
-                const cx sv = op.src < 0 ? v0[p] : V.ld_(op.src * 3 + p);
-                cx rv = csub(sv, drop_col(t, b0, b1, b2, p));
-                if (op.mask & (1 << p)) rv = mk(0, 0);
-                V.st(op.dst * 3 + p, rv);
+                b[p] = Ib.ld_(op.ib * 3 + p);
+                sv[p] = op.src < 0 ? v0[p] : V.ld_(op.src * 3 + p);
+            }
+            for (int q = 0; q < f.n_fw; ++q) {
+                const bool more = q + 1 < f.n_fw;
+                FwOp nx = op;
+                cx nb[3], nsv[3];
+                if (more) {
+                    nx = f.fw_ops[q + 1];
+                    for (int p = 0; p < 3; ++p) {
+                        nb[p] = Ib.ld_(nx.ib * 3 + p);
+                        nsv[p] = mk(0, 0);
+                        if (!(nx.pad & 1)) nsv[p] = nx.src < 0 ? v0[p] : V.ld_(nx.src * 3 + p);
+                    }
+                }
+                const double *t = f.tz + 18 * (size_t)q;
+                for (int p = 0; p < 3; ++p) {
+                    cx rv = csub(sv[p], drop_col(t, b[0], b[1], b[2], p));
+                    if (op.mask & (1 << p)) rv = mk(0, 0);
+                    V.st(op.dst * 3 + p, rv);
+                    if (more && (nx.pad & 1)) nsv[p] = rv;
+                }
+                if (more)
+                    for (int p = 0; p < 3; ++p) {
+                        b[p] = nb[p];
+                        sv[p] = nsv[p];
+                    }
+                op = nx;
             }
         }
         // convergence  :199-210

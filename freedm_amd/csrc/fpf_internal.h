@@ -25,12 +25,13 @@ namespace fpf {
 // phase p zeroed when bit p of mask is set (DPF_return7.cpp:163-195).
 // src < 0 means the constant V0 (the special first branch, :168).
 struct FwOp {
-    int32_t dst, src, ib, code, mask, pad;
+    int32_t dst, src, ib, code, mask, pad;   // generic kernel: pad & 1 = src is the previous op's dst
 };
 
 // Backward-sweep op (DPF_return7.cpp:136-160), executed in list order:
 //   kind 0 (branch)    : Ib[idx] = (Ib[idx] + Ibl) + IL[idx];  Ibl = Ib[idx]
 //   kind 1 (separator) : Ib[idx] = Ib[idx] + Ibl;              Ibl = 0
+//   kind | 2           : first op on Ib[idx] in the sweep: Ib[idx] reads as 0
 struct BwOp {
     int32_t kind, idx;
 };

@@ -95,7 +95,7 @@ def test_auto_kernel_choice():
     assert _pf(g["Dl"], g["Z"]).kernel == "wave"            # fast mode (default)
     assert _pf(g["Dl"], g["Z"], exact=1).kernel == "tiled"  # the reference's roundings
     g4 = load_golden("g4_2048bus")
-    assert _pf(g4["Dl"], g4["Z"]).kernel == "tiled"         # above the wave kernel's size
+    assert _pf(g4["Dl"], g4["Z"]).kernel == "generic"       # above the wave kernel's size, tile 1
     f = F.demo_feeder()
     Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # 2->3 before 1->2: legal for the reference, not well formed
     pf = _pf(Dl, f.Z)
