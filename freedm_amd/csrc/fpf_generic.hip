@@ -85,20 +85,35 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
                 IL.st((op.ndr - 1) * 3 + p, load_current(Sld.ld_(op.row * 3 + p), V.ld_(op.ndr * 3 + p)));
         }
         // backward sweep  :134-160
+        // op q+1's IL (not written here) is loaded before op q runs
         cx ibl[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
-        for (int q = 0; q < f.n_bw; ++q) {
-            const BwOp op = f.bw_ops[q];
-            const bool first = op.kind & 2;    // wave-uniform
-            auto ib = [&](int p) { return first ? mk(0, 0) : Ib.ld_(op.idx * 3 + p); };
-            if (op.kind & 1) {
-                for (int p = 0; p < 3; ++p) Ib.st(op.idx * 3 + p, cadd(ib(p), ibl[p]));
-                for (int p = 0; p < 3; ++p) ibl[p] = mk(0, 0);
-            } else {
-                for (int p = 0; p < 3; ++p) {
-                    const cx x = cadd(cadd(ib(p), ibl[p]), IL.ld_(op.idx * 3 + p));
-                    Ib.st(op.idx * 3 + p, x);
-                    ibl[p] = x;
+        if (f.n_bw > 0) {
+            BwOp op = f.bw_ops[0];
+            cx il[3];
+            for (int p = 0; p < 3; ++p) il[p] = (op.kind & 1) ? mk(0, 0) : IL.ld_(op.idx * 3 + p);
+            for (int q = 0; q < f.n_bw; ++q) {
+                const bool more = q + 1 < f.n_bw;
+                BwOp nx = op;
+                cx nil[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+                if (more) {
+                    nx = f.bw_ops[q + 1];
+                    if (!(nx.kind & 1))
+                        for (int p = 0; p < 3; ++p) nil[p] = IL.ld_(nx.idx * 3 + p);
                 }
+                const bool first = op.kind & 2;    // wave-uniform
+                auto ib = [&](int p) { return first ? mk(0, 0) : Ib.ld_(op.idx * 3 + p); };
+                if (op.kind & 1) {
+                    for (int p = 0; p < 3; ++p) Ib.st(op.idx * 3 + p, cadd(ib(p), ibl[p]));
+                    for (int p = 0; p < 3; ++p) ibl[p] = mk(0, 0);
+                } else {
+                    for (int p = 0; p < 3; ++p) {
+                        const cx x = cadd(cadd(ib(p), ibl[p]), il[p]);
+                        Ib.st(op.idx * 3 + p, x);
+                        ibl[p] = x;
+                    }
+                }
+                for (int p = 0; p < 3; ++p) il[p] = nil[p];
+                op = nx;
             }
         }
         // forward sweep  :163-195
