@@ -1059,6 +1059,17 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             }
     }
     const size_t o_bw = push_blob(blob, bw_dev);
+    // generic kernel: the backward sweep evaluates IL(idx) itself from the op
+    // that last writes that slot in the load-current pass (list order)
+    std::vector<IlOp> bw_il(h.bw.size(), IlOp{-1, 0});
+    {
+        std::vector<IlOp> last(h.nn > 0 ? h.nn : 1, IlOp{-1, 0});
+        for (const auto &op : h.il)
+            if (op.ndr - 1 >= 0 && op.ndr - 1 < (int)last.size()) last[op.ndr - 1] = op;
+        for (size_t q = 0; q < h.bw.size(); ++q)
+            if (h.bw[q].kind == 0 && h.bw[q].idx >= 0 && h.bw[q].idx < (int)last.size()) bw_il[q] = last[h.bw[q].idx];
+    }
+    const size_t o_bwil = push_blob(blob, bw_il);
     // generic kernel: flag (pad | 1) a forward op whose source V is the one the
     // previous op writes, so it is carried in registers
     std::vector<FwOp> fw_dev = h.fw;
@@ -1106,6 +1117,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     d.tz = (const double *)(base + o_tz);
     d.il_ops = (const IlOp *)(base + o_il);
     d.bw_ops = (const BwOp *)(base + o_bw);
+    d.bw_il = (const IlOp *)(base + o_bwil);
     d.fw_ops = (const FwOp *)(base + o_fw);
     d.node_ops = (const NodeOp *)(base + o_node);
     d.seq_bw = (const SeqBw *)(base + o_sbw);

@@ -54,17 +54,19 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
         }
 
     // IL and Ib are fresh zeros every sweep (:106, :134).  The load-current ops
-    // write the same IL slots every sweep and each Ib slot's first op reads the
-    // constant 0 (BwOp kind | 2), so only the slots no op writes need zeroing,
-    // and that once: they are never written afterwards
+    // write the same IL slots every sweep (stored once, final sweep) and each Ib
+    // slot's first op reads the constant 0 (BwOp kind | 2), so only the slots no
+    // op writes need zeroing, and that once: they are never written afterwards
     for (int k = 0; k < nn * 3; ++k) IL.st(k, mk(0, 0));
     for (int k = 0; k < (nn - 1) * 3; ++k) Ib.st(k, mk(0, 0));
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     int iters = 0, status = 1;
-    for (int it = 0; it < f.mxitr; ++it) {
-        // load currents  :106-130
-        // 4 ops' loads issued before their stores (IL, Sld and V are disjoint
-        // slot ranges; the stores keep list order, so a repeated slot's last write wins)
+    // load currents  :106-130.  IL itself is only stored for the final sweep
+    // (the post-processing's Ild); during the sweeps the backward pass
+    // evaluates each IL it adds from the same Sld and (not yet updated) V.
+    // 4 ops' loads are issued before their stores (IL, Sld and V are disjoint
+    // slot ranges; the stores keep list order, so a repeated slot's last write wins)
+    auto store_il = [&]() {
         int q = 0;
         for (; q + 4 <= f.n_il; q += 4) {
             IlOp op[4];
@@ -84,22 +86,35 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
             for (int p = 0; p < 3; ++p)
                 IL.st((op.ndr - 1) * 3 + p, load_current(Sld.ld_(op.row * 3 + p), V.ld_(op.ndr * 3 + p)));
         }
+    };
+    for (int it = 0; it < f.mxitr; ++it) {
         // backward sweep  :134-160
-        // op q+1's IL (not written here) is loaded before op q runs
+        // IL(idx) of a branch op = load_current of the op that last writes that
+        // slot in the load-current pass (FeederDev.bw_il; none: 0).  Op q+1's
+        // Sld and V operands are loaded before op q runs (neither is written here)
         cx ibl[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+        auto il_operands = [&](int q, cx sl[3], cx vv[3]) {
+            const IlOp w = f.bw_il[q];
+            for (int p = 0; p < 3; ++p) {
+                sl[p] = w.row < 0 ? mk(0, 0) : Sld.ld_(w.row * 3 + p);
+                vv[p] = w.row < 0 ? mk(0, 0) : V.ld_(w.ndr * 3 + p);
+            }
+        };
         if (f.n_bw > 0) {
             BwOp op = f.bw_ops[0];
-            cx il[3];
-            for (int p = 0; p < 3; ++p) il[p] = (op.kind & 1) ? mk(0, 0) : IL.ld_(op.idx * 3 + p);
+            cx sl[3], vv[3];
+            il_operands(0, sl, vv);
             for (int q = 0; q < f.n_bw; ++q) {
                 const bool more = q + 1 < f.n_bw;
                 BwOp nx = op;
-                cx nil[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+                cx nsl[3], nvv[3];
                 if (more) {
                     nx = f.bw_ops[q + 1];
-                    if (!(nx.kind & 1))
-                        for (int p = 0; p < 3; ++p) nil[p] = IL.ld_(nx.idx * 3 + p);
+                    il_operands(q + 1, nsl, nvv);
                 }
+                const bool has_il = f.bw_il[q].row >= 0;    // wave-uniform
+                cx il[3];
+                for (int p = 0; p < 3; ++p) il[p] = has_il ? load_current(sl[p], vv[p]) : mk(0, 0);
                 const bool first = op.kind & 2;    // wave-uniform
                 auto ib = [&](int p) { return first ? mk(0, 0) : Ib.ld_(op.idx * 3 + p); };
                 if (op.kind & 1) {
@@ -112,10 +127,25 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
                         ibl[p] = x;
                     }
                 }
-                for (int p = 0; p < 3; ++p) il[p] = nil[p];
+                if (more)
+                    for (int p = 0; p < 3; ++p) {
+                        sl[p] = nsl[p];
+                        vv[p] = nvv[p];
+                    }
                 op = nx;
             }
         }
+        // convergence  :199-210 -- tested here, before the forward sweep, which
+        // does not touch Ib; the forward sweep still runs in the final sweep
+        double errmx = 0;
+        for (int p = 0; p < 3; ++p) {
+            const cx d = csub(Ib.ld_(p), ibo[p]);
+            const double df = hypot(d.re, d.im);
+            if (p == 0 || df > errmx) errmx = df;
+        }
+        for (int p = 0; p < 3; ++p) ibo[p] = Ib.ld_(p);
+        const bool conv = errmx < f.eps;
+        if (conv || it + 1 == f.mxitr) store_il();   // the final sweep's IL (Ild)
         // forward sweep  :163-195
         // software-pipelined: op q+1's Ib (not written here) and source V are
         // loaded before op q stores; when op q+1 reads the V op q writes
@@ -154,16 +184,8 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
                 op = nx;
             }
         }
-        // convergence  :199-210
-        double errmx = 0;
-        for (int p = 0; p < 3; ++p) {
-            const cx d = csub(Ib.ld_(p), ibo[p]);
-            const double df = hypot(d.re, d.im);
-            if (p == 0 || df > errmx) errmx = df;
-        }
-        for (int p = 0; p < 3; ++p) ibo[p] = Ib.ld_(p);
         iters = it + 1;
-        if (errmx < f.eps) { status = 0; break; }
+        if (conv) { status = 0; break; }
     }
 
     // post-processing (:222-253) fused with the VVC reductions

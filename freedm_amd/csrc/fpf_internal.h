@@ -103,6 +103,8 @@ struct FeederDev {
     int32_t slot_bytes;      // bytes per state slot of the specialised layout (padded, see fpf_api.cpp: bank_layout)
     int32_t phase_bytes;     // bytes between the phases of one slot (specialised layout)
     int32_t temp_lds;        // specialised layout: TEMP blocks staged in LDS
+    const IlOp *bw_il;       // generic only, [n_bw]: the load-current op whose IL the
+                             // branch op reads (the slot's last writer), row < 0: none
 };
 
 // Wave kernel (fpf_wave.hip, fast mode): SPW scenarios per wavefront, one
