@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
                     help="BASELINE config: 2 (the bench line), 3 (2048-bus x 65536), 4 (hosting study shard)")
     ap.add_argument("--scenarios", type=int, default=0, help="scenarios per GPU per step (0: the config's)")
+    ap.add_argument("--nodes", type=int, default=0, help="diagnostic: synthetic feeder size override (seed = nodes)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-specialize", action="store_true")
@@ -134,6 +135,8 @@ def main():
     from freedm_amd import PowerFlow, hosting_loads, scenario_loads, synthetic_feeder
 
     n_nodes, f_seed, b_cfg, s_seed, model = CONFIGS[args.config]
+    if args.nodes:
+        n_nodes, f_seed = args.nodes, args.nodes
     loads = {"scenario": scenario_loads, "hosting": hosting_loads}[model]
     feeder = synthetic_feeder(n_nodes, f_seed)
     pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize,
