@@ -56,27 +56,80 @@ def bytes_alg_streaming(nb: int, nn: int, k_sum: float, n_scen: int) -> float:
     return bytes_alg_per_scenario(nb, nn) * n_scen + 192.0 * nb * k_sum
 
 
-def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
-    from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    from freedm_amd import scenario_loads
-    pq = scenario_loads(feeder, np.arange(chunk), seed=SCEN_SEED)
-    n_conv = 0
-    n_done = 0
-    passes = 0
+def usable_cpus() -> tuple[int, dict]:
+    """CPUs this process can actually run on: the affinity mask, capped by the
+    cgroup CPU quota (cpu.max) -- on the GPU box the affinity mask lists all 256
+    host threads while the quota grants 16 CPUs of time, so more threads than
+    the quota only time-slice."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, {"affinity": aff, "cgroup_quota_cpus": quota, "nproc_host": os.cpu_count()}
+
+
+def _host_cores():
+    """(physical cores, logical CPUs) of the host from /proc/cpuinfo."""
+    phys, logical = set(), 0
+    try:
+        pid = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("processor"):
+                logical += 1
+            elif line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                phys.add((pid, core))
+    except OSError:
+        pass
+    return len(phys) or None, logical or None
+
+
+def _time_oracle(O, feeder, pq, threads: int, seconds: float):
+    n_conv = passes = 0
     t0 = time.perf_counter()
     while True:
         r = O.dpf_batch(feeder.Dl, feeder.Z, pq, nthreads=threads, want_full=False)
         n_conv += int((r["status"] == 0).sum())
-        n_done += chunk
         passes += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": n_conv / dt, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} passes x {chunk} scenarios of the config-2 batch (123-bus, seed {SCEN_SEED}), "
-                      f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s",
-            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    return n_conv / dt, passes, dt
+
+
+def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
+    """The CPU oracle (oracle/ref_dpf.c, a scalar port of DPF_return7 + the VVC
+    reductions) on this host: once on every usable CPU (value, cores) and once
+    on a single core.  Bounded sample: `seconds` of the all-core leg plus
+    seconds/3 of the single-core leg over one chunk of the config-2 batch."""
+    from oracle import oracle as O
+    from freedm_amd import scenario_loads
+    threads, cpu_info = usable_cpus()
+    pq = scenario_loads(feeder, np.arange(chunk), seed=SCEN_SEED)
+    v_all, passes, dt = _time_oracle(O, feeder, pq, threads, seconds)
+    pq1 = np.ascontiguousarray(pq[:, :, :4096])
+    v_one, passes1, dt1 = _time_oracle(O, feeder, pq1, 1, max(1.0, seconds / 3))
+    phys, logical = _host_cores()
+    out = {"value": v_all, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
+           "sample": f"{passes} passes x {chunk} scenarios of the config-2 batch (123-bus, seed {SCEN_SEED}), "
+                     f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s; single core: "
+                     f"{passes1} passes x 4096 scenarios, {dt1:.1f} s",
+           "single_core": {"value": v_one, "unit": "converged scenarios/s", "cores": 1},
+           "parallel_efficiency": v_all / (v_one * threads),
+           "cpu_model": _cpu_model(), "host_physical_cores": phys, "host_logical_cpus": logical}
+    out.update(cpu_info)
+    if phys:
+        # not measured: what the whole host would give if the port scaled linearly
+        # over every physical core (the box's cgroup grants only `cores` CPUs)
+        out["full_host_linear_estimate"] = v_one * phys
+    return out
 
 
 def _cpu_model():
@@ -258,8 +311,12 @@ def main():
             "host_submit_ms_per_step": t_submit / args.steps * 1e3,
         }
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(feeder, seconds=args.cpu_seconds)
-            res["speedup_vs_cpu"] = value / res["cpu_baseline"]["value"]
+            cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
+            res["cpu_baseline"] = cb
+            res["speedup_vs_cpu"] = value / cb["value"]
+            res["speedup_vs_cpu_single_core"] = value / cb["single_core"]["value"]
+            if cb.get("full_host_linear_estimate"):
+                res["speedup_vs_cpu_full_host_estimate"] = value / cb["full_host_linear_estimate"]
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -66,6 +66,15 @@ struct fpf_feeder {
     // wave kernel (fast mode)
     void *d_wave = nullptr;
     WaveDev wdev{};
+    // the partials + ticket scratch is shared by every aggregating launch on
+    // this feeder (fused wave/specialised aggregate, fpf_aggregate_device): a
+    // launch on another stream than the previous one first waits for it
+    hipEvent_t agg_event = nullptr;
+    hipStream_t agg_stream = nullptr;
+    bool agg_pending = false;
+    // auto choice between the interpreted tiled and the generic kernel, made
+    // per batch (both table sets are built): tiled below AUTO_GENERIC_MIN_SCEN
+    bool auto_batch = false;
 };
 
 static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
@@ -846,7 +855,12 @@ struct RtcPlan {
 };
 
 constexpr int MAX_TILE = 16;   // = MAX_SEQ_TILE of fpf_tiled_body.h (flag arrays)
-constexpr int AUTO_MIN_TILE = 4;   // smallest interpreted tile the auto choice prefers to the generic kernel
+// Auto choice between the interpreted tiled kernel and the generic kernel (no
+// hipRTC plan): per batch.  The generic kernel needs >= ~32 k scenarios (one
+// wavefront per SIMD) to hide its memory latency; the tiled kernel scales
+// linearly from few scenarios (profiles/r01i/autotile: 123- to
+// 1024-bus feeders, generic faster at 65 536, tiled faster at 4 096).
+constexpr int AUTO_GENERIC_MIN_SCEN = 32768;
 
 bool plan_rtc(const HostFeeder &h, const fpf_opts &o, RtcPlan *out) {
     int force_t = 0;
@@ -1174,14 +1188,19 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     // auto: the interpreted tiled kernel only pays with several scenarios per
     // workgroup; below that (large feeders, e.g. 2048-bus at tile 1: 794 ms vs
     // 112 ms per 65536-scenario batch, profiles/r01f) the generic kernel wins
-    if (kern == FPF_KERNEL_AUTO)
-        kern = (h.wf && (have_plan || tile >= AUTO_MIN_TILE)) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
+    bool auto_batch = false;
+    if (kern == FPF_KERNEL_AUTO) {
+        auto_batch = h.wf && !have_plan && tile >= 1;
+        // reported kernel: the one a large (hosting-study) batch runs
+        kern = (h.wf && have_plan) ? FPF_KERNEL_TILED : FPF_KERNEL_GENERIC;
+    }
     if (kern == FPF_KERNEL_TILED && (!h.wf || (tile < 1 && !have_plan))) {
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_UNSUPPORTED,
                     "tiled kernel needs a well-formed feeder that fits in LDS: " + (h.wf ? std::string("too large") : h.wf_why));
     }
     in.kernel = kern;
+    f->auto_batch = auto_batch;
     if (kern == FPF_KERNEL_TILED && have_plan) {
         const RtcSpec sp = make_rtc_spec(h, plan, o);
         std::string err;
@@ -1204,7 +1223,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         fpf_feeder_destroy(f);
         return fail(ctx, FPF_ERR_UNSUPPORTED, "specialised kernel failed and the interpreted one does not fit: " + ctx->err);
     }
-    in.tile = kern == FPF_KERNEL_TILED ? d.tile : (kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : 0);
+    in.tile = (kern == FPF_KERNEL_TILED || auto_batch) ? d.tile
+                                                        : (kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : 0);
     in.specialized = f->rtc ? 1 : 0;
     *out = f;
     return FPF_OK;
@@ -1225,7 +1245,32 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_partials);
     (void)hipFree(f->d_ticket);
     (void)hipFree(f->d_wave);
+    if (f->agg_event) (void)hipEventDestroy(f->agg_event);
+    if (f->rtc) rtc_release(f->rtc_kernel);
+    if (f->rtc_ib) rtc_release(f->rtc_kernel_ib);
     delete f;
+}
+
+// Order an aggregating launch on `st` after the previous one on this feeder
+// (they share d_partials / d_ticket); call agg_after() once it is enqueued.
+static hipError_t agg_before(fpf_feeder *f, hipStream_t st) {
+    if (!f->agg_event) {
+        hipError_t e = hipEventCreateWithFlags(&f->agg_event, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    if (f->agg_pending && f->agg_stream != st) return hipStreamWaitEvent(st, f->agg_event, 0);
+    return hipSuccess;
+}
+// the kernel a batch of n_scen scenarios runs on
+static int kernel_for(const fpf_feeder *f, int n_scen) {
+    if (f->auto_batch) return n_scen >= AUTO_GENERIC_MIN_SCEN ? FPF_KERNEL_GENERIC : FPF_KERNEL_TILED;
+    return f->info.kernel;
+}
+
+static hipError_t agg_after(fpf_feeder *f, hipStream_t st) {
+    f->agg_stream = st;
+    f->agg_pending = true;
+    return hipEventRecord(f->agg_event, st);
 }
 
 // the options the feeder was created with (fpf_vvc.cpp)
@@ -1241,7 +1286,18 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
     if (!f || max_scen < 0) return FPF_ERR_ARG;
     fpf_ctx *ctx = f->ctx;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    if (max_scen <= f->cap) return FPF_OK;
+    const bool need_scratch = kernel_for(f, max_scen) == FPF_KERNEL_GENERIC;
+    if (max_scen <= f->cap) {
+        if (!need_scratch || (f->d_scratch && f->scratch_ld >= (size_t)max_scen)) return FPF_OK;
+        (void)hipFree(f->d_scratch);
+        f->d_scratch = nullptr;
+        f->scratch_ld = 0;
+        const size_t ld = ((size_t)max_scen + 63) & ~(size_t)63;
+        const size_t per = (size_t)6 * (2 * f->dev.nl + 2 * f->dev.nn - 1);
+        HIPCHK(ctx, hipMalloc(&f->d_scratch, sizeof(double) * per * ld));
+        f->scratch_ld = ld;
+        return FPF_OK;
+    }
     (void)hipFree(f->d_iters);
     (void)hipFree(f->d_status);
     (void)hipFree(f->d_loss);
@@ -1256,7 +1312,7 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
     HIPCHK(ctx, hipMalloc(&f->d_loss, sizeof(double) * max_scen));
     HIPCHK(ctx, hipMalloc(&f->d_vmin, sizeof(double) * max_scen));
     HIPCHK(ctx, hipMalloc(&f->d_vmax, sizeof(double) * max_scen));
-    if (f->info.kernel == FPF_KERNEL_GENERIC) {
+    if (need_scratch) {
         const size_t ld = ((size_t)max_scen + 63) & ~(size_t)63;
         const size_t per = (size_t)6 * (2 * f->dev.nl + 2 * f->dev.nn - 1);
         HIPCHK(ctx, hipMalloc(&f->d_scratch, sizeof(double) * per * ld));
@@ -1296,11 +1352,12 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     o.ticket = nullptr;
     hipError_t e;
     bool agg_done = false;
+    const int kern = kernel_for(f, n_scen);
     static const bool fused_agg = !getenv("FPF_FUSED_AGG") || atoi(getenv("FPF_FUSED_AGG")) != 0;
-    const bool fuses_agg = (f->info.kernel == FPF_KERNEL_TILED && f->rtc) || f->info.kernel == FPF_KERNEL_WAVE;
+    const bool fuses_agg = (kern == FPF_KERNEL_TILED && f->rtc) || kern == FPF_KERNEL_WAVE;
     if (d_agg && fused_agg && fuses_agg) {
         // the specialised and wave kernels reduce the batch aggregate in their last workgroup
-        const int per = f->info.kernel == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : f->dev.tile;
+        const int per = kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : f->dev.tile;
         const size_t tiles = ((size_t)n_scen + per - 1) / per;
         if (tiles > f->partials_cap) {
             (void)hipFree(f->d_partials);
@@ -1313,10 +1370,11 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         o.partials = f->d_partials;
         o.ticket = f->d_ticket;
         agg_done = true;
+        HIPCHK(ctx, agg_before(f, st));
     }
-    if (f->info.kernel == FPF_KERNEL_WAVE) {
+    if (kern == FPF_KERNEL_WAVE) {
         e = launch_wave(f->wdev, n_scen, d_pq, o, st);
-    } else if (f->info.kernel == FPF_KERNEL_TILED) {
+    } else if (kern == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {
             std::string err;
             if (rtc_build(ctx->device, f->rtc_spec, &f->rtc_kernel_ib, &err) != 0)
@@ -1333,6 +1391,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         e = launch_generic(f->dev, n_scen, d_pq, f->d_scratch, f->scratch_ld, o, st);
     }
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("solve launch: ") + hipGetErrorString(e));
+    if (agg_done) HIPCHK(ctx, agg_after(f, st));
     if (d_agg && !agg_done) {
         e = launch_aggregate(n_scen, o.status, o.loss, o.vmin, o.vmax, f->dev.lb_v, f->dev.ub_v, d_agg, nullptr,
                              nullptr, st);
@@ -1355,9 +1414,11 @@ extern "C" int fpf_aggregate_device(fpf_feeder *f, int n_scen, const signed char
         HIPCHK(ctx, hipMalloc(&f->d_partials, 256 * 8 * sizeof(double)));
         f->partials_cap = 256;
     }
+    HIPCHK(ctx, agg_before(f, st));
     hipError_t e = launch_aggregate(n_scen, (const int8_t *)d_status, d_loss, d_vmin, d_vmax, f->dev.lb_v, f->dev.ub_v,
                                     d_agg, f->d_partials, f->d_ticket, st);
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("aggregate launch: ") + hipGetErrorString(e));
+    HIPCHK(ctx, agg_after(f, st));
     return FPF_OK;
 }
 

@@ -211,6 +211,7 @@ struct RtcKernel {
 };
 std::string rtc_source(const RtcSpec &spec);
 int rtc_build(int device, const RtcSpec &spec, RtcKernel *out, std::string *err);
+void rtc_release(const RtcKernel &k);   // drop one reference; the last unloads the code object
 hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
                       hipStream_t st);
 #endif

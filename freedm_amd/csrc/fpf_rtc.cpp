@@ -37,7 +37,13 @@ extern "C" int fpf_debug_set_rtc_stamp_buffer(void *dptr) {
 
 namespace {
 std::mutex g_mu;
-std::map<std::pair<int, std::string>, RtcKernel> g_cache;
+// one code object per (device, source), shared by the feeders that compile the
+// same topology; unloaded when the last of them is destroyed (rtc_release)
+struct RtcEntry {
+    RtcKernel k;
+    int refs;
+};
+std::map<std::pair<int, std::string>, RtcEntry> g_cache;
 
 // The sequential stages as one straight-line instruction stream that runs the
 // feeder's multi-track schedule (fpf_internal.h: TrackSched): at step s every
@@ -237,7 +243,8 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
     auto key = std::make_pair(device, src);
     auto it = g_cache.find(key);
     if (it != g_cache.end()) {
-        *out = it->second;
+        ++it->second.refs;
+        *out = it->second.k;
         return 0;
     }
     hiprtcProgram prog;
@@ -267,17 +274,34 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
     hiprtcGetCode(prog, &code[0]);
     hiprtcDestroyProgram(&prog);
     RtcKernel k{};
-    if (hipModuleLoadData(&k.mod, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&k.fn, k.mod, "fpf_rtc_tiled") != hipSuccess) {
-        *err = "hipModuleLoadData / hipModuleGetFunction failed";
+    if (hipModuleLoadData(&k.mod, code.data()) != hipSuccess) {
+        *err = "hipModuleLoadData failed";
+        return -1;
+    }
+    if (hipModuleGetFunction(&k.fn, k.mod, "fpf_rtc_tiled") != hipSuccess) {
+        (void)hipModuleUnload(k.mod);
+        *err = "hipModuleGetFunction failed";
         return -1;
     }
     k.nt = sp.nt;
     // dynamic LDS above the default 64 KiB (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    g_cache[key] = k;
+    g_cache[key] = RtcEntry{k, 1};
     *out = k;
     return 0;
+}
+
+void rtc_release(const RtcKernel &k) {
+    if (!k.mod) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto it = g_cache.begin(); it != g_cache.end(); ++it)
+        if (it->second.k.mod == k.mod) {
+            if (--it->second.refs == 0) {
+                (void)hipModuleUnload(it->second.k.mod);
+                g_cache.erase(it);
+            }
+            return;
+        }
 }
 
 hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const double *pq, const OutDev &o,

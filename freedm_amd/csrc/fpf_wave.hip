@@ -37,7 +37,10 @@
 // double (a solve that diverges past 1e+-150 p.u. gets non-finite values; its
 // status is NONCONVERGED either way).
 #include <algorithm>
+#include <array>
 #include <cstdio>
+#include <mutex>
+#include <set>
 #include <cstdlib>
 #include <type_traits>
 
@@ -745,15 +748,24 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, w.half); id = 5; }
     else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, w.half); id = 6; }
     if (!k) return hipErrorInvalidValue;
-    static bool attr[7][2][2] = {};
-    if (!attr[id][full][w.half]) {   // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the static part)
-        hipFuncAttributes fa{};
-        hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024 - (int)fa.sharedSizeBytes);
-        if (e != hipSuccess) return e;
-        attr[id][full][w.half] = true;
+    // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the
+    // static part) -- a per-device setting, done once per (device, variant)
+    static std::mutex mu;
+    static std::set<std::array<int, 4>> attr_done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        const std::array<int, 4> key = {dev, id, (int)full, w.half};
+        if (!attr_done.count(key)) {
+            hipFuncAttributes fa{};
+            hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - (int)fa.sharedSizeBytes);
+            if (e != hipSuccess) return e;
+            attr_done.insert(key);
+        }
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(wave_wpb(w) * 64), lds, st, w, n_scen, pq, o);
     const hipError_t e = hipGetLastError();

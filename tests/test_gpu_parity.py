@@ -70,12 +70,14 @@ def test_matches_golden(name, kernel, spec, exact):
     if exact:
         assert _vrel(r["V_re"], r["V_im"], g["V_re"], g["V_im"]) <= 1e-10
     else:
-        _close(r["PQb"][:, :, :4][..., conv[:4]], g["PQb"][..., conv[:4]], 1e-9)
-        _close(r["PQL"][:, :, :4][..., conv[:4]], g["PQL"][..., conv[:4]], 1e-9)
         _close(r["loss"][conv], g["loss"][conv], 1e-8)
-        _close(r["Vpolar"][0::2, :, :4][..., conv[:4]], g["Vpolar"][0::2][..., conv[:4]], 1e-10)
         np.testing.assert_allclose(r["vmin"][conv], g["vmin"][conv], rtol=1e-10)
         np.testing.assert_allclose(r["vmax"][conv], g["vmax"][conv], rtol=1e-10)
+        # whole batches (the fixtures keep 4 scenarios of the matrix outputs): the
+        # oracle recomputes Vpolar / PQb / PQL for every converged scenario
+        from oracle import oracle as O
+        c = O.dpf_batch(g["Dl"], g["Z"], g["pq"], nthreads=8)
+        _fast_mode_outputs_match(r, c, conv)
         return
     # the stronger claim: same operations, same order -> same bits
     np.testing.assert_array_equal(r["V_re"], g["V_re"])
@@ -88,6 +90,71 @@ def test_matches_golden(name, kernel, spec, exact):
     np.testing.assert_allclose(r["Vpolar"][1::2, :, :4], g["Vpolar"][1::2], rtol=0, atol=1e-12)
     np.testing.assert_allclose(r["vmin"], g["vmin"], rtol=1e-14)
     np.testing.assert_allclose(r["vmax"], g["vmax"], rtol=1e-14)
+
+
+def _fast_mode_outputs_match(r, c, conv):
+    """Fast-mode matrix outputs against the oracle on the converged scenarios:
+    PQb / PQL within 1e-9 of each field's scale, |V| within 1e-10 relative, and
+    the angles (DPF_return7.cpp:231-235, atan of imag/real in degrees) within
+    1e-8 deg -- V is within 1e-10 relative, so an angle moves by at most ~6e-9
+    deg; a zeroed phase must read exactly the reference's -180 / +180 pattern."""
+    _close(r["PQb"][..., conv], c["PQb"][..., conv], 1e-9)
+    _close(r["PQL"][..., conv], c["PQL"][..., conv], 1e-9)
+    mag_r, mag_c = r["Vpolar"][0::2][..., conv], c["Vpolar"][0::2][..., conv]
+    np.testing.assert_allclose(mag_r, mag_c, rtol=1e-10, atol=0)
+    ang_r, ang_c = r["Vpolar"][1::2][..., conv], c["Vpolar"][1::2][..., conv]
+    np.testing.assert_allclose(ang_r, ang_c, rtol=0, atol=1e-8)
+    zero = mag_c == 0
+    np.testing.assert_array_equal(mag_r[zero], 0.0)
+    np.testing.assert_array_equal(ang_r[zero], ang_c[zero])
+
+
+def test_wave_divergent_convergence_in_one_wavefront():
+    """Scenarios sharing a wavefront converge at different sweeps (loads scaled
+    0.05x .. 3x, interleaved): each keeps the state of its own last sweep while
+    the wave sweeps on (DPF_return7.cpp:199-217 break), so iteration counts,
+    V and the matrix outputs match the oracle scenario by scenario."""
+    from oracle import oracle as O
+    f = F.synthetic_feeder(123, 123)
+    pq = F.scenario_loads(f, np.arange(256))
+    scale = np.tile(np.array([0.05, 3.0, 0.4, 2.2, 1.0, 0.15, 2.8, 0.7]), 32)
+    pq = np.ascontiguousarray(pq * scale[None, None, :])
+    pf = _pf(f.Dl, f.Z, kernel="wave")
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert len(np.unique(c["iters"])) >= 3, np.unique(c["iters"])
+    assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+    conv = c["status"] == 0
+    assert _vrel(r["V_re"][..., conv], r["V_im"][..., conv], c["V_re"][..., conv], c["V_im"][..., conv]) <= 1e-10
+    _fast_mode_outputs_match(r, c, conv)
+    _close(r["loss"][conv], c["loss"][conv], 1e-8)
+
+
+def test_aggregates_on_two_streams():
+    """Two aggregating solves of one feeder in flight on two streams (they share
+    the feeder's partials / ticket scratch, which the library orders): both
+    aggregates are right."""
+    import torch
+    f = F.synthetic_feeder(123, 123)
+    pf = _pf(f.Dl, f.Z)
+    dev = torch.device("cuda:0")
+    B = 8192
+    pqs = [F.scenario_loads(f, np.arange(i * B, (i + 1) * B)) for i in range(2)]
+    host = [pf.solve(p)["aggregate"] for p in pqs]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    d_pq = [torch.from_numpy(p).to(dev) for p in pqs]
+    aggs = [torch.zeros(8, dtype=torch.float64, device=dev) for _ in range(2)]
+    outs = [{"loss": torch.zeros(B, dtype=torch.float64, device=dev)} for _ in range(2)]
+    torch.cuda.synchronize()
+    for rep in range(20):
+        for i in (0, 1):
+            pf.solve_device(d_pq[i], outs[i], agg=aggs[i], stream=streams[i])
+        torch.cuda.synchronize()
+        for i in (0, 1):
+            a = aggs[i].cpu().numpy()
+            h = host[i]
+            assert a[3] == h["n_conv"] and a[7] == h["n_scen"] and a[1] == h["vmin"] and a[2] == h["vmax"], (rep, i)
+            assert a[0] == pytest.approx(h["loss_sum"], rel=1e-12)
 
 
 def test_auto_kernel_choice():
@@ -148,13 +215,17 @@ def test_dpf_return7_dropin():
     from freedm_amd import DPF_return7, NonConvergedError
     from oracle import oracle as O
     f = F.demo_feeder()
-    vpq = DPF_return7(f.Dl, f.Z)
+    vpq = DPF_return7(f.Dl, f.Z)          # default: exact mode, the reference's roundings
     c = O.dpf_solve(f.Dl, f.Z)
     assert vpq.iters == c["iters"] == 5
-    _close(vpq.PQb, c["PQb"], 1e-9)
-    _close(vpq.PQL, c["PQL"], 1e-9)
-    np.testing.assert_allclose(vpq.Vpolar, c["Vpolar"], rtol=1e-10, atol=1e-9)
+    np.testing.assert_array_equal(vpq.PQb, c["PQb"])
+    np.testing.assert_array_equal(vpq.PQL, c["PQL"])
+    np.testing.assert_allclose(vpq.Vpolar, c["Vpolar"], rtol=1e-14, atol=1e-12)
     np.testing.assert_array_equal(vpq.Qset_b[:, 0], f.Dl[:, 9])
+    fast = DPF_return7(f.Dl, f.Z, exact=False)
+    assert fast.iters == 5
+    _close(fast.PQb, c["PQb"], 1e-9)
+    np.testing.assert_allclose(fast.Vpolar, c["Vpolar"], rtol=1e-10, atol=1e-8)
     g = load_golden("g5_nonconv")
     Dl = g["Dl"].copy()
     with pytest.raises(NonConvergedError):
