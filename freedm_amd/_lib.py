@@ -21,7 +21,7 @@ KERNELS = {"auto": FPF_KERNEL_AUTO, "generic": FPF_KERNEL_GENERIC, "tiled": FPF_
 EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_destroy", "fpf_last_error",
            "fpf_feeder_create", "fpf_feeder_destroy", "fpf_feeder_get_info", "fpf_feeder_reserve",
            "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source",
-           "fpf_selftest_division", "fpf_vvc_line_search"]
+           "fpf_selftest_division", "fpf_vvc_line_search", "fpf_feeder_wave_plan"]
 
 
 class FpfOpts(C.Structure):
@@ -112,6 +112,10 @@ def load(path: str | None = None):
     L.fpf_vvc_line_search.argtypes = [vp, _dp, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int), C.c_int, C.c_double,
                                       C.c_double, C.c_int, C.c_double, C.POINTER(FpfLineSearch)]
     L.fpf_vvc_line_search.restype = C.c_int
+    if hasattr(L, "fpf_feeder_wave_plan") or path == LIB_PATH:   # (older diagnostic builds lack it)
+        L.fpf_feeder_wave_plan.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
+                                           C.POINTER(C.c_int)]
+        L.fpf_feeder_wave_plan.restype = C.c_int
     L.fpf_selftest_division.argtypes = [C.c_int, C.c_long, C.c_ulong]
     L.fpf_selftest_division.restype = C.c_long
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",

@@ -63,9 +63,10 @@ struct fpf_feeder {
     RtcKernel rtc_kernel_ib{};   // with PQb: built on the first solve that asks for it
     bool rtc_ib = false;
     RtcSpec rtc_spec;
-    // wave kernel (fast mode)
+    // wave kernel (fast mode); wdev_big: the same tables launched with the
+    // waves per workgroup of large batches
     void *d_wave = nullptr;
-    WaveDev wdev{};
+    WaveDev wdev{}, wdev_big{};
     // the partials + ticket scratch is shared by every aggregating launch on
     // this feeder (fused wave/specialised aggregate, fpf_aggregate_device): a
     // launch on another stream than the previous one first waits for it
@@ -374,12 +375,14 @@ void analyse_tiled(HostFeeder &h) {
 // Ib the backward sweep hands up a block (DPF_return7.cpp:147-157) flows to the
 // node's forward source (:176-178) -- the sweep then computes subtree sums.
 constexpr size_t WAVE_LDS_BUDGET = 159 * 1024;   // 160 KiB per CU minus the kernel's static LDS
+constexpr int WAVE_SMALL_WPB_MIN_SCEN = 16384;    // batches from here on use WaveHost::wpb_big_batch
 
 struct WaveHost {
     bool ok = false;
     std::string why;
-    int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0, half = 0;
-    std::vector<int32_t> row, node, info, mref, pairs;
+    int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0, wpb = 0, off_in_x = 0;
+    int wpb_big_batch = 0;
+    std::vector<int32_t> row, node, info, blk, mref, pairs;
     std::vector<double> temp;
 };
 
@@ -443,61 +446,69 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
                 }
         }
     }
-    // positions whose scan values other slots gather: subtree ends (backward),
-    // taps and the positions before lateral blocks (forward), zeroed ancestors
-    std::vector<int> comp(n, -1);
-    int ncomp = 0;
-    auto need = [&](int q) { if (comp[q] < 0) comp[q] = ncomp++; };
-    for (int q = 0; q < n; ++q) need(q + size[at[q]] - 1);
+    // positions whose scan values other slots gather, in two index spaces that
+    // share one LDS array X (the backward values are dead before the forward
+    // ones are stored): backward = subtree ends; forward = taps, the positions
+    // before lateral blocks, zeroed ancestors
+    std::vector<int> cb(n, -1), cf(n, -1);
+    int nb_c = 0, nf_c = 0;
+    for (int q = 0; q < n; ++q) {
+        const int e = q + size[at[q]] - 1;
+        if (cb[e] < 0) cb[e] = nb_c++;
+    }
+    auto needf = [&](int q) { if (cf[q] < 0) cf[q] = nf_c++; };
     for (int b = 1; b < nblk; ++b) {
-        need(pos[par[bfirst[b]]]);
-        need(pos[bfirst[b]] - 1);
+        needf(pos[par[bfirst[b]]]);
+        needf(pos[bfirst[b]] - 1);
     }
     for (int k = 1; k < nn; ++k)
         for (int p = 0; p < 3; ++p)
-            if (mref[k][p] >= 1) need(pos[mref[k][p]]);
-    // bank-aware numbering: the entries one 16-lane group of a gather reads
-    // (ds_read_b128 serves four such groups, MI355X_MICROARCH.md LDS) get
-    // distinct 16-byte units mod 16 where a coloring allows
-    {
-        static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
-                                       {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
-                                       {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
-                                       {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+            if (mref[k][p] >= 1) needf(pos[mref[k][p]]);
+    int maxd = 0;
+    for (int b = 1; b < nblk; ++b) {
+        int d = 0;
+        for (int j = b; j != 0; j = blk[par[bfirst[j]]]) ++d;
+        maxd = std::max(maxd, d);
+    }
+    // bank-aware numbering of one space: the entries one 16-lane group of a
+    // gather reads (ds_read_b128 serves four such groups, MI355X_MICROARCH.md
+    // LDS) get distinct 16-byte units mod 16 where a coloring allows
+    static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                   {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                   {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                   {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+    auto color_space = [&](std::vector<int> &comp, int &ncomp, bool backward) {
         std::vector<std::vector<char>> adj(ncomp, std::vector<char>(ncomp, 0));
         auto clique = [&](const std::vector<int> &v) {
             for (size_t a = 0; a < v.size(); ++a)
                 for (size_t b = a + 1; b < v.size(); ++b)
                     if (v[a] != v[b]) adj[v[a]][v[b]] = adj[v[b]][v[a]] = 1;
         };
-        for (const auto &g : grp)
-            for (int c = 0; c < C; ++c) {
-                std::vector<int> v;
-                for (int ln : g) {
-                    const int q = (ln % L) * C + c;
-                    if (q < n) v.push_back(comp[q + size[at[q]] - 1]);
-                }
-                clique(v);
-            }
-        int maxd = 0;
-        for (int b = 1; b < nblk; ++b) {
-            int d = 0;
-            for (int j = b; j != 0; j = blk[par[bfirst[j]]]) ++d;
-            maxd = std::max(maxd, d);
-        }
-        for (const auto &g : grp)
-            for (int jd = 0; jd < maxd; ++jd)
-                for (int side = 0; side < 2; ++side) {
+        if (backward) {
+            for (const auto &g : grp)
+                for (int c = 0; c < C; ++c) {
                     std::vector<int> v;
                     for (int ln : g) {
-                        int b = ln % L, j = b, d = 0;
-                        if (b == 0 || b >= nblk) continue;
-                        for (; j != 0 && d < jd; j = blk[par[bfirst[j]]]) ++d;
-                        if (j == 0) continue;
-                        v.push_back(side ? comp[pos[bfirst[j]] - 1] : comp[pos[par[bfirst[j]]]]);
+                        const int q = (ln % L) * C + c;
+                        if (q < n) v.push_back(comp[q + size[at[q]] - 1]);
                     }
                     clique(v);
                 }
+        } else {
+            for (const auto &g : grp)
+                for (int jd = 0; jd < maxd; ++jd)
+                    for (int side = 0; side < 2; ++side) {
+                        std::vector<int> v;
+                        for (int ln : g) {
+                            int b = ln % L, j = b, d = 0;
+                            if (b == 0 || b >= nblk) continue;
+                            for (; j != 0 && d < jd; j = blk[par[bfirst[j]]]) ++d;
+                            if (j == 0) continue;
+                            v.push_back(side ? comp[pos[bfirst[j]] - 1] : comp[pos[par[bfirst[j]]]]);
+                        }
+                        clique(v);
+                    }
+        }
         std::vector<int> order(ncomp), color(ncomp, -1), deg(ncomp, 0);
         for (int a = 0; a < ncomp; ++a) {
             order[a] = a;
@@ -518,20 +529,25 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
             renum[a] = best + 16 * used[best]++;
         }
         int top = 0;
+        for (int a = 0; a < ncomp; ++a) top = std::max(top, renum[a] + 1);
+        if (top > ncomp + 8) return;   // the holes would cost more LDS than the conflicts: keep the dense numbering
         for (int q = 0; q < n; ++q)
-            if (comp[q] >= 0) {
-                comp[q] = renum[comp[q]];
-                top = std::max(top, comp[q] + 1);
-            }
-        ncomp = top;   // holes allowed; entry ncomp is the zero
-    }
+            if (comp[q] >= 0) comp[q] = renum[comp[q]];
+        ncomp = top;   // holes allowed
+    };
+    color_space(cb, nb_c, true);
+    color_space(cf, nf_c, false);
+    // entry ncomp of X is the permanent zero; in the common case the block
+    // offsets are stored over X's first nblk entries (off_in_x, fpf_wave.hip)
+    const bool off_in_x = nblk <= L && maxd <= 4;   // = the kernel's register-resolved path (WAVE_BD)
+    const int ncomp = std::max(std::max(nb_c, nf_c), off_in_x ? nblk : 0);
     if (ncomp > 510) return no("too many gathered positions");
     // off(b) = sum over b's block-ancestor chain of Ginc[tap] - Ginc[first - 1]
     std::vector<std::vector<std::pair<int, int>>> chainp(nblk);
     int bdepth = 0;
     for (int b = 1; b < nblk; ++b) {
         for (int j = b; j != 0; j = blk[par[bfirst[j]]])
-            chainp[b].push_back({comp[pos[par[bfirst[j]]]], comp[pos[bfirst[j]] - 1]});
+            chainp[b].push_back({cf[pos[par[bfirst[j]]]], cf[pos[bfirst[j]] - 1]});
         bdepth = std::max(bdepth, (int)chainp[b].size());
     }
     w.pairs.assign((size_t)std::max(bdepth, 1) * 2 * nblk, ncomp);
@@ -543,7 +559,8 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     const size_t S = (size_t)C * L;
     w.row.assign(S, -1);
     w.node.assign(S, -1);
-    w.info.assign(S, (ncomp << 13));   // empty slot: gathers the zero entry, block 0
+    w.info.assign(S, (ncomp << 13));   // empty slot: gathers the zero entry, stores nothing
+    w.blk.assign(S, 0);                // empty slot: block 0
     w.mref.assign(3 * S, -1);
     w.temp.assign(9 * S * 2, 0.0);
     for (int q = 0; q < n; ++q) {
@@ -551,9 +568,10 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
         const NodeOp &nd = h.node[k];
         w.row[i] = nd.row;
         w.node[i] = k;
-        w.info[i] = (nd.mask & 7) | 8 | ((comp[q] + 1) << 4) | (comp[q + size[k] - 1] << 13) | (blk[k] << 22);
+        w.info[i] = (nd.mask & 7) | 8 | ((cb[q] + 1) << 4) | (cb[q + size[k] - 1] << 13) | ((cf[q] + 1) << 22);
+        w.blk[i] = blk[k];
         for (int p = 0; p < 3; ++p)
-            if (mref[k][p] >= 1) w.mref[(p * C + c) * L + lane] = comp[pos[mref[k][p]]];
+            if (mref[k][p] >= 1) w.mref[(p * C + c) * L + lane] = cf[pos[mref[k][p]]];
         for (int j = 0; j < 9; ++j) {
             w.temp[((j * C + c) * L + lane) * 2 + 0] = h.tz[(size_t)nd.fw * 18 + 2 * j];
             w.temp[((j * C + c) * L + lane) * 2 + 1] = h.tz[(size_t)nd.fw * 18 + 2 * j + 1];
@@ -567,7 +585,11 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     w.ncomp = ncomp;
     w.has_rel = has_rel;
     w.has_mask = has_mask;
-    // LDS: the full workgroup, else half of it (static LDS ~1 KB aside)
+    w.off_in_x = off_in_x ? 1 : 0;
+    // waves per workgroup: the smaller workgroup when two of them fit in a CU's
+    // LDS (each then stages its loads and writes its V while the other sweeps;
+    // the registers allow 2 waves per SIMD = 8 per CU for these geometries),
+    // else the larger one if it fits, else the smaller one alone
     WaveDev probe{};
     probe.spw = spw;
     probe.C = C;
@@ -575,12 +597,24 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     probe.nblk = nblk;
     probe.bdepth = bdepth;
     probe.ncomp = ncomp;
-    w.half = 0;
-    if (wave_lds_bytes(probe) > WAVE_LDS_BUDGET) {
-        probe.half = 1;
-        if (wave_lds_bytes(probe) > WAVE_LDS_BUDGET) return no("per-scenario LDS above the budget");
-        w.half = 1;
+    probe.off_in_x = w.off_in_x;
+    const int big = spw * C <= 2 ? 16 : 8, small = big / 2;
+    auto lds_at = [&](int wpb) { probe.wpb = wpb; return wave_lds_bytes(probe); };
+    // Measured (profiles/r02a, 123-bus): two 8-scenario workgroups per CU are
+    // 11 % faster on a 131 072-scenario batch (config 4), one 16-scenario
+    // workgroup 6 % faster on a 4 096 batch (config 2, one workgroup per CU:
+    // nothing to overlap) -- so wpb_big_batch is used from WAVE_SMALL_WPB_MIN_SCEN.
+    int wpb = 0, wpb_big_batch = 0;
+    if (lds_at(big) <= WAVE_LDS_BUDGET) wpb = big;
+    else if (lds_at(small) <= WAVE_LDS_BUDGET) wpb = small;
+    else return no("per-scenario LDS above the budget");
+    wpb_big_batch = (spw * C > 2 && 2 * (lds_at(small) + 1024) <= 160 * 1024) ? small : wpb;
+    if (const char *e = getenv("FPF_WAVE_WPB")) {   // experiments
+        const int x = atoi(e);
+        if (wave_wpb_supported(spw, C, x) && lds_at(x) <= WAVE_LDS_BUDGET) wpb = wpb_big_batch = x;
     }
+    w.wpb = wpb;
+    w.wpb_big_batch = wpb_big_batch;
     w.ok = true;
 }
 
@@ -1146,6 +1180,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         WaveDev &w = f->wdev;
         std::vector<char> wb;
         const size_t o_row = push_blob(wb, wh.row), o_node = push_blob(wb, wh.node), o_info = push_blob(wb, wh.info);
+        const size_t o_blk = push_blob(wb, wh.blk);
         const size_t o_mref = push_blob(wb, wh.mref);
         const size_t o_tmp = push_blob(wb, wh.temp), o_pairs = push_blob(wb, wh.pairs);
         e = hipMalloc(&f->d_wave, wb.size());
@@ -1165,7 +1200,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.ncomp = wh.ncomp;
         w.has_rel = wh.has_rel;
         w.has_mask = wh.has_mask;
-        w.half = wh.half;
+        w.wpb = wh.wpb;
+        w.off_in_x = wh.off_in_x;
         w.dbg = getenv("FPF_WAVE_DBG") ? atoi(getenv("FPF_WAVE_DBG")) : 0;
         w.mxitr = o.mxitr;
         for (int p = 0; p < 3; ++p) w.K[p] = d.K[p];
@@ -1177,6 +1213,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.slot_row = (const int32_t *)(wbase + o_row);
         w.slot_node = (const int32_t *)(wbase + o_node);
         w.slot_info = (const int32_t *)(wbase + o_info);
+        w.slot_blk = (const int32_t *)(wbase + o_blk);
         w.slot_mref = (const int32_t *)(wbase + o_mref);
         w.slot_temp = (const double *)(wbase + o_tmp);
         w.blk_pairs = (const int32_t *)(wbase + o_pairs);
@@ -1184,6 +1221,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             fpf_feeder_destroy(f);
             return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
         }
+        f->wdev_big = w;
+        f->wdev_big.wpb = wh.wpb_big_batch;
     }
     // auto: the interpreted tiled kernel only pays with several scenarios per
     // workgroup; below that (large feeders, e.g. 2048-bus at tile 1: 794 ms vs
@@ -1261,6 +1300,11 @@ static hipError_t agg_before(fpf_feeder *f, hipStream_t st) {
     if (f->agg_pending && f->agg_stream != st) return hipStreamWaitEvent(st, f->agg_event, 0);
     return hipSuccess;
 }
+// the wave kernel's launch geometry for a batch of n_scen scenarios
+static const WaveDev &wave_dev_for(const fpf_feeder *f, int n_scen) {
+    return n_scen >= WAVE_SMALL_WPB_MIN_SCEN ? f->wdev_big : f->wdev;
+}
+
 // the kernel a batch of n_scen scenarios runs on
 static int kernel_for(const fpf_feeder *f, int n_scen) {
     if (f->auto_batch) return n_scen >= AUTO_GENERIC_MIN_SCEN ? FPF_KERNEL_GENERIC : FPF_KERNEL_TILED;
@@ -1357,7 +1401,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     const bool fuses_agg = (kern == FPF_KERNEL_TILED && f->rtc) || kern == FPF_KERNEL_WAVE;
     if (d_agg && fused_agg && fuses_agg) {
         // the specialised and wave kernels reduce the batch aggregate in their last workgroup
-        const int per = kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(f->wdev) : f->dev.tile;
+        const int per = kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(wave_dev_for(f, n_scen)) : f->dev.tile;
         const size_t tiles = ((size_t)n_scen + per - 1) / per;
         if (tiles > f->partials_cap) {
             (void)hipFree(f->d_partials);
@@ -1373,7 +1417,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         HIPCHK(ctx, agg_before(f, st));
     }
     if (kern == FPF_KERNEL_WAVE) {
-        e = launch_wave(f->wdev, n_scen, d_pq, o, st);
+        e = launch_wave(wave_dev_for(f, n_scen), n_scen, d_pq, o, st);
     } else if (kern == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {
             std::string err;
@@ -1507,4 +1551,34 @@ extern "C" long fpf_feeder_rtc_source(const double *dl, int nl, int ncols, const
         buf[n] = 0;
     }
     return (long)src.size() + 1;
+}
+
+extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+                                    const fpf_opts *opts, int out[8]) {
+    if (!dl || !out || nl < 1 || ncols < 12 || z_rows < 0 || (z_rows > 0 && !z)) return FPF_ERR_ARG;
+    fpf_opts o;
+    if (opts) o = *opts;
+    else fpf_opts_default(&o);
+    HostFeeder h;
+    h.nl = nl;
+    h.ncols = ncols;
+    h.dl.assign(dl, dl + (size_t)nl * ncols);
+    std::string why = build_ops(h, z, z_rows, z_cols, o);
+    if (why.empty()) why = build_lnum(h, z, z_rows, o);
+    if (!why.empty()) return FPF_ERR_TOPOLOGY;
+    analyse_tiled(h);
+    WaveHost wh;
+    analyse_wave(h, wh);
+    WaveDev w{};
+    w.spw = wh.spw;
+    w.C = wh.C;
+    w.nl = nl;
+    w.nblk = wh.nblk;
+    w.bdepth = wh.bdepth;
+    w.ncomp = wh.ncomp;
+    w.wpb = wh.wpb;
+    w.off_in_x = wh.off_in_x;
+    const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, wh.ok ? (int)wave_lds_bytes(w) : 0, wh.ncomp, wh.nblk, wh.bdepth};
+    std::memcpy(out, v, sizeof(v));
+    return FPF_OK;
 }

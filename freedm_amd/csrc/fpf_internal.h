@@ -125,15 +125,19 @@ struct WaveDev {
     int32_t mxitr;
     int32_t K[3];            // Lnum_p + 1 (V_abc_list.cpp:12-17)
     int32_t dbg;             // diagnostic ablations (FPF_WAVE_DBG; results are wrong when set)
-    int32_t half;            // 1: half the wavefronts per workgroup (LDS-heavy feeders)
+    int32_t wpb;             // wavefronts per workgroup (16, 8 or 4; fpf_api.cpp: analyse_wave)
+    int32_t off_in_x;        // 1: block offsets stored over X's first nblk entries (nblk <= L, depth <= 4)
     double V0[6], s3, eps, lb_v, ub_v;
     const int32_t *slot_row;    // [C][L] Dl row of the slot's node (-1: empty slot)
     const int32_t *slot_node;   // [C][L] node id
-    const int32_t *slot_info;   // [C][L] bits 0-2 zero mask, 3 valid, 4-12 compact index + 1,
-                                //        13-21 compact index of the subtree's last node, 22-30 block
-    const int32_t *slot_mref;   // [3][C][L] compact index of the nearest zeroed proper ancestor, -1 none
-    const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch
-    const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) compact indices; pad = ncomp (zero)
+    const int32_t *slot_info;   // [C][L] bits 0-2 zero mask, 3 valid, 4-12 backward index + 1 (the
+                                //        slot's store), 13-21 backward index of the subtree's last
+                                //        node (its gather), 22-30 forward index + 1 (its store)
+    const int32_t *slot_blk;    // [C][L] block of the slot's node
+    const int32_t *slot_mref;   // [3][C][L] forward index of the nearest zeroed proper ancestor, -1 none
+    const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch (read
+                                // from global memory: L1/L2-resident, 18 KB for 128 slots)
+    const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) forward indices; pad = ncomp (zero)
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -161,6 +165,7 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
 size_t wave_lds_bytes(const WaveDev &w);
 bool wave_geometry(int n, int *spw, int *c);
 int wave_scenarios_per_block(const WaveDev &w);
+bool wave_wpb_supported(int spw, int c, int wpb);
 size_t tiled_lds_bytes(const FeederDev &f, int tile);
 size_t tiled_lds_bytes_rtc(const FeederDev &f, int tile);
 int tiled_max_tile(const FeederDev &f);

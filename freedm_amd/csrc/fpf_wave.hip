@@ -51,7 +51,9 @@ namespace fpf {
 
 // diagnostic ablation build (make ablate): FPF_WAVE_DBG bits switch pieces off;
 // results are wrong when set.  Compiled out of the product.
-#ifdef FPF_WAVE_ABLATE
+#if defined(FPF_WAVE_ABL)
+#define DBG(bit) (FPF_WAVE_ABL & (bit))   // compile-time ablation (tools/build_ablations.sh)
+#elif defined(FPF_WAVE_ABLATE)
 #define DBG(bit) (f.dbg & (bit))
 #else
 #define DBG(bit) 0
@@ -194,20 +196,26 @@ __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn,
 // packed per-slot info (fpf_api.cpp: analyse_wave)
 __device__ __forceinline__ int si_mask(int x) { return x & 7; }
 __device__ __forceinline__ bool si_valid(int x) { return (x >> 3) & 1; }
-__device__ __forceinline__ int si_comp(int x) { return ((x >> 4) & 511) - 1; }   // -1: not gathered
+__device__ __forceinline__ int si_store_b(int x) { return ((x >> 4) & 511) - 1; }   // -1: not gathered
 __device__ __forceinline__ int si_last(int x) { return (x >> 13) & 511; }
-__device__ __forceinline__ int si_blk(int x) { return (x >> 22) & 511; }
+__device__ __forceinline__ int si_store_f(int x) { return ((x >> 22) & 511) - 1; }  // -1: not gathered
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
 
-template <int SPW, int C, bool HALF = false>
+template <int SPW, int C>
 struct WaveGeom {
     static constexpr int L = 64 / SPW;                 // lanes per scenario
-    // wavefronts per workgroup (halved for feeders whose per-scenario LDS is large)
-    static constexpr int WPB = (SPW * C <= 2 ? 16 : 8) >> (HALF ? 1 : 0);
     static constexpr int MINW = SPW * C <= 2 ? 4 : 2;  // waves per SIMD the registers allow
-    static constexpr int SPB = WPB * SPW;              // scenarios per workgroup
 };
+
+// the TEMP blocks are staged in LDS once per workgroup (a diagnostic build
+// reads them from global memory instead: L1/L2-resident, but the compiler
+// hoists the loads and spills -- 39 % slower, variants_r02a)
+#ifdef FPF_WAVE_TEMP_GLOBAL
+constexpr bool TEMP_IN_LDS = false;
+#else
+constexpr bool TEMP_IN_LDS = true;
+#endif
 
 // segment-wide reductions by the DPP scan pattern; the segment's last lane holds
 // the result.  Lanes without a source keep +inf (bound_ctrl off, old = +inf).
@@ -231,10 +239,10 @@ __device__ __forceinline__ double seg_reduce_min(double x) {
 template <int L>
 __device__ __forceinline__ double seg_reduce_max(double x) { return -seg_reduce_min<L>(-x); }
 
-template <int SPW, int C, bool FULL, bool HALF>
-__global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, C, HALF>::MINW)) void dpf_wave_kernel(
+template <int SPW, int C, bool FULL, int WPB>
+__global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
-    constexpr int L = WaveGeom<SPW, C, HALF>::L, WPB = WaveGeom<SPW, C, HALF>::WPB, SPB = WaveGeom<SPW, C, HALF>::SPB;
+    constexpr int L = WaveGeom<SPW, C>::L, SPB = WPB * SPW;
     constexpr int NT = WPB * 64;
     extern __shared__ double2 lds[];
     if (DBG(4096)) return;
@@ -245,24 +253,31 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
     const int s0 = blockIdx.x * SPB, s = s0 + sc;
     const int nsb = min(SPB, B - s0);              // scenarios of this workgroup
     const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
-    // LDS: per workgroup the TEMP blocks and the block-chain table; per scenario
-    // Sld (later V in node order), the gathered scan values X ([3][XC], entry XC-1
-    // = 0) and the block offsets
-    double2 *const tl = lds;                                          // [9][C][L]
-    int *const pairs = (int *)(tl + 9 * C * L);                       // [bdepth][2][nblk]
+    // LDS: per workgroup the block-chain table (and, in a diagnostic build, the
+    // TEMP blocks); per scenario Sld (later V in node order), the gathered scan
+    // values X ([3][XC], entry XC-1 = 0; backward and forward entries share it)
+    // and the block offsets
+    double2 *const tl = lds;                                          // [9][C][L] if TEMP_IN_LDS
+    int *const pairs = (int *)(tl + (TEMP_IN_LDS ? 9 * C * L : 0));   // [bdepth][2][nblk]
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
     int *const knode = pairs + pair_n;                                // [C][L] node of each slot
     double2 *const reg0 = (double2 *)(knode + C * L);                 // per-scenario regions
-    const int RS = (3 * C * L + 3 * XC + 3 * nblk) | 1;              // double2 per region (odd: V read-out banks)
+    const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
+    const int RS = (3 * C * L + 3 * XC + noff) | 1;                  // double2 per region (odd: V read-out banks)
     double2 *const SL = reg0 + sc * RS;
     double2 *const X = SL + 3 * C * L;
-    double2 *const OFF = X + 3 * XC;
+    // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
+    // pair read of the scenario precedes the offset stores in its one wave's
+    // program order), else after X
+    double2 *const OFF = f.off_in_x ? X : X + 3 * XC;
+    const int OS = f.off_in_x ? XC : nblk;
     const bool live = sc < nsb;
-    int si[C], row[C];
+    int si[C], row[C], bk[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         row[c] = f.slot_row[c * L + li];
         si[c] = f.slot_info[c * L + li];
+        bk[c] = f.slot_blk[c * L + li];
     }
 
     // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced (16 scenarios = one
@@ -289,21 +304,23 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             }
         }
         // the feeder tables: all loads in flight before the LDS stores
-        constexpr int UT = (9 * C * L + NT - 1) / NT;
-        double2 t[UT];
+        if (TEMP_IN_LDS) {
+            constexpr int UT = (9 * C * L + NT - 1) / NT;
+            double2 t[UT];
 #pragma unroll
-        for (int u = 0; u < UT; ++u) {
-            const int i = u * NT + (int)threadIdx.x;
-            t[u] = ld_global2(f.slot_temp, i < 9 * C * L ? i : 0);
+            for (int u = 0; u < UT; ++u) {
+                const int i = u * NT + (int)threadIdx.x;
+                t[u] = ld_global2(f.slot_temp, i < 9 * C * L ? i : 0);
+            }
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                const int i = u * NT + (int)threadIdx.x;
+                if (i < 9 * C * L) tl[i] = t[u];
+            }
         }
         const int np2 = 2 * bdepth * nblk;
         const int pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
         const int kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
-#pragma unroll
-        for (int u = 0; u < UT; ++u) {
-            const int i = u * NT + (int)threadIdx.x;
-            if (i < 9 * C * L) tl[i] = t[u];
-        }
         if ((int)threadIdx.x < np2) pairs[threadIdx.x] = pv;
         for (int i = threadIdx.x + NT; i < np2; i += NT) pairs[i] = f.blk_pairs[i];
         if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
@@ -388,7 +405,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
         wfence();
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const int ci = si_comp(si[c]);
+            const int ci = si_store_b(si[c]);
             if (ci >= 0 && !DBG(32)) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
@@ -434,7 +451,12 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             for (int a = 0; a < 3; ++a) {
                 cx tm[9];
 #pragma unroll
-                for (int l = 0; l < 3; ++l) tm[l * 3 + a] = DBG(1) ? mk(0.001 * l, 0.002 * a) : ldx(tl, ((l * 3 + a) * C + c) * L + li);
+                for (int l = 0; l < 3; ++l) {
+                    const int ti = ((l * 3 + a) * C + c) * L + li;
+                    if (DBG(1)) tm[l * 3 + a] = mk(0.001 * l, 0.002 * a);
+                    else if (TEMP_IN_LDS) tm[l * 3 + a] = ldx(tl, ti);
+                    else { const double2 t = ld_global2(f.slot_temp, ti); tm[l * 3 + a] = mk(t.x, t.y); }
+                }
                 g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
                 lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
             }
@@ -457,7 +479,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
         wfence();
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const int ci = si_comp(si[c]);
+            const int ci = si_store_f(si[c]);
             if (ci >= 0 && !DBG(64)) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
@@ -479,7 +501,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
                     }
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + li, of[p]);
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, of[p]);
             }
         } else {
             for (int b = li; b < nblk; b += L) {
@@ -490,7 +512,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, of[p]);
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, of[p]);
             }
         }
         wfence();
@@ -498,7 +520,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
         for (int c = 0; c < C; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                g[c][p] = cadd(g[c][p], ldx(OFF, p * nblk + si_blk(si[c])));   // A(k)
+                g[c][p] = cadd(g[c][p], ldx(OFF, p * OS + bk[c]));   // A(k)
                 v[c][p] = csub(v0[p], g[c][p]);
                 if (FULL && ((si_mask(si[c]) >> p) & 1)) v[c][p] = mk(0.0, 0.0);
             }
@@ -507,7 +529,7 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
             wfence();
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const int ci = si_comp(si[c]);
+                const int ci = si_store_f(si[c]);
                 if (ci >= 0) {
 #pragma unroll
                     for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
@@ -707,27 +729,35 @@ __global__ __launch_bounds__((WaveGeom<SPW, C, HALF>::WPB * 64), (WaveGeom<SPW, 
     }
 }
 
-namespace {
-int wave_wpb(const WaveDev &w) { return (w.spw * w.C <= 2 ? 16 : 8) >> (w.half ? 1 : 0); }   // = WaveGeom::WPB
-}  // namespace
-
 size_t wave_lds_bytes(const WaveDev &w) {
-    const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)wave_wpb(w) * w.spw;
+    const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + 3 * (size_t)w.nblk) | 1);
+    const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk)) | 1);
     const size_t stage = 8 * 6 * (size_t)w.nl * (spb + 1);           // the loads, staged over the regions
-    const size_t agg = 8 * 8 * (size_t)wave_wpb(w) * 64;               // the last workgroup's fold
-    return 16 * (9 * (size_t)w.C * L) + pairs + std::max(regions, std::max(stage, agg));
+    const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
+    const size_t temp = TEMP_IN_LDS ? 16 * (9 * (size_t)w.C * L) : 0;
+    return temp + pairs + std::max(regions, std::max(stage, agg));
 }
 
-int wave_scenarios_per_block(const WaveDev &w) { return wave_wpb(w) * w.spw; }
+int wave_scenarios_per_block(const WaveDev &w) { return w.wpb * w.spw; }
+
+// the waves-per-workgroup choices each geometry is built for
+bool wave_wpb_supported(int spw, int c, int wpb) {
+    return spw * c <= 2 ? (wpb == 16 || wpb == 8) : (wpb == 8 || wpb == 4);
+}
 
 namespace {
 typedef void (*WaveKernel)(WaveDev, int, const double *, OutDev);
 template <int SPW, int C>
-WaveKernel pick(bool full, bool half) {
-    return half ? (full ? dpf_wave_kernel<SPW, C, true, true> : dpf_wave_kernel<SPW, C, false, true>)
-                : (full ? dpf_wave_kernel<SPW, C, true, false> : dpf_wave_kernel<SPW, C, false, false>);
+WaveKernel pick(bool full, int wpb) {
+    if constexpr (SPW * C <= 2) {
+        if (wpb == 16) return full ? dpf_wave_kernel<SPW, C, true, 16> : dpf_wave_kernel<SPW, C, false, 16>;
+        if (wpb == 8) return full ? dpf_wave_kernel<SPW, C, true, 8> : dpf_wave_kernel<SPW, C, false, 8>;
+    } else {
+        if (wpb == 8) return full ? dpf_wave_kernel<SPW, C, true, 8> : dpf_wave_kernel<SPW, C, false, 8>;
+        if (wpb == 4) return full ? dpf_wave_kernel<SPW, C, true, 4> : dpf_wave_kernel<SPW, C, false, 4>;
+    }
+    return nullptr;
 }
 }  // namespace
 
@@ -740,13 +770,13 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
     WaveKernel k = nullptr;
     int id = -1;
-    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, w.half); id = 0; }
-    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full, w.half); id = 1; }
-    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full, w.half); id = 2; }
-    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full, w.half); id = 3; }
-    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full, w.half); id = 4; }
-    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, w.half); id = 5; }
-    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, w.half); id = 6; }
+    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, w.wpb); id = 0; }
+    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full, w.wpb); id = 1; }
+    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full, w.wpb); id = 2; }
+    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full, w.wpb); id = 3; }
+    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full, w.wpb); id = 4; }
+    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, w.wpb); id = 5; }
+    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, w.wpb); id = 6; }
     if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the
     // static part) -- a per-device setting, done once per (device, variant)
@@ -756,7 +786,7 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> lk(mu);
-        const std::array<int, 4> key = {dev, id, (int)full, w.half};
+        const std::array<int, 4> key = {dev, id, (int)full, w.wpb};
         if (!attr_done.count(key)) {
             hipFuncAttributes fa{};
             hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
@@ -767,13 +797,13 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
             attr_done.insert(key);
         }
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(wave_wpb(w) * 64), lds, st, w, n_scen, pq, o);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(w.wpb * 64), lds, st, w, n_scen, pq, o);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess && getenv("FPF_DEBUG")) {
         hipFuncAttributes fa{};
         (void)hipFuncGetAttributes(&fa, (const void *)k);
         fprintf(stderr, "launch_wave: %s grid %u block %d dyn lds %zu static %zu maxdyn %d regs %d local %zu\n",
-                hipGetErrorString(e), grid, wave_wpb(w) * 64, lds, fa.sharedSizeBytes, fa.maxDynamicSharedSizeBytes,
+                hipGetErrorString(e), grid, w.wpb * 64, lds, fa.sharedSizeBytes, fa.maxDynamicSharedSizeBytes,
                 fa.numRegs, fa.localSizeBytes);
     }
     return e;

@@ -175,6 +175,14 @@ long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
                                   const double *z, int z_rows, int z_cols,
                                   const fpf_opts *opts, char *buf, size_t buf_size);
 
+/* Diagnostics (no device needed): the wave kernel's plan for this feeder.
+ * out[0..7] = {accepted (1/0), scenarios per wavefront, slots per lane,
+ * wavefronts per workgroup, LDS bytes per workgroup, gathered scan entries,
+ * blocks, block-chain depth}.  Returns FPF_OK or FPF_ERR_*. */
+int         fpf_feeder_wave_plan(const double *dl, int nl, int ncols,
+                                 const double *z, int z_rows, int z_cols,
+                                 const fpf_opts *opts, int out[8]);
+
 /* Device-memory batch aggregate over per-scenario results (deterministic
  * reduction); same layout as fpf_aggregate.  Lets a caller aggregate several
  * batches, or time the solve kernel alone. */

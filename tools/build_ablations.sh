@@ -1,0 +1,17 @@
+#!/bin/bash
+# Compile-time ablation builds of the wave kernel (FPF_WAVE_ABL=<bits>, see the
+# DBG() uses in fpf_wave.hip): one library per bit set in freedm_amd/lib/abl/.
+# Diagnostic only -- results are wrong by design.
+set -e
+cd "$(dirname "$0")/../freedm_amd/csrc"
+OUT=../lib/abl
+mkdir -p $OUT
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I../../include"
+OBJS="../lib/fpf_api.o ../lib/fpf_generic.o ../lib/fpf_tiled.o ../lib/fpf_rtc.o ../lib/fpf_selftest.o ../lib/fpf_vvc.o"
+for m in "$@"; do
+  /opt/rocm/bin/hipcc $FLAGS -DFPF_WAVE_ABL=$m -c fpf_wave.hip -o $OUT/wave_$m.o &
+done
+wait
+for m in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libfreedm_pf_$m.so $OBJS $OUT/wave_$m.o -lhiprtc
+done
