@@ -371,6 +371,12 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     // last scenario is done.
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     bool done = !live;
+#ifdef FPF_WAVE_STAGGER
+    // diagnostic: start the second half of the workgroup's waves (each shares a
+    // SIMD with one of the first half) later, so partners sit in different
+    // phases of a sweep (MI355X_MICROARCH.md "Two waves per SIMD", item 9)
+    if (WPB >= 8 && wv >= WPB / 2) __builtin_amdgcn_s_sleep(FPF_WAVE_STAGGER);
+#endif
     WSTAMP(2);
     for (int it = 0; __ballot(!done) != 0; ++it) {
         // ---- load currents (:106-130)
@@ -437,6 +443,8 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         const unsigned long long cbits = __ballot(li == L - 1 && err2 < f.eps * f.eps);
         const bool conv = (cbits >> (seg * L + L - 1)) & 1;
         const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
+        // the loss terms are needed only in a scenario's last sweep
+        const bool any_fin = __ballot(fin) != 0;
 
         // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
         // Also Re(drop . conj(Ib)) per phase: on a feeder without zeroed phases
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     else { const double2 t = ld_global2(f.slot_temp, ti); tm[l * 3 + a] = mk(t.x, t.y); }
                 }
                 g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
-                lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
+                if (any_fin) lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
             }
         }
 #pragma unroll
@@ -486,9 +494,11 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             }
         }
         wfence();
-        // block offsets, one lane per block (block 0, node 1's chain, has none);
-        // the chain's index pairs sit in registers (bp), all its reads issue together
+        // block offsets, one lane per block (block 0, node 1's chain, has none),
+        // stored as V0 - off so that V = (V0 - off) - Ginc is one subtraction per
+        // slot; the chain's index pairs sit in registers (bp), all its reads issue together
         if (DBG(8)) {
+            if (li < 3) X[li * XC] = make_double2(v0[li].re, v0[li].im);
         } else if (nblk <= L && bdepth <= WAVE_BD) {
             if (li < nblk) {
                 cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
@@ -501,7 +511,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     }
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, of[p]);
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(v0[p], of[p]));
             }
         } else {
             for (int b = li; b < nblk; b += L) {
@@ -512,7 +522,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, of[p]);
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(v0[p], of[p]));
             }
         }
         wfence();
@@ -520,12 +530,13 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         for (int c = 0; c < C; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                g[c][p] = cadd(g[c][p], ldx(OFF, p * OS + bk[c]));   // A(k)
-                v[c][p] = csub(v0[p], g[c][p]);
-                if (FULL && ((si_mask(si[c]) >> p) & 1)) v[c][p] = mk(0.0, 0.0);
+                const cx vr = csub(ldx(OFF, p * OS + bk[c]), g[c][p]);   // V0 - A(k)
+                if (FULL) g[c][p] = vr;
+                v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;
             }
         if (FULL && f.has_rel) {
-            // below a zeroed ancestor m: V(k,p) = A(m) - A(k)
+            // below a zeroed ancestor m: V(k,p) = A(m) - A(k) = Vr(k) - Vr(m), Vr = V0 - A
+            // before the zeroing (held in g)
             wfence();
 #pragma unroll
             for (int c = 0; c < C; ++c) {
@@ -541,7 +552,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     const int mr = f.slot_mref[(p * C + c) * L + li];
-                    if (mr >= 0 && !((si_mask(si[c]) >> p) & 1)) v[c][p] = csub(ldx(X, p * XC + mr), g[c][p]);
+                    if (mr >= 0 && !((si_mask(si[c]) >> p) & 1)) v[c][p] = csub(g[c][p], ldx(X, p * XC + mr));
                 }
         }
         wfence();
