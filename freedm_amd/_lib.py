@@ -21,7 +21,9 @@ KERNELS = {"auto": FPF_KERNEL_AUTO, "generic": FPF_KERNEL_GENERIC, "tiled": FPF_
 EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_destroy", "fpf_last_error",
            "fpf_feeder_create", "fpf_feeder_destroy", "fpf_feeder_get_info", "fpf_feeder_reserve",
            "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source",
-           "fpf_selftest_division", "fpf_vvc_line_search", "fpf_feeder_wave_plan"]
+           "fpf_selftest_division", "fpf_vvc_line_search", "fpf_feeder_wave_plan",
+           "fpf_multi_create", "fpf_multi_destroy", "fpf_multi_last_error", "fpf_multi_solve", "fpf_multi_get_feeder",
+           "fpf_multi_shard", "fpf_aggregate_fold"]
 
 
 class FpfOpts(C.Structure):
@@ -118,6 +120,22 @@ def load(path: str | None = None):
         L.fpf_feeder_wave_plan.restype = C.c_int
     L.fpf_selftest_division.argtypes = [C.c_int, C.c_long, C.c_ulong]
     L.fpf_selftest_division.restype = C.c_long
+    if hasattr(L, "fpf_multi_create") or path == LIB_PATH:   # (older diagnostic builds lack them)
+        L.fpf_multi_create.argtypes = [C.c_int, _dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
+                                       C.POINTER(vp)]
+        L.fpf_multi_create.restype = C.c_int
+        L.fpf_multi_destroy.argtypes = [vp]
+        L.fpf_multi_destroy.restype = None
+        L.fpf_multi_last_error.argtypes = [vp]
+        L.fpf_multi_last_error.restype = C.c_char_p
+        L.fpf_multi_solve.argtypes = [vp, C.c_int, _dp, C.POINTER(FpfOutputs), C.POINTER(FpfAggregate)]
+        L.fpf_multi_solve.restype = C.c_int
+        L.fpf_multi_get_feeder.argtypes = [vp, C.c_int, C.POINTER(vp)]
+        L.fpf_multi_get_feeder.restype = C.c_int
+        L.fpf_multi_shard.argtypes = [C.c_int, C.c_int, C.c_long, C.POINTER(C.c_long), C.POINTER(C.c_long)]
+        L.fpf_multi_shard.restype = C.c_int
+        L.fpf_aggregate_fold.argtypes = [C.POINTER(FpfAggregate), C.c_int, C.POINTER(FpfAggregate)]
+        L.fpf_aggregate_fold.restype = None
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
                  "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device"):
         getattr(L, name).restype = C.c_int

@@ -21,7 +21,7 @@ import numpy as np
 from . import _lib
 from .feeder import Feeder
 
-__all__ = ["PowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError"]
+__all__ = ["PowerFlow", "MultiPowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError"]
 
 
 class DPFError(RuntimeError):
@@ -262,6 +262,69 @@ class PowerFlow:
                    PQL=r["PQL"][:, :, 0].T.copy(), Qset_a=Dl[:, 7:8].copy(), Qset_b=Dl[:, 9:10].copy(),
                    Qset_c=Dl[:, 11:12].copy(), V=V, iters=int(r["iters"][0]), loss=float(r["loss"][0]),
                    vmin=float(r["vmin"][0]), vmax=float(r["vmax"][0]))
+
+
+class MultiPowerFlow:
+    """One process, n GPUs (fpf_multi_*): the batch is sharded contiguously over
+    devices 0..n-1, every device solves its shard, and the per-device
+    aggregates are combined by one RCCL all-reduce inside the library."""
+
+    def __init__(self, feeder: Feeder, n_gpus: int = 1, kernel: str = "auto", **opts):
+        L = _lib.load()
+        self.feeder = feeder
+        self.n_gpus = n_gpus
+        o = _lib.default_opts(kernel=kernel, **opts)
+        dl = np.asfortranarray(feeder.Dl, dtype=np.float64)
+        Z = np.asarray(feeder.Z, dtype=np.complex128)
+        zbuf = np.zeros(max(2 * Z.size, 2))
+        zbuf[0:2 * Z.size:2] = Z.real.ravel(order="F")
+        zbuf[1:2 * Z.size:2] = Z.imag.ravel(order="F")
+        h = C.c_void_p()
+        rc = L.fpf_multi_create(n_gpus, dl.ctypes.data_as(_lib._dp), dl.shape[0], dl.shape[1],
+                                zbuf.ctypes.data_as(_lib._dp), Z.shape[0], Z.shape[1], C.byref(o), C.byref(h))
+        if rc:
+            raise DPFError(rc, f"fpf_multi_create(n_gpus={n_gpus}) failed")
+        self.h = h
+        f0 = C.c_void_p()
+        L.fpf_multi_get_feeder(h, 0, C.byref(f0))
+        info = _lib.FpfFeederInfo()
+        L.fpf_feeder_get_info(f0, C.byref(info))
+        self.info = info.as_dict()
+        self.nl, self.nn = self.info["nl"], self.info["nn"]
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            _lib.load().fpf_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, pq: np.ndarray, full: bool = True) -> dict:
+        """Same arguments and results as PowerFlow.solve, over all the GPUs."""
+        L = _lib.load()
+        pq = np.ascontiguousarray(pq, dtype=np.float64)
+        if pq.ndim != 3 or pq.shape[:2] != (6, self.nl):
+            raise ValueError(f"pq must be [6][{self.nl}][B]")
+        B, nn = pq.shape[2], self.nn
+        r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
+             "vmin": np.zeros(B), "vmax": np.zeros(B)}
+        if full:
+            r.update(Vpolar=np.zeros((6, nn, B)), PQb=np.zeros((6, nn, B)), PQL=np.zeros((6, nn, B)),
+                     V_re=np.zeros((3, nn, B)), V_im=np.zeros((3, nn, B)))
+        out = _lib.FpfOutputs(_ptr(r.get("Vpolar")), _ptr(r.get("PQb")), _ptr(r.get("PQL")), _ptr(r.get("V_re")),
+                              _ptr(r.get("V_im")), _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]),
+                              _ptr(r["vmin"]), _ptr(r["vmax"]))
+        agg = _lib.FpfAggregate()
+        rc = L.fpf_multi_solve(self.h, B, pq.ctypes.data_as(_lib._dp), C.byref(out), C.byref(agg))
+        if rc < 0:
+            raise DPFError(rc, L.fpf_multi_last_error(self.h).decode())
+        r["n_nonconv"] = rc
+        r["aggregate"] = agg.as_dict()
+        return r
 
 
 _pf_cache: "OrderedDict[tuple, PowerFlow]" = OrderedDict()

@@ -168,6 +168,34 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);
 
+/* ---- Multi-GPU study: one process, n GPUs of a node.
+ * fpf_multi_create uploads the feeder to devices 0..n_gpus-1 (one context,
+ * stream and feeder each) and builds an RCCL communicator over them
+ * (ncclCommInitAll; xGMI inside an MI355X node).  fpf_multi_solve cuts the
+ * batch into contiguous shards (fpf_multi_shard), solves every shard on its
+ * device concurrently and combines the per-device batch aggregates with one
+ * RCCL all-reduce (sum of the 8 fields, min of vmin, max of vmax) -- the only
+ * exchange: per-scenario results go straight back to the caller's host arrays
+ * at their global index.  pq / out / agg as fpf_solve_batch (host memory, the
+ * whole batch's layout).  Returns >= 0 (non-converged scenarios) or FPF_ERR_*.
+ * With n_gpus = 1 the results equal fpf_solve_batch's bit for bit. */
+typedef struct fpf_multi fpf_multi;
+int         fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
+                             const double *z, int z_rows, int z_cols,
+                             const fpf_opts *opts, fpf_multi **out);
+void        fpf_multi_destroy(fpf_multi *m);
+const char *fpf_multi_last_error(const fpf_multi *m);
+int         fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq,
+                            const fpf_outputs *out, fpf_aggregate *agg);
+/* the feeder handle of one device (for fpf_feeder_get_info, device batches) */
+int         fpf_multi_get_feeder(fpf_multi *m, int device, fpf_feeder **out);
+/* The partition (no device needed): scenarios [lo, hi) of `rank` out of
+ * n_total over n_gpus, contiguous, sizes differing by at most one. */
+int         fpf_multi_shard(int rank, int n_gpus, long n_total, long *lo, long *hi);
+/* The combine the all-reduce performs, on the host (no device needed):
+ * sums of fields 0 and 3..7, min of vmin, max of vmax; n = 0 gives the identity. */
+void        fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate *out);
+
 /* Diagnostics (no device needed): the hipRTC source fpf_feeder_create would
  * compile for this feeder's tiled kernel.  Writes at most buf_size bytes
  * (NUL-terminated) and returns the full size including the NUL, or FPF_ERR_*. */
