@@ -369,3 +369,48 @@ def test_track_counts_are_bit_identical(tracks, monkeypatch):
         np.testing.assert_array_equal(r["PQb"][:, :, :4], g["PQb"], err_msg=name)
         np.testing.assert_array_equal(r["PQL"][:, :, :4], g["PQL"], err_msg=name)
         np.testing.assert_array_equal(r["loss"], g["loss"], err_msg=name)
+
+
+def test_config3_full_size_against_oracle():
+    """BASELINE config 3 at its stated size: the 2048-bus feeder, 65 536
+    scenarios in one batch (auto kernel = the generic kernel at this batch
+    size).  The batch is built on the GPU from 1 024 seeded base scenarios
+    (config-3 generator, seed 65536) times a per-scenario multiplier, so all
+    65 536 differ; a strided sample of 65 scenarios is recomputed by the oracle
+    with the same inputs: identical iteration counts and status, V bit-identical
+    (the generic kernel is exact mode) and within the 1e-10 bar."""
+    import torch
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(2048, 2048)
+    B, NB = 65536, 1024
+    base = F.scenario_loads(f, np.arange(NB), seed=65536)
+    dev = torch.device("cuda:0")
+    s = np.arange(B, dtype=np.int64)
+    mult = 0.9 + 0.2 * (((s * 2654435761) % 1000) / 1000.0)
+    d_pq = torch.from_numpy(base).to(dev)[:, :, torch.from_numpy(s % NB).to(dev)] * torch.from_numpy(mult).to(dev)
+    pf = PowerFlow(f, device=0)
+    nn = pf.nn
+    out = {"v_re": torch.empty((3, nn, B), dtype=torch.float64, device=dev),
+           "v_im": torch.empty((3, nn, B), dtype=torch.float64, device=dev),
+           "iters": torch.empty(B, dtype=torch.int32, device=dev), "status": torch.empty(B, dtype=torch.int8, device=dev),
+           "loss": torch.empty(B, dtype=torch.float64, device=dev), "vmin": torch.empty(B, dtype=torch.float64, device=dev),
+           "vmax": torch.empty(B, dtype=torch.float64, device=dev)}
+    agg = torch.zeros(8, dtype=torch.float64, device=dev)
+    pf.solve_device(d_pq, out, agg=agg)
+    torch.cuda.synchronize()
+    a = agg.cpu().numpy()
+    assert a[7] == B and a[3] + a[4] == B
+    idx = np.arange(0, B, 1021)
+    ti = torch.from_numpy(idx).to(dev)
+    pq_s = np.ascontiguousarray(base[:, :, idx % NB] * mult[idx])
+    c = O.dpf_batch(f.Dl, f.Z, pq_s, nthreads=8)
+    it = out["iters"][ti].cpu().numpy()
+    st = out["status"][ti].cpu().numpy()
+    assert (it == c["iters"]).all() and (st == c["status"]).all()
+    v_re = out["v_re"][:, :, ti].cpu().numpy()
+    v_im = out["v_im"][:, :, ti].cpu().numpy()
+    assert _vrel(v_re, v_im, c["V_re"], c["V_im"]) <= 1e-10
+    np.testing.assert_array_equal(v_re, c["V_re"])
+    np.testing.assert_array_equal(v_im, c["V_im"])
+    np.testing.assert_array_equal(out["loss"][ti].cpu().numpy(), c["loss"])
