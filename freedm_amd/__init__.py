@@ -11,12 +11,12 @@ from .feeder import (Feeder, demo_feeder, dl_new_feeder, synthetic_feeder, scena
 
 __all__ = ["Feeder", "demo_feeder", "dl_new_feeder", "synthetic_feeder", "scenario_loads", "hosting_loads",
            "load_raw_ascii", "load_arma_bin", "save_arma_bin", "save_raw_ascii",
-           "PowerFlow", "MultiPowerFlow", "DPF_return7", "VPQ", "DPFError", "NonConvergedError", "build"]
+           "PowerFlow", "MultiPowerFlow", "AreaPowerFlow", "DPF_return7", "VPQ", "DPFError", "NonConvergedError", "build"]
 
 
 def __getattr__(name):
     # the engine loads libfreedm_pf (and torch's HIP runtime) lazily
-    if name in ("PowerFlow", "MultiPowerFlow", "DPF_return7", "VPQ", "DPFError", "NonConvergedError"):
+    if name in ("PowerFlow", "MultiPowerFlow", "AreaPowerFlow", "DPF_return7", "VPQ", "DPFError", "NonConvergedError"):
         from . import engine
         return getattr(engine, name)
     raise AttributeError(name)

@@ -23,7 +23,8 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source",
            "fpf_selftest_division", "fpf_vvc_line_search", "fpf_feeder_wave_plan",
            "fpf_multi_create", "fpf_multi_destroy", "fpf_multi_last_error", "fpf_multi_solve", "fpf_multi_get_feeder",
-           "fpf_multi_shard", "fpf_aggregate_fold"]
+           "fpf_multi_shard", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
+           "fpf_areas_info", "fpf_areas_solve"]
 
 
 class FpfOpts(C.Structure):
@@ -136,6 +137,19 @@ def load(path: str | None = None):
         L.fpf_multi_shard.restype = C.c_int
         L.fpf_aggregate_fold.argtypes = [C.POINTER(FpfAggregate), C.c_int, C.POINTER(FpfAggregate)]
         L.fpf_aggregate_fold.restype = None
+    if hasattr(L, "fpf_areas_create") or path == LIB_PATH:
+        L.fpf_areas_create.argtypes = [vp, _dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int,
+                                       C.POINTER(FpfOpts), C.POINTER(vp)]
+        L.fpf_areas_create.restype = C.c_int
+        L.fpf_areas_destroy.argtypes = [vp]
+        L.fpf_areas_destroy.restype = None
+        L.fpf_areas_last_error.argtypes = [vp]
+        L.fpf_areas_last_error.restype = C.c_char_p
+        L.fpf_areas_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.fpf_areas_info.restype = C.c_int
+        L.fpf_areas_solve.argtypes = [vp, C.c_int, _dp, C.c_double, C.c_int, C.POINTER(FpfOutputs),
+                                      C.POINTER(FpfAggregate)]
+        L.fpf_areas_solve.restype = C.c_int
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
                  "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device"):
         getattr(L, name).restype = C.c_int

@@ -133,6 +133,8 @@ extern "C" void fpf_ctx_destroy(fpf_ctx *c) {
 
 extern "C" const char *fpf_last_error(const fpf_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
+int fpf::ctx_device(const fpf_ctx *c) { return c ? c->device : 0; }
+
 // ---------------------------------------------------------------------------- feeder analysis
 
 namespace {
@@ -1368,6 +1370,11 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
 
 extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out,
                                       double *d_agg, void *stream) {
+    return fpf::solve_batch_device_ex(f, n_scen, d_pq, d_out, d_agg, stream, nullptr, nullptr);
+}
+
+int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
+                               void *stream, const double *d_vsrc, double *d_s_in) {
     if (!f || n_scen < 0 || (n_scen > 0 && !d_pq)) return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "bad arguments");
     fpf_ctx *ctx = f->ctx;
     if (n_scen == 0) return FPF_OK;
@@ -1394,6 +1401,8 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
     o.agg = nullptr;
     o.partials = nullptr;
     o.ticket = nullptr;
+    o.vsrc = d_vsrc;
+    o.s_in = d_s_in;
     hipError_t e;
     bool agg_done = false;
     const int kern = kernel_for(f, n_scen);
@@ -1416,6 +1425,8 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
         agg_done = true;
         HIPCHK(ctx, agg_before(f, st));
     }
+    if ((d_vsrc || d_s_in) && kern != FPF_KERNEL_WAVE)
+        return fail(ctx, FPF_ERR_UNSUPPORTED, "per-scenario source voltages need the wave kernel");
     if (kern == FPF_KERNEL_WAVE) {
         e = launch_wave(wave_dev_for(f, n_scen), n_scen, d_pq, o, st);
     } else if (kern == FPF_KERNEL_TILED) {

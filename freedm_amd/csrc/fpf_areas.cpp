@@ -1,0 +1,470 @@
+// fpf_areas.cpp -- the multi-area solve (BASELINE config 5: the Broker_s1..s3
+// feeder areas).  The reference splits the feeder by SST ownership across
+// three slave DGIs (Broker_s1/src/vvc/VoltVarCtrl.cpp:327-395: s1 = SST2-4,
+// s2 = SST1, s3 = SST5-7 -- the rows of the master's SST map,
+// Broker/src/vvc/VoltVarCtrl.cpp:442-1135) but the slaves never solve a power
+// flow; this is the "per-area batched solves with boundary-voltage exchange"
+// of SURVEY.md 8(d) config 5 -- an algorithm with no reference counterpart,
+// checked against the monolithic solve.
+//
+// Each area is a connected subtree of the feeder.  Its own Dl table (rebuilt
+// with local node numbers, chain-first blocks) is fed from its boundary bus:
+// local node 0 is the bus of the parent area its top branch hangs off.  One
+// outer iteration, batched over all scenarios on the GPU:
+//   for each area, parents before children:
+//     loads  = the area's own loads + at every bus a child hangs off, the power
+//              the child drew at its source in the previous iteration (PQb row 0);
+//     source = V0 for the root area, else the parent's voltage at the boundary
+//              bus from this iteration;
+//     a full DPF solve of the area (wave kernel, the caller's eps / mxitr).
+// until no boundary voltage moves by more than `tol` (p.u.).  At the fixed
+// point every area satisfies the monolithic equations (constant-power loads,
+// the same branch impedances), so V equals the monolithic solution to the
+// solver tolerance: the areas' eps and `tol` near 1e-12 give 1e-10 agreement
+// with a monolithic solve run to the same eps (tests/test_areas.py).
+#include "../../include/freedm_pf.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fpf_internal.h"
+
+namespace fpf {
+hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, int nl, int B, double *dst,
+                             hipStream_t st);
+hipError_t areas_add_row(double *work, int nl, int lrow, int B, const double *add, hipStream_t st);
+hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
+                             hipStream_t st);
+hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
+                               hipStream_t st);
+hipError_t areas_fold_results(int B, const double *loss, const double *vmin, const double *vmax, const int8_t *status,
+                              int first, double *o_loss, double *o_vmin, double *o_vmax, int8_t *o_status,
+                              hipStream_t st);
+hipError_t areas_max(const double *x, int n, double *out, hipStream_t st);
+}  // namespace fpf
+
+using namespace fpf;
+
+namespace {
+struct Area {
+    int parent = -1;             // parent area, -1: the root (fed from the substation)
+    int bus = 0;                 // monolithic bus it is fed from (root: 0)
+    int lb = 0;                  // that bus's local node in the parent area
+    std::vector<double> dl;      // local Dl, nl x ncols column-major
+    int nl = 0, nn = 0;
+    std::vector<int32_t> row_of_local;   // local Dl row -> monolithic row (-1: separator)
+    std::vector<int32_t> mono;           // local node -> monolithic node (local 0 -> bus)
+    std::vector<int> local_of;           // monolithic node -> local node (-1: not here)
+    std::vector<std::pair<int, int>> kids;   // (local row carrying the bus's load, child area)
+    fpf_feeder *feeder = nullptr;
+    // device buffers
+    int32_t *d_rows = nullptr, *d_mono = nullptr;
+    double *d_base = nullptr, *d_work = nullptr, *d_vsrc = nullptr, *d_sin = nullptr;
+    double *d_vre = nullptr, *d_vim = nullptr, *d_loss = nullptr, *d_vmin = nullptr, *d_vmax = nullptr;
+    int32_t *d_iters = nullptr;
+    int8_t *d_status = nullptr;
+};
+}  // namespace
+
+struct fpf_areas {
+    fpf_ctx *ctx = nullptr;
+    int nl = 0, ncols = 0, nn = 0;
+    std::vector<Area> area;      // index = area id, parents before children
+    std::vector<int> order;      // solve order
+    int cap = 0;
+    double *d_pq = nullptr, *d_diff = nullptr, *d_max = nullptr;
+    std::string err;
+};
+
+namespace {
+int afail(fpf_areas *a, int code, const std::string &msg) {
+    if (a) a->err = msg;
+    return code;
+}
+#define AHIP(a, expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) return afail(a, FPF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+void free_area_buffers(Area &ar) {
+    (void)hipFree(ar.d_base);
+    (void)hipFree(ar.d_work);
+    (void)hipFree(ar.d_vsrc);
+    (void)hipFree(ar.d_sin);
+    (void)hipFree(ar.d_vre);
+    (void)hipFree(ar.d_vim);
+    (void)hipFree(ar.d_loss);
+    (void)hipFree(ar.d_vmin);
+    (void)hipFree(ar.d_vmax);
+    (void)hipFree(ar.d_iters);
+    (void)hipFree(ar.d_status);
+    ar.d_base = ar.d_work = ar.d_vsrc = ar.d_sin = ar.d_vre = ar.d_vim = nullptr;
+    ar.d_loss = ar.d_vmin = ar.d_vmax = nullptr;
+    ar.d_iters = nullptr;
+    ar.d_status = nullptr;
+}
+}  // namespace
+
+extern "C" void fpf_areas_destroy(fpf_areas *a) {
+    if (!a) return;
+    if (a->ctx) (void)hipSetDevice(ctx_device(a->ctx));
+    for (Area &ar : a->area) {
+        free_area_buffers(ar);
+        (void)hipFree(ar.d_rows);
+        (void)hipFree(ar.d_mono);
+        fpf_feeder_destroy(ar.feeder);
+    }
+    (void)hipFree(a->d_pq);
+    (void)hipFree(a->d_diff);
+    (void)hipFree(a->d_max);
+    delete a;
+}
+
+extern "C" const char *fpf_areas_last_error(const fpf_areas *a) { return a ? a->err.c_str() : "null context"; }
+
+extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncols, const double *z, int z_rows,
+                                int z_cols, const int *node_area, int nn, const fpf_opts *opts, fpf_areas **out) {
+    if (!ctx || !dl || !node_area || !out || nl < 1 || ncols < 12 || nn < 2) return FPF_ERR_ARG;
+    *out = nullptr;
+    if (hipSetDevice(ctx_device(ctx)) != hipSuccess) return FPF_ERR_HIP;
+    auto at = [&](int r, int c) { return dl[(size_t)c * nl + r]; };
+    // the feeder tree: row of each node, parent bus
+    std::vector<int> row_of(nn, -1), par(nn, -1);
+    int nb = 0;
+    for (int m = 0; m < nl; ++m) {
+        if (at(m, 0) == 0) continue;
+        const int k = (int)at(m, 2), s = m == 0 ? 0 : (int)at(m, 1);
+        if (k < 1 || k >= nn || s < 0 || s >= nn || row_of[k] >= 0) return FPF_ERR_TOPOLOGY;
+        row_of[k] = m;
+        par[k] = s;
+        ++nb;
+    }
+    if (nb != nn - 1) return FPF_ERR_TOPOLOGY;
+    int n_areas = 0;
+    for (int k = 1; k < nn; ++k) {
+        if (node_area[k] < 0) return FPF_ERR_ARG;
+        n_areas = std::max(n_areas, node_area[k] + 1);
+    }
+    fpf_areas *a = new fpf_areas();
+    a->ctx = ctx;
+    a->nl = nl;
+    a->ncols = ncols;
+    a->nn = nn;
+    a->area.resize(n_areas);
+    // each area: exactly one top node (parent outside the area)
+    std::vector<int> top(n_areas, -1);
+    for (int k = 1; k < nn; ++k) {
+        const int ar = node_area[k];
+        if (par[k] == 0 || node_area[par[k]] != ar) {
+            if (top[ar] >= 0) {
+                fpf_areas_destroy(a);
+                return FPF_ERR_TOPOLOGY;   // area not connected
+            }
+            top[ar] = k;
+        }
+    }
+    for (int ar = 0; ar < n_areas; ++ar)
+        if (top[ar] < 0) {
+            fpf_areas_destroy(a);
+            return FPF_ERR_ARG;   // empty area id
+        }
+    // children of every node, in monolithic row order
+    std::vector<std::vector<int>> kids(nn);
+    for (int m = 0; m < nl; ++m)
+        if (at(m, 0) != 0) {
+            const int k = (int)at(m, 2);
+            kids[par[k]].push_back(k);
+        }
+    for (int ar = 0; ar < n_areas; ++ar) {
+        Area &A = a->area[ar];
+        const int t = top[ar];
+        A.bus = par[t];
+        A.parent = A.bus == 0 ? -1 : node_area[A.bus];
+        A.local_of.assign(nn, -1);
+        A.mono.push_back(A.bus);
+        A.local_of[A.bus] = 0;
+        // rows: chain-first blocks, laterals (within the area) after separators
+        std::vector<std::vector<double>> rows;   // each ncols wide
+        std::vector<int32_t> mrow;
+        std::vector<std::pair<int, int>> queue = {{A.bus, t}};
+        for (size_t qi = 0; qi < queue.size(); ++qi) {
+            int u = queue[qi].first, v = queue[qi].second;
+            if (qi > 0) {
+                rows.push_back(std::vector<double>(ncols, 0.0));
+                mrow.push_back(-1);
+            }
+            while (v >= 0) {
+                const int lv = (int)A.mono.size();
+                A.mono.push_back(v);
+                A.local_of[v] = lv;
+                std::vector<double> r(ncols);
+                for (int c = 0; c < ncols; ++c) r[c] = at(row_of[v], c);
+                r[1] = A.local_of[u];
+                r[2] = lv;
+                rows.push_back(r);
+                mrow.push_back(row_of[v]);
+                int next = -1;
+                for (int w : kids[v])
+                    if (node_area[w] == ar) {
+                        if (next < 0) next = w;
+                        else queue.push_back({v, w});
+                    }
+                u = v;
+                v = next;
+            }
+        }
+        // DPF_return7 indexes V by receiving bus in a field of Nl entries
+        // (DPF_return7.cpp:92-96, 113), so a table without a separator row
+        // cannot hold its last bus: such an area gets a zero-length, unloaded
+        // lateral (its bus repeats its tap's voltage and carries no current)
+        if (std::find(mrow.begin(), mrow.end(), -1) == mrow.end()) {
+            rows.push_back(std::vector<double>(ncols, 0.0));
+            mrow.push_back(-1);
+            std::vector<double> r(ncols, 0.0);
+            r[0] = 1;
+            r[1] = 1;
+            r[2] = (double)A.mono.size();
+            r[3] = rows[0][3];
+            r[4] = 0.0;
+            r[5] = rows[0][5];
+            rows.push_back(r);
+            mrow.push_back(-2);
+            A.mono.push_back(-1);
+        }
+        A.nl = (int)rows.size();
+        A.nn = (int)A.mono.size();
+        A.dl.assign((size_t)A.nl * ncols, 0.0);
+        int ln = 0;
+        for (int r = 0; r < A.nl; ++r) {
+            for (int c = 0; c < ncols; ++c) A.dl[(size_t)c * A.nl + r] = rows[r][c];
+            if (mrow[r] != -1) A.dl[r] = ++ln;
+        }
+        for (auto &m : mrow) m = m < 0 ? -1 : m;   // the pad row gathers no loads
+        A.row_of_local = mrow;
+    }
+    // children of each area: the local row whose receiving bus is the boundary bus
+    for (int ar = 0; ar < n_areas; ++ar) {
+        Area &A = a->area[ar];
+        if (A.parent < 0) continue;
+        Area &P = a->area[A.parent];
+        A.lb = P.local_of[A.bus];
+        int lrow = -1;
+        for (int r = 0; r < P.nl; ++r)
+            if (P.row_of_local[r] == row_of[A.bus]) lrow = r;
+        if (A.lb < 1 || lrow < 0) {
+            fpf_areas_destroy(a);
+            return FPF_ERR_TOPOLOGY;
+        }
+        P.kids.push_back({lrow, ar});
+    }
+    // solve order: parents first
+    std::vector<int> depth(n_areas, 0);
+    for (int ar = 0; ar < n_areas; ++ar)
+        for (int p = a->area[ar].parent; p >= 0; p = a->area[p].parent) ++depth[ar];
+    a->order.resize(n_areas);
+    for (int ar = 0; ar < n_areas; ++ar) a->order[ar] = ar;
+    std::stable_sort(a->order.begin(), a->order.end(), [&](int x, int y) { return depth[x] < depth[y]; });
+    if (a->area[a->order[0]].parent >= 0) {
+        fpf_areas_destroy(a);
+        return FPF_ERR_TOPOLOGY;
+    }
+    // one feeder per area: the wave kernel (fast mode; per-scenario source voltage)
+    fpf_opts o;
+    if (opts) o = *opts;
+    else fpf_opts_default(&o);
+    o.kernel = FPF_KERNEL_WAVE;
+    o.exact = 0;
+    for (Area &A : a->area) {
+        const int rc = fpf_feeder_create(ctx, A.dl.data(), A.nl, ncols, z, z_rows, z_cols, &o, &A.feeder);
+        if (rc != FPF_OK) {
+            a->err = fpf_last_error(ctx);
+            fpf_areas_destroy(a);
+            return rc;
+        }
+        if (hipMalloc(&A.d_rows, sizeof(int32_t) * A.nl) != hipSuccess ||
+            hipMalloc(&A.d_mono, sizeof(int32_t) * A.nn) != hipSuccess ||
+            hipMemcpy(A.d_rows, A.row_of_local.data(), sizeof(int32_t) * A.nl, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(A.d_mono, A.mono.data(), sizeof(int32_t) * A.nn, hipMemcpyHostToDevice) != hipSuccess) {
+            fpf_areas_destroy(a);
+            return FPF_ERR_HIP;
+        }
+    }
+    *out = a;
+    return FPF_OK;
+}
+
+extern "C" int fpf_areas_info(const fpf_areas *a, int *n_areas, int *area_nodes, int *area_parent) {
+    if (!a || !n_areas) return FPF_ERR_ARG;
+    *n_areas = (int)a->area.size();
+    for (size_t i = 0; i < a->area.size(); ++i) {
+        if (area_nodes) area_nodes[i] = a->area[i].nn - 1;
+        if (area_parent) area_parent[i] = a->area[i].parent;
+    }
+    return FPF_OK;
+}
+
+static int areas_reserve(fpf_areas *a, int B) {
+    if (B <= a->cap) return FPF_OK;
+    for (Area &A : a->area) free_area_buffers(A);
+    (void)hipFree(a->d_pq);
+    (void)hipFree(a->d_diff);
+    (void)hipFree(a->d_max);
+    a->d_pq = a->d_diff = a->d_max = nullptr;
+    a->cap = 0;
+    const size_t b = (size_t)B;
+    AHIP(a, hipMalloc(&a->d_pq, sizeof(double) * 6 * a->nl * b));
+    AHIP(a, hipMalloc(&a->d_diff, sizeof(double) * b));
+    AHIP(a, hipMalloc(&a->d_max, sizeof(double)));
+    for (Area &A : a->area) {
+        AHIP(a, hipMalloc(&A.d_base, sizeof(double) * 6 * A.nl * b));
+        AHIP(a, hipMalloc(&A.d_work, sizeof(double) * 6 * A.nl * b));
+        AHIP(a, hipMalloc(&A.d_vsrc, sizeof(double) * 6 * b));
+        AHIP(a, hipMalloc(&A.d_sin, sizeof(double) * 6 * b));
+        AHIP(a, hipMalloc(&A.d_vre, sizeof(double) * 3 * A.nn * b));
+        AHIP(a, hipMalloc(&A.d_vim, sizeof(double) * 3 * A.nn * b));
+        AHIP(a, hipMalloc(&A.d_loss, sizeof(double) * b));
+        AHIP(a, hipMalloc(&A.d_vmin, sizeof(double) * b));
+        AHIP(a, hipMalloc(&A.d_vmax, sizeof(double) * b));
+        AHIP(a, hipMalloc(&A.d_iters, sizeof(int32_t) * b));
+        AHIP(a, hipMalloc(&A.d_status, sizeof(int8_t) * b));
+    }
+    a->cap = B;
+    return FPF_OK;
+}
+
+// pq: host [6][Nl][B] of the whole feeder; out (host): v_re / v_im [3][Nn][B]
+// in the feeder's node numbering, iters = outer iterations, status (worst
+// area; FPF_NONCONVERGED also when the outer loop did not reach tol), loss
+// (sum over areas), vmin / vmax (over areas).  vpolar / pqb / pql must be NULL.
+extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, double tol, int max_outer,
+                               const fpf_outputs *out, fpf_aggregate *agg) {
+    if (!a || n_scen < 0 || (n_scen > 0 && !pq) || !(tol > 0) || max_outer < 1)
+        return afail(a, FPF_ERR_ARG, "fpf_areas_solve: bad arguments");
+    fpf_outputs none;
+    std::memset(&none, 0, sizeof(none));
+    const fpf_outputs &u = out ? *out : none;
+    if (u.vpolar || u.pqb || u.pql) return afail(a, FPF_ERR_UNSUPPORTED, "fpf_areas_solve: Vpolar / PQb / PQL not produced");
+    if (n_scen == 0) {
+        if (agg) fpf_aggregate_fold(nullptr, 0, agg);
+        return 0;
+    }
+    const int B = n_scen;
+    const size_t b = (size_t)B;
+    AHIP(a, hipSetDevice(ctx_device(a->ctx)));
+    int rc = areas_reserve(a, B);
+    if (rc) return rc;
+    hipStream_t st = nullptr;
+    AHIP(a, hipMemcpy(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice));
+    for (Area &A : a->area) {
+        AHIP(a, areas_gather_rows(a->d_pq, a->nl, A.d_rows, A.nl, B, A.d_base, st));
+        AHIP(a, hipMemsetAsync(A.d_sin, 0, sizeof(double) * 6 * b, st));
+        AHIP(a, hipMemsetAsync(A.d_vsrc, 0, sizeof(double) * 6 * b, st));
+    }
+    int outer = 0;
+    bool conv = false;
+    double last = INFINITY;
+    for (outer = 1; outer <= max_outer && !conv; ++outer) {
+        AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b, st));
+        for (int ar : a->order) {
+            Area &A = a->area[ar];
+            AHIP(a, hipMemcpyAsync(A.d_work, A.d_base, sizeof(double) * 6 * A.nl * b, hipMemcpyDeviceToDevice, st));
+            for (const auto &k : A.kids) AHIP(a, areas_add_row(A.d_work, A.nl, k.first, B, a->area[k.second].d_sin, st));
+            if (A.parent >= 0) {
+                const Area &P = a->area[A.parent];
+                AHIP(a, areas_gather_vsrc(P.d_vre, P.d_vim, P.nn, A.lb, B, A.d_vsrc, a->d_diff, st));
+            }
+            fpf_outputs o;
+            std::memset(&o, 0, sizeof(o));
+            o.v_re = A.d_vre;
+            o.v_im = A.d_vim;
+            o.iters = A.d_iters;
+            o.status = (signed char *)A.d_status;
+            o.loss = A.d_loss;
+            o.vmin = A.d_vmin;
+            o.vmax = A.d_vmax;
+            rc = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)st, A.parent >= 0 ? A.d_vsrc : nullptr,
+                                       A.d_sin);
+            if (rc < 0) return afail(a, rc, std::string("area solve: ") + fpf_last_error(a->ctx));
+        }
+        // the boundary voltages' largest move this iteration (the first always moves)
+        double mx = 0.0;
+        AHIP(a, areas_max(a->d_diff, B, a->d_max, st));
+        AHIP(a, hipMemcpy(&mx, a->d_max, sizeof(double), hipMemcpyDeviceToHost));
+        last = mx;
+        conv = outer > 1 && mx <= tol;
+        if (a->area.size() == 1) conv = true;
+    }
+    --outer;
+    // results in the feeder's numbering; whole-feeder loss / extremes / status
+    double *d_vre = nullptr, *d_vim = nullptr, *d_loss = nullptr, *d_vmin = nullptr, *d_vmax = nullptr;
+    int8_t *d_status = nullptr;
+    AHIP(a, hipMalloc(&d_loss, sizeof(double) * b));
+    AHIP(a, hipMalloc(&d_vmin, sizeof(double) * b));
+    AHIP(a, hipMalloc(&d_vmax, sizeof(double) * b));
+    AHIP(a, hipMalloc(&d_status, b));
+    if (u.v_re || u.v_im) {
+        AHIP(a, hipMalloc(&d_vre, sizeof(double) * 3 * a->nn * b));
+        AHIP(a, hipMalloc(&d_vim, sizeof(double) * 3 * a->nn * b));
+    }
+    bool first = true;
+    for (int ar : a->order) {
+        Area &A = a->area[ar];
+        AHIP(a, areas_fold_results(B, A.d_loss, A.d_vmin, A.d_vmax, A.d_status, first ? 1 : 0, d_loss, d_vmin, d_vmax,
+                                   d_status, st));
+        first = false;
+        if (d_vre) {
+            // the root area's local node 0 is the substation (monolithic node 0)
+            const int k0 = A.parent < 0 ? 0 : 1;
+            AHIP(a, areas_scatter_nodes(A.d_vre, A.nn, k0, A.d_mono, a->nn, B, d_vre, st));
+            AHIP(a, areas_scatter_nodes(A.d_vim, A.nn, k0, A.d_mono, a->nn, B, d_vim, st));
+        }
+    }
+    std::vector<int8_t> h_status(b);
+    AHIP(a, hipMemcpy(h_status.data(), d_status, b, hipMemcpyDeviceToHost));
+    if (!conv)
+        for (auto &x : h_status) x = FPF_NONCONVERGED;
+    std::vector<double> h_loss(b), h_vmin(b), h_vmax(b);
+    AHIP(a, hipMemcpy(h_loss.data(), d_loss, sizeof(double) * b, hipMemcpyDeviceToHost));
+    AHIP(a, hipMemcpy(h_vmin.data(), d_vmin, sizeof(double) * b, hipMemcpyDeviceToHost));
+    AHIP(a, hipMemcpy(h_vmax.data(), d_vmax, sizeof(double) * b, hipMemcpyDeviceToHost));
+    if (u.v_re) AHIP(a, hipMemcpy(u.v_re, d_vre, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost));
+    if (u.v_im) AHIP(a, hipMemcpy(u.v_im, d_vim, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost));
+    (void)hipFree(d_vre);
+    (void)hipFree(d_vim);
+    (void)hipFree(d_loss);
+    (void)hipFree(d_vmin);
+    (void)hipFree(d_vmax);
+    (void)hipFree(d_status);
+    if (u.iters)
+        for (int s = 0; s < B; ++s) u.iters[s] = outer;
+    if (u.status) std::memcpy(u.status, h_status.data(), b);
+    if (u.loss) std::memcpy(u.loss, h_loss.data(), sizeof(double) * b);
+    if (u.vmin) std::memcpy(u.vmin, h_vmin.data(), sizeof(double) * b);
+    if (u.vmax) std::memcpy(u.vmax, h_vmax.data(), sizeof(double) * b);
+    int n_nonconv = 0;
+    fpf_aggregate g;
+    std::memset(&g, 0, sizeof(g));
+    g.vmin = INFINITY;
+    g.vmax = -INFINITY;
+    for (int s = 0; s < B; ++s) {
+        if (h_status[s] == FPF_CONVERGED) {
+            g.loss_sum += h_loss[s];
+            g.vmin = std::min(g.vmin, h_vmin[s]);
+            g.vmax = std::max(g.vmax, h_vmax[s]);
+            g.n_conv += 1;
+        } else {
+            g.n_nonconv += 1;
+            ++n_nonconv;
+        }
+    }
+    g.n_scen = B;
+    if (agg) *agg = g;
+    a->err = "outer iterations " + std::to_string(outer) + ", last boundary move " + std::to_string(last);
+    return n_nonconv;
+}

@@ -1,0 +1,125 @@
+// fpf_areas_kernels.hip -- the boundary exchange of the multi-area solve
+// (fpf_areas.cpp): every kernel is one pass over [field][row][scenario]
+// arrays, scenario fastest, one thread per scenario and field -- coalesced,
+// HBM-bound, a few KB per scenario per outer iteration.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+namespace fpf {
+namespace {
+
+// dst[f][r][s] = src[f][row[r]][s] (row[r] < 0: a separator row, 0)
+__global__ void gather_rows_kernel(const double *__restrict__ src, int nl_src, const int32_t *__restrict__ row, int nl,
+                                   int B, double *__restrict__ dst) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int fr = blockIdx.y;   // f * nl + r
+    if (s >= B) return;
+    const int f = fr / nl, r = fr % nl, m = row[r];
+    dst[(size_t)fr * B + s] = m < 0 ? 0.0 : src[((size_t)f * nl_src + m) * B + s];
+}
+
+// work[f][lrow][s] += add[f][s]  for the 6 load fields (P1 Q1 P2 Q2 P3 Q3)
+__global__ void add_row_kernel(double *__restrict__ work, int nl, int lrow, int B, const double *__restrict__ add) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int f = blockIdx.y;
+    if (s >= B) return;
+    work[((size_t)f * nl + lrow) * B + s] += add[(size_t)f * B + s];
+}
+
+// vsrc[2p][s], vsrc[2p+1][s] = V(p, node lb) of the parent area; diff[s] = max(diff[s], |change|)
+__global__ void gather_vsrc_kernel(const double *__restrict__ v_re, const double *__restrict__ v_im, int nn, int lb,
+                                   int B, double *__restrict__ vsrc, double *__restrict__ diff) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    double d = diff[s];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const double re = v_re[((size_t)p * nn + lb) * B + s], im = v_im[((size_t)p * nn + lb) * B + s];
+        d = fmax(d, fmax(fabs(re - vsrc[(size_t)(2 * p) * B + s]), fabs(im - vsrc[(size_t)(2 * p + 1) * B + s])));
+        vsrc[(size_t)(2 * p) * B + s] = re;
+        vsrc[(size_t)(2 * p + 1) * B + s] = im;
+    }
+    diff[s] = d;
+}
+
+// dst[p][mono[k]][s] = src[p][k][s] for k = k0 .. nn-1
+__global__ void scatter_nodes_kernel(const double *__restrict__ src, int nn, int k0, const int32_t *__restrict__ mono,
+                                     int nn_dst, int B, double *__restrict__ dst) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pk = blockIdx.y;   // p * (nn - k0) + (k - k0)
+    if (s >= B) return;
+    const int p = pk / (nn - k0), k = k0 + pk % (nn - k0), m = mono[k];
+    if (m >= 0) dst[((size_t)p * nn_dst + m) * B + s] = src[((size_t)p * nn + k) * B + s];   // m < 0: a pad bus
+}
+
+// whole-feeder results from the areas': loss summed, extremes folded, status = worst
+__global__ void fold_results_kernel(int B, const double *__restrict__ loss, const double *__restrict__ vmin,
+                                    const double *__restrict__ vmax, const int8_t *__restrict__ status, int first,
+                                    double *__restrict__ o_loss, double *__restrict__ o_vmin, double *__restrict__ o_vmax,
+                                    int8_t *__restrict__ o_status) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    if (first) {
+        o_loss[s] = loss[s];
+        o_vmin[s] = vmin[s];
+        o_vmax[s] = vmax[s];
+        o_status[s] = status[s];
+    } else {
+        o_loss[s] += loss[s];
+        o_vmin[s] = fmin(o_vmin[s], vmin[s]);
+        o_vmax[s] = fmax(o_vmax[s], vmax[s]);
+        o_status[s] = o_status[s] > status[s] ? o_status[s] : status[s];
+    }
+}
+
+__global__ void max_kernel(const double *__restrict__ x, int n, double *__restrict__ out) {
+    __shared__ double sh[256];
+    double m = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) m = fmax(m, x[i]);
+    sh[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sh[0];
+}
+
+inline dim3 grid(int B, int y) { return dim3((unsigned)((B + 255) / 256), (unsigned)y); }
+}  // namespace
+
+hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, int nl, int B, double *dst,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(gather_rows_kernel, grid(B, 6 * nl), dim3(256), 0, st, src, nl_src, row, nl, B, dst);
+    return hipGetLastError();
+}
+hipError_t areas_add_row(double *work, int nl, int lrow, int B, const double *add, hipStream_t st) {
+    hipLaunchKernelGGL(add_row_kernel, grid(B, 6), dim3(256), 0, st, work, nl, lrow, B, add);
+    return hipGetLastError();
+}
+hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(gather_vsrc_kernel, grid(B, 1), dim3(256), 0, st, v_re, v_im, nn, lb, B, vsrc, diff);
+    return hipGetLastError();
+}
+hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
+                               hipStream_t st) {
+    if (nn - k0 <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_nodes_kernel, grid(B, 3 * (nn - k0)), dim3(256), 0, st, src, nn, k0, mono, nn_dst, B, dst);
+    return hipGetLastError();
+}
+hipError_t areas_fold_results(int B, const double *loss, const double *vmin, const double *vmax, const int8_t *status,
+                              int first, double *o_loss, double *o_vmin, double *o_vmax, int8_t *o_status,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(fold_results_kernel, grid(B, 1), dim3(256), 0, st, B, loss, vmin, vmax, status, first, o_loss,
+                       o_vmin, o_vmax, o_status);
+    return hipGetLastError();
+}
+hipError_t areas_max(const double *x, int n, double *out, hipStream_t st) {
+    hipLaunchKernelGGL(max_kernel, dim3(1), dim3(256), 0, st, x, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace fpf

@@ -14,6 +14,8 @@ using __hip_internal::uint32_t;
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/freedm_pf.h"
+
 #include <array>
 #include <string>
 #include <vector>
@@ -151,9 +153,22 @@ struct OutDev {
     double *agg;
     double *partials;        // [grid][8]
     unsigned *ticket;        // arrival counter, 0 between launches
+    // wave kernel only (the multi-area solve, fpf_areas.cpp): per-scenario
+    // source voltage [6][B] (re/im per phase) in place of V0, and the power
+    // entering at the source [6][B] = PQb row 0 (P1 Q1 P2 Q2 P3 Q3, kW / kVAr)
+    const double *vsrc;
+    double *s_in;
 };
 
 #ifndef __HIPCC_RTC__
+}  // namespace fpf
+struct fpf_feeder;
+namespace fpf {
+int ctx_device(const fpf_ctx *ctx);   // the HIP device of a context
+// fpf_solve_batch_device with the wave kernel's two extra per-scenario arrays
+// (OutDev::vsrc, OutDev::s_in; both device memory, may be NULL)
+int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
+                          void *stream, const double *d_vsrc, double *d_s_in);
 // launchers (fpf_generic.hip, fpf_tiled.hip, fpf_rtc.cpp)
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st);

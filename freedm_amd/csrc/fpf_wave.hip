@@ -359,7 +359,13 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     // per-scenario results for the workgroup aggregate: [sc][loss, vmin, vmax, status]
     __shared__ double res[SPB][4];
 
-    const cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+    // the source voltage: V0 (DPF_return7.cpp:84-89), or this scenario's when the
+    // caller supplies one (an area of the multi-area solve, fed from its boundary bus)
+    cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+    if (o.vsrc && live) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) v0[p] = mk(o.vsrc[(size_t)(2 * p) * B + s], o.vsrc[(size_t)(2 * p + 1) * B + s]);
+    }
     cx v[C][3];
 #pragma unroll
     for (int c = 0; c < C; ++c)
@@ -583,6 +589,11 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     // substation row 0: V0, Ib(0) = this sweep's total, no load
                     stx(SL, p * nn + 0, v0[p]);
                     if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0[p], mk(0, 0), ibo[p]);
+                    if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
+                        const cx sb = cmul(cmul(v0[p], mk(f.s3, 0.0)), cconj(ibo[p]));
+                        o.s_in[(size_t)(2 * p) * B + s] = sb.re;
+                        o.s_in[(size_t)(2 * p + 1) * B + s] = sb.im;
+                    }
                     const double m2 = fma(v0[p].re, v0[p].re, v0[p].im * v0[p].im);
                     mn = fmin(mn, m2);
                     mx = fmax(mx, m2);

@@ -21,7 +21,7 @@ import numpy as np
 from . import _lib
 from .feeder import Feeder
 
-__all__ = ["PowerFlow", "MultiPowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError"]
+__all__ = ["PowerFlow", "MultiPowerFlow", "AreaPowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError"]
 
 
 class DPFError(RuntimeError):
@@ -324,6 +324,69 @@ class MultiPowerFlow:
             raise DPFError(rc, L.fpf_multi_last_error(self.h).decode())
         r["n_nonconv"] = rc
         r["aggregate"] = agg.as_dict()
+        return r
+
+
+class AreaPowerFlow:
+    """The multi-area solve (fpf_areas_*, BASELINE config 5): the feeder split
+    into areas (node_area[k] = area of bus k), each solved as its own feeder
+    fed from its boundary bus, boundary voltages and source powers exchanged
+    until they settle.  eps / mxitr are the areas' inner convergence test."""
+
+    def __init__(self, feeder: Feeder, node_area, device: int = 0, eps: float = 1e-12, mxitr: int = 200, **opts):
+        L = _lib.load()
+        self.feeder = feeder
+        self.ctx = _Ctx.get(device)
+        o = _lib.default_opts(kernel="wave", eps=eps, mxitr=mxitr, **opts)
+        dl = np.asfortranarray(feeder.Dl, dtype=np.float64)
+        Z = np.asarray(feeder.Z, dtype=np.complex128)
+        zbuf = np.zeros(max(2 * Z.size, 2))
+        zbuf[0:2 * Z.size:2] = Z.real.ravel(order="F")
+        zbuf[1:2 * Z.size:2] = Z.imag.ravel(order="F")
+        na = np.ascontiguousarray(node_area, dtype=np.int32)
+        h = C.c_void_p()
+        rc = L.fpf_areas_create(self.ctx.h, dl.ctypes.data_as(_lib._dp), dl.shape[0], dl.shape[1],
+                                zbuf.ctypes.data_as(_lib._dp), Z.shape[0], Z.shape[1],
+                                na.ctypes.data_as(C.POINTER(C.c_int)), na.size, C.byref(o), C.byref(h))
+        if rc:
+            raise DPFError(rc, f"fpf_areas_create failed: {self.ctx.err()}")
+        self.h = h
+        self.nl, self.nn = dl.shape[0], na.size
+        n = C.c_int()
+        L.fpf_areas_info(h, C.byref(n), None, None)
+        nodes, parent = (C.c_int * n.value)(), (C.c_int * n.value)()
+        L.fpf_areas_info(h, C.byref(n), nodes, parent)
+        self.area_nodes, self.area_parent = list(nodes), list(parent)
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            _lib.load().fpf_areas_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, pq: np.ndarray, tol: float = 1e-12, max_outer: int = 100) -> dict:
+        L = _lib.load()
+        pq = np.ascontiguousarray(pq, dtype=np.float64)
+        if pq.ndim != 3 or pq.shape[:2] != (6, self.nl):
+            raise ValueError(f"pq must be [6][{self.nl}][B]")
+        B, nn = pq.shape[2], self.nn
+        r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
+             "vmin": np.zeros(B), "vmax": np.zeros(B), "V_re": np.zeros((3, nn, B)), "V_im": np.zeros((3, nn, B))}
+        out = _lib.FpfOutputs(None, None, None, _ptr(r["V_re"]), _ptr(r["V_im"]), _ptr(r["iters"]), _ptr(r["status"]),
+                              _ptr(r["loss"]), _ptr(r["vmin"]), _ptr(r["vmax"]))
+        agg = _lib.FpfAggregate()
+        rc = L.fpf_areas_solve(self.h, B, pq.ctypes.data_as(_lib._dp), float(tol), int(max_outer), C.byref(out),
+                               C.byref(agg))
+        if rc < 0:
+            raise DPFError(rc, L.fpf_areas_last_error(self.h).decode())
+        r["n_nonconv"] = rc
+        r["aggregate"] = agg.as_dict()
+        r["note"] = L.fpf_areas_last_error(self.h).decode()
         return r
 
 

@@ -327,3 +327,55 @@ def hosting_loads(feeder: Feeder, scen_idx: np.ndarray, seed: int = 1 << 20,
         out[2 * p] = np.where(live, P, 0.0)
         out[2 * p + 1] = np.where(live, Q, 0.0)
     return np.ascontiguousarray(out)
+
+
+# --------------------------------------------------------------------------- feeder areas (config 5)
+
+# The master VVC's SST map on the demo feeder (Broker/src/vvc/VoltVarCtrl.cpp:442-1135):
+# SST1..SST4 -> Dl rows 1..4, SST5 -> row 8, SST6 -> row 7, SST7 -> row 6; and
+# the slave DGI owning each SST (Broker_s1..s3/src/vvc/VoltVarCtrl.cpp:327-395):
+# s1 = SST2-4, s2 = SST1, s3 = SST5-7.
+SST_ROW = {1: 1, 2: 2, 3: 3, 4: 4, 5: 8, 6: 7, 7: 6}
+SST_OWNER = {1: "s2", 2: "s1", 3: "s1", 4: "s1", 5: "s3", 6: "s3", 7: "s3"}
+AREA_OF_BROKER = {"s2": 0, "s1": 1, "s3": 2}   # s2 holds SST1, next to the substation: the root area
+
+
+def sst_node_areas(feeder: Feeder) -> np.ndarray:
+    """node_area for the multi-area solve of the demo feeder by SST ownership:
+    every SST's bus (the receiving bus of its Dl row) goes to its slave's area;
+    a bus without an SST (bus 1, the substation transformer's secondary) joins
+    the area of its parent, else the root."""
+    Dl = feeder.Dl
+    nn = int((Dl[:, 0] != 0).sum()) + 1
+    area = np.full(nn, -1, dtype=np.int32)
+    for sst, row in SST_ROW.items():
+        area[int(Dl[row, 2])] = AREA_OF_BROKER[SST_OWNER[sst]]
+    par = np.zeros(nn, dtype=np.int64)
+    for m in range(Dl.shape[0]):
+        if Dl[m, 0] != 0:
+            par[int(Dl[m, 2])] = 0 if m == 0 else int(Dl[m, 1])
+    for k in range(1, nn):
+        if area[k] < 0:
+            area[k] = area[par[k]] if par[k] > 0 and area[par[k]] >= 0 else 0
+    area[0] = 0
+    return area
+
+
+def subtree_node_areas(feeder: Feeder, tops) -> np.ndarray:
+    """node_area with area 0 the whole feeder except the subtrees under the
+    buses `tops` (area i + 1 for tops[i]; a later top nested in an earlier
+    subtree takes its own part)."""
+    Dl = feeder.Dl
+    nn = int((Dl[:, 0] != 0).sum()) + 1
+    kids = [[] for _ in range(nn)]
+    for m in range(Dl.shape[0]):
+        if Dl[m, 0] != 0:
+            kids[0 if m == 0 else int(Dl[m, 1])].append(int(Dl[m, 2]))
+    area = np.zeros(nn, dtype=np.int32)
+    for i, t in enumerate(tops):
+        st = [int(t)]
+        while st:
+            k = st.pop()
+            area[k] = i + 1
+            st.extend(kids[k])
+    return area

@@ -196,6 +196,30 @@ int         fpf_multi_shard(int rank, int n_gpus, long n_total, long *lo, long *
  * sums of fields 0 and 3..7, min of vmin, max of vmax; n = 0 gives the identity. */
 void        fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate *out);
 
+/* ---- Multi-area solve (BASELINE config 5, the Broker_s1..s3 areas;
+ * Broker_s1/src/vvc/VoltVarCtrl.cpp:327-395).  node_area[k] (k = 1..nn-1;
+ * node_area[0] ignored) assigns every bus to an area; each area must be a
+ * connected subtree, the area of bus 1 is the root.  Every area is solved as
+ * its own feeder fed from its boundary bus (fast mode, wave kernel, the
+ * opts' eps / mxitr), parents first, children's source power added to their
+ * boundary bus as a load, until no boundary voltage moves by more than tol
+ * (p.u.) or max_outer outer iterations.  This algorithm has no reference
+ * counterpart: at its fixed point V is the monolithic solution (to the
+ * solver tolerances).  out (host): v_re / v_im in the feeder's numbering,
+ * iters = outer iterations, status, loss (sum of the areas' branch losses),
+ * vmin / vmax; vpolar / pqb / pql must be NULL.  fpf_areas_last_error also
+ * reports the last outer iteration's largest boundary move. */
+typedef struct fpf_areas fpf_areas;
+int         fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncols,
+                             const double *z, int z_rows, int z_cols,
+                             const int *node_area, int nn, const fpf_opts *opts,
+                             fpf_areas **out);
+void        fpf_areas_destroy(fpf_areas *a);
+const char *fpf_areas_last_error(const fpf_areas *a);
+int         fpf_areas_info(const fpf_areas *a, int *n_areas, int *area_nodes, int *area_parent);
+int         fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, double tol, int max_outer,
+                            const fpf_outputs *out, fpf_aggregate *agg);
+
 /* Diagnostics (no device needed): the hipRTC source fpf_feeder_create would
  * compile for this feeder's tiled kernel.  Writes at most buf_size bytes
  * (NUL-terminated) and returns the full size including the NUL, or FPF_ERR_*. */
