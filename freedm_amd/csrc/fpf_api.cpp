@@ -1321,6 +1321,7 @@ static hipError_t agg_after(fpf_feeder *f, hipStream_t st) {
 
 // the options the feeder was created with (fpf_vvc.cpp)
 double fpf_feeder_bkva(const fpf_feeder *f) { return f->opts.bkva; }
+double fpf_feeder_bkv(const fpf_feeder *f) { return f->opts.bkv; }
 
 extern "C" int fpf_feeder_get_info(const fpf_feeder *f, fpf_feeder_info *info) {
     if (!f || !info) return FPF_ERR_ARG;

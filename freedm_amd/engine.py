@@ -248,6 +248,61 @@ class PowerFlow:
         r.update(stop=res.stop, reverse=res.reverse, first_nonconv=res.first_nonconv, n_nonconv=rc)
         return r
 
+    # ------------------------------------------------------------------ VVC gradient / round
+    def _zbuf(self):
+        Z = np.asarray(self.feeder.Z, dtype=np.complex128)
+        zbuf = np.zeros(max(2 * Z.size, 2))
+        zbuf[0:2 * Z.size:2] = Z.real.ravel(order="F")
+        zbuf[1:2 * Z.size:2] = Z.imag.ravel(order="F")
+        return zbuf, Z.shape
+
+    def vvc_gradient(self, ctrl_dl: np.ndarray, beta0: float = 0.1) -> dict:
+        """fpf_vvc_gradient (VoltVarCtrl.cpp:1141-1325): the loss gradient with
+        respect to the SST Q injections at the control ctrl_dl."""
+        L = _lib.load()
+        ctrl = np.asfortranarray(ctrl_dl, dtype=np.float64)
+        zbuf, zs = self._zbuf()
+        ld = ctrl.shape[0]
+        g, nodes, st = np.zeros((3, ld)), np.zeros((3, ld)), np.zeros(8)
+        n = (C.c_int * 3)()
+        rc = L.fpf_vvc_gradient(self.h, ctrl.ctypes.data_as(_lib._dp), ctrl.shape[0], ctrl.shape[1],
+                                zbuf.ctypes.data_as(_lib._dp), zs[0], zs[1], float(beta0), ld,
+                                g.ctypes.data_as(_lib._dp), nodes.ctypes.data_as(_lib._dp), n,
+                                st.ctypes.data_as(_lib._dp))
+        if rc:
+            raise DPFError(rc, self.ctx.err())
+        return {"g": [g[x, :n[x]].copy() for x in range(3)], "load_nodes": [nodes[x, :n[x]].copy() for x in range(3)],
+                "gmin": st[0], "gmax": st[1], "gabs_min": st[2], "c0": st[3], "ploss_orig": st[4],
+                "vmin_orig": st[5], "vmax_orig": st[6], "iters": int(st[7])}
+
+    def vvc_round(self, ctrl_dl: np.ndarray, beta0: float = 0.1, alpha: float = 1.1, m_max: int = 100) -> dict:
+        """fpf_vvc_round: one VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762) --
+        gradient, batched step-size search, reversal -- and the control after it."""
+        L = _lib.load()
+        ctrl = np.asfortranarray(ctrl_dl, dtype=np.float64)
+        zbuf, zs = self._zbuf()
+        ld = ctrl.shape[0]
+        g, nodes = np.zeros((3, ld)), np.zeros((3, ld))
+        n = (C.c_int * 3)()
+        lf, lr = np.full(m_max + 1, np.nan), np.full(m_max + 1, np.nan)
+        out = np.zeros_like(ctrl, order="F")
+        res = np.zeros(13)
+        rc = L.fpf_vvc_round(self.h, ctrl.ctypes.data_as(_lib._dp), ctrl.shape[0], ctrl.shape[1],
+                             zbuf.ctypes.data_as(_lib._dp), zs[0], zs[1], float(beta0), float(alpha), int(m_max), ld,
+                             g.ctypes.data_as(_lib._dp), nodes.ctypes.data_as(_lib._dp), n,
+                             lf.ctypes.data_as(_lib._dp), lr.ctypes.data_as(_lib._dp), out.ctypes.data_as(_lib._dp),
+                             res.ctypes.data_as(_lib._dp))
+        if rc < 0:
+            raise DPFError(rc, self.ctx.err())
+        keys = ["ploss_orig", "vmin_orig", "vmax_orig", "c0", "stop_fwd", "stop_rev", "reversed", "sent",
+                "ploss_after", "gmin", "gmax", "gabs_min", "nonconv"]
+        r = {k: float(v) for k, v in zip(keys, res)}
+        for k in ("stop_fwd", "stop_rev", "reversed", "sent", "nonconv"):
+            r[k] = int(r[k])
+        r.update(g=[g[x, :n[x]].copy() for x in range(3)], load_nodes=[nodes[x, :n[x]].copy() for x in range(3)],
+                 loss_fwd=lf, loss_rev=lr, Dl=out)
+        return r
+
     # ------------------------------------------------------------------ reference call
     def dpf_return7(self, Dl: np.ndarray) -> VPQ:
         Dl = np.asarray(Dl, dtype=np.float64)

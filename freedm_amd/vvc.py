@@ -40,3 +40,14 @@ def step_size0(g, bkva: float = 1000.0, beta0: float = BETA0) -> float:
     """c0 = beta0 / (bkva/3) / min over all phases of |g| (:1316-1323)."""
     gabs_min = min(float(np.min(np.abs(np.asarray(x)))) for x in g if len(x))
     return beta0 / (bkva / 3) / gabs_min
+
+
+# The 21 SST set-points of the master's Gradient message (VoltVarCtrl.cpp:1504-1506):
+# Q of Dl rows 1, 2, 3, 4, 6, 7, 8 (SST1..4, SST7, SST6, SST5), phase a, then b, then c
+S2_ROWS = (1, 2, 3, 4, 6, 7, 8)
+
+
+def s2_setpoints(Dl: np.ndarray) -> np.ndarray:
+    """S2 of the Gradient message sent to the slaves (:1504-1508), 21 values (kVAr)."""
+    Dl = np.asarray(Dl, dtype=np.float64)
+    return np.array([Dl[r, c] for c in (7, 9, 11) for r in S2_ROWS])

@@ -271,6 +271,34 @@ int         fpf_vvc_line_search(fpf_feeder *feeder, const double *ctrl_dl, int n
                                 double c0, double alpha, int m_max, double ploss_orig,
                                 fpf_line_search *res);
 
+/* The VVC gradient (VoltVarCtrl.cpp:1141-1325): one DPF of ctrl_dl on the
+ * device, then on the host, per phase: the self-impedance admittance matrix
+ * (form_Yabc.cpp), V_abc_list, rename_brn, dF/dtheta, dF/dV and the Jacobian
+ * (form_Ftheta.cpp, form_Fv.cpp, form_J.cpp; long double sums as the
+ * reference), lambda = -inv(J^T) Fx and g_vq = -gu^T lambda.  z is the
+ * feeder's Z (fpf_feeder_create's layout).  g, load_nodes: [3][ld] (phase
+ * major), n_loads[3] = Lla/Llb/Llc; stats[8] (may be NULL) = gmin, gmax,
+ * gabs_min, c0 = beta0/(bkva/3)/gabs_min, Ploss_orig, Vmin_orig, Vmax_orig,
+ * sweeps of the base solve.  Returns FPF_OK or FPF_ERR_* (FPF_ERR_UNSUPPORTED:
+ * the base solve did not converge -- the reference throws). */
+int         fpf_vvc_gradient(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
+                             const double *z, int z_rows, int z_cols, double beta0, int ld,
+                             double *g, double *load_nodes, int *n_loads, double *stats);
+
+/* One whole VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762): the gradient,
+ * the step-size search as one batch (fpf_vvc_line_search), and the reversed
+ * search when the reference reverses.  loss_fwd / loss_rev [m_max + 1] (loss_rev
+ * may be NULL), dl_out (nl x ncols): the control after the round (the kept
+ * candidate, Dl = Dl_osize, :1486/1707; else ctrl_dl).  res[13] = Ploss_orig,
+ * Vmin_orig, Vmax_orig, c0, stop_fwd, stop_rev, reversed, sent (the S2
+ * set-points go to the slaves, :1495/1716), Ploss_after, gmin, gmax,
+ * gabs_min, nonconverged (a candidate the reference solves did not converge:
+ * it throws).  Returns 0, 1 (nonconverged) or FPF_ERR_*. */
+int         fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
+                          const double *z, int z_rows, int z_cols, double beta0, double alpha,
+                          int m_max, int ld, double *g, double *load_nodes, int *n_loads,
+                          double *loss_fwd, double *loss_rev, double *dl_out, double *res);
+
 /* Diagnostics: on-device check, over n seeded operand sets, that the
  * shared-reciprocal division the tiled kernel uses gives the same bits as the
  * compiler's a / b and as the libgcc __divdc3 complex division.  Returns the

@@ -166,3 +166,61 @@ def dpf_batch(Dl, Z, pq, opts: RefOpts | None = None, nthreads: int = 1, want_fu
                          _dp(out["loss"]), _dp(out["vmin"]), _dp(out["vmax"]), nthreads)
     out["rc"] = rc
     return out
+
+
+def vvc_gradient(Dl, Z, Vpolar, beta0: float = 0.1, bkva: float = 1000.0, bkv: float = 12.47) -> dict:
+    """The VVC gradient (ref_vvc.c: VoltVarCtrl.cpp:1141-1325) at a DPF result."""
+    L = lib()
+    L.ref_vvc_gradient.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int,
+                                   C.POINTER(C.c_double), C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
+                                   C.POINTER(C.c_double)]
+    dl = _fortran(Dl)
+    zb, zshape = _zbuf(Z)
+    zb = np.ascontiguousarray(zb)
+    vp = np.asfortranarray(np.asarray(Vpolar, dtype=np.float64))
+    ld = dl.shape[0]
+    g = np.zeros((3, ld))
+    nodes = np.zeros((3, ld))
+    nload = (C.c_int * 3)()
+    stats = np.zeros(4)
+    rc = L.ref_vvc_gradient(_dp(dl), dl.shape[0], dl.shape[1], _dp(zb), zshape[0], zshape[1], _dp(vp), vp.shape[0],
+                            bkva, bkv, beta0, ld, _dp(g), _dp(nodes), nload, _dp(stats))
+    if rc:
+        raise ValueError(f"ref_vvc_gradient failed ({rc})")
+    n = list(nload)
+    return {"g": [g[x, :n[x]].copy() for x in range(3)], "load_nodes": [nodes[x, :n[x]].copy() for x in range(3)],
+            "gmin": stats[0], "gmax": stats[1], "gabs_min": stats[2], "c0": stats[3]}
+
+
+def vvc_main(Dl, Z, beta0: float = 0.1, alpha: float = 1.1, m_max: int = 100, opts: RefOpts | None = None) -> dict:
+    """vvc_main's numerics, sequentially as the reference (ref_vvc.c,
+    VoltVarCtrl.cpp:1141-1762): base solve, gradient, step-size search, reversal."""
+    L = lib()
+    L.ref_vvc_main.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int,
+                               C.POINTER(RefOpts), C.c_double, C.c_double, C.c_int, C.c_int, C.POINTER(C.c_double),
+                               C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                               C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    dl = _fortran(Dl)
+    zb, zshape = _zbuf(Z)
+    zb = np.ascontiguousarray(zb)
+    ld = dl.shape[0]
+    g = np.zeros((3, ld))
+    nodes = np.zeros((3, ld))
+    nload = (C.c_int * 3)()
+    lf = np.full(m_max, np.nan)
+    lr = np.full(m_max, np.nan)
+    out = np.zeros_like(dl, order="F")
+    res = np.zeros(13)
+    o = opts if opts is not None else default_opts()
+    rc = L.ref_vvc_main(_dp(dl), dl.shape[0], dl.shape[1], _dp(zb), zshape[0], zshape[1], C.byref(o), beta0, alpha,
+                        m_max, ld, _dp(g), _dp(nodes), nload, _dp(lf), _dp(lr), _dp(out), _dp(res))
+    n = list(nload)
+    keys = ["ploss_orig", "vmin_orig", "vmax_orig", "c0", "stop_fwd", "stop_rev", "reversed", "sent", "ploss_after",
+            "gmin", "gmax", "gabs_min", "calls"]
+    r = {k: float(v) for k, v in zip(keys, res)}
+    for k in ("stop_fwd", "stop_rev", "reversed", "sent", "calls"):
+        r[k] = int(r[k])
+    r.update(rc=rc, g=[g[x, :n[x]].copy() for x in range(3)], load_nodes=[nodes[x, :n[x]].copy() for x in range(3)],
+             loss_fwd=lf, loss_rev=lr, Dl=out)
+    return r

@@ -92,6 +92,22 @@ int ref_dpf_batch(const double *dl, int nl, int ncols,
                   double *loss, double *vmin, double *vmax,
                   int nthreads);
 
+/* ---- the VVC round (ref_vvc.c) ----
+ * Gradient of the loss w.r.t. the SST Q injections (VoltVarCtrl.cpp:1141-1325)
+ * at the DPF result vpolar (nn x 6) of dl.  g, load_nodes: [3][ld];
+ * n_loads[3]; stats[4] = gmin, gmax, gabs_min, cvq (the first step size).
+ * Returns 0 or REF_BAD_INPUT. */
+int ref_vvc_gradient(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+                     const double *vpolar, int nn, double bkva, double bkv, double beta0, int ld,
+                     double *g, double *load_nodes, int *n_loads, double *stats);
+
+/* vvc_main's numerics, sequential as the reference (VoltVarCtrl.cpp:1141-1762):
+ * res[13] = ploss_orig, vmin_orig, vmax_orig, c0, stop_fwd, stop_rev, reversed,
+ * sent, ploss_after, gmin, gmax, gabs_min, DPF calls. */
+int ref_vvc_main(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols, const ref_opts *o,
+                 double beta0, double alpha, int m_max, int ld, double *g, double *load_nodes, int *n_loads,
+                 double *loss_fwd, double *loss_rev, double *dl_out, double *res);
+
 #ifdef __cplusplus
 }
 #endif
