@@ -142,17 +142,51 @@ def _cpu_model():
     return "unknown"
 
 
-def _pmc_traffic():
-    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3
-    --pmc summary (profiles/pmc_traffic.json), or None."""
+def _pmc_traffic(workload: str):
+    """Per-launch HBM bytes of the dominant kernel for `workload` ("123-bus x
+    4096") from the committed rocprofv3 --pmc summaries
+    (profiles/pmc_traffic.json, tools/pmc_summary.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        if d.get("workload") == f"{FEEDER_NODES}-bus x {SCEN_PER_GPU}":
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
+        e = d.get("by_workload", {}).get(workload)
+        if e is None and d.get("workload") == workload:
+            e = d
+        return e.get("hbm_bytes_per_launch") if e else None
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
+def _loads_on_device(torch, dev, loads, feeder, ids, seed, chunk=8192):
+    """[6][Nl][len(ids)] scenario loads of the global ids, generated on the host
+    in chunks, scenario-fastest on the device."""
+    out = torch.empty((6, feeder.nl, len(ids)), dtype=torch.float64, device=dev)
+    for a in range(0, len(ids), chunk):
+        b = min(len(ids), a + chunk)
+        out[:, :, a:b] = torch.from_numpy(loads(feeder, ids[a:b], seed=seed)).to(dev)
+    return out
+
+
+def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
+    """Average launch time (HIP events on the launch stream) of `steps`
+    back-to-back solves of the device batch d_pq, plus the iterations."""
+    out = {"iters": torch.zeros(B, dtype=torch.int32, device=dev), "status": torch.zeros(B, dtype=torch.int8, device=dev),
+           "loss": torch.zeros(B, dtype=torch.float64, device=dev), "vmin": torch.zeros(B, dtype=torch.float64, device=dev),
+           "vmax": torch.zeros(B, dtype=torch.float64, device=dev)}
+    if want_v:
+        out.update(v_re=torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
+                   v_im=torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev))
+    solve = pf.bind_device(d_pq, out, stream=stream)[0]
+    for _ in range(warmup):
+        solve()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        solve()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / steps, out
 
 
 def main():
@@ -171,6 +205,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-v-out", action="store_true", help="diagnostic: do not request the V outputs")
+    ap.add_argument("--in-batches", type=int, default=0,
+                    help="distinct input batches the steps cycle through (0: enough for > 256 MiB of inputs, so "
+                         "the Infinity Cache cannot hold them; 1: re-solve one batch)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the config-4 throughput leg of the config-2 run")
     args = ap.parse_args()
 
     import torch
@@ -197,12 +235,17 @@ def main():
     B = args.scenarios or b_cfg
     pf.reserve(B)
     from freedm_amd import dist as D
-    lo, hi = D.shard_range(rank, world, world * B)   # weak scaling: B global ids per GPU
-    # generated in chunks of 8192 scenarios (host memory), scenario-fastest on the GPU
-    d_pq = torch.empty((6, feeder.nl, B), dtype=torch.float64, device=dev)
-    for c in range(lo, hi, 8192):
-        e = min(hi, c + 8192)
-        d_pq[:, :, c - lo:e - lo] = torch.from_numpy(loads(feeder, np.arange(c, e), seed=s_seed)).to(dev)
+    # the steps cycle through n_in distinct input batches (together more than the
+    # 256 MiB Infinity Cache, so every step streams its loads from HBM); weak
+    # scaling: rank r's batch b holds global ids (b * world + r) * B ... + B
+    batch_bytes = 48 * feeder.nl * B
+    n_in = args.in_batches or max(1, min(64, -(-300 * 2 ** 20 // batch_bytes)))
+    n_in = min(n_in, max(args.steps, 1))
+    d_pqs = []
+    for b in range(n_in):
+        lo, hi = D.shard_range(rank, world, world * B)
+        ids = np.arange(lo, hi) + b * world * B
+        d_pqs.append(_loads_on_device(torch, dev, loads, feeder, ids, s_seed))
     # per-scenario outputs of every timed step (the study's results); V is
     # overwritten step after step
     K = max(args.steps, 1)
@@ -214,7 +257,7 @@ def main():
     v_out = {} if args.no_v_out else {"v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
                                       "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
     stream = torch.cuda.current_stream(dev)
-    solves = [pf.bind_device(d_pq, dict(v_out, **{k: t[i] for k, t in res.items()}), stream=stream)[0]
+    solves = [pf.bind_device(d_pqs[i % n_in], dict(v_out, **{k: t[i] for k, t in res.items()}), stream=stream)[0]
               for i in range(K)]
     flat = {k: t.view(-1) for k, t in res.items()}
     agg = torch.zeros(8, dtype=torch.float64, device=dev)
@@ -272,7 +315,7 @@ def main():
     else:
         bytes_launch = bpa * B
     achieved = bytes_launch / avg_kern_s / 1e9
-    traffic = _pmc_traffic() if (args.config == 2 and B == SCEN_PER_GPU) else None
+    traffic = _pmc_traffic(f"{n_nodes}-bus x {B}")
     # algorithmic fp64 flops per scenario = 123 Nb k_s + 60 Nn, over
     # the timed launches, against the 78.6 TFLOP/s fp64 vector peak
     flops = 123.0 * nb * k_sum + 60.0 * nn * B * args.steps
@@ -294,6 +337,7 @@ def main():
             "data": f"synthetic (seeded {n_nodes}-bus radial feeder + seeded {model} load/PV scenarios)",
             "config": {"workload": f"BASELINE config {args.config}: {n_nodes}-bus feeder, {B} scenarios per GPU per step",
                        "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
+                       "input_batches": n_in, "input_mib": n_in * batch_bytes / 2 ** 20,
                        "tile": pf.info["tile"], "specialized": pf.info["specialized"], "exact": bool(args.exact),
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -310,6 +354,23 @@ def main():
             "converged_per_step_rank0": conv_per_step,
             "host_submit_ms_per_step": t_submit / args.steps * 1e3,
         }
+        if world == 1 and args.config == 2 and not args.no_c4 and not args.nodes and not args.scenarios:
+            # the throughput-sized roofline next to the bench line (BASELINE config 4:
+            # one GPU's 131 072-scenario shard of the hosting study, 843 MB of inputs)
+            n4, s4, b4, seed4, m4 = CONFIGS[4]
+            ids4 = np.arange(b4)
+            d4 = _loads_on_device(torch, dev, hosting_loads, feeder, ids4, seed4)
+            pf.reserve(b4)
+            ms4, o4 = _kernel_ms(torch, pf, d4, b4, 5, 2, stream, dev)
+            conv4 = int((o4["status"] == 0).sum().item())
+            ach4 = bpa * b4 / (ms4 / 1e3) / 1e9
+            res["roofline_config4"] = {
+                "workload": f"BASELINE config 4: {n4}-bus feeder, {b4} hosting scenarios per GPU per launch",
+                "bound": "hbm", "achieved": ach4, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach4 / HBM_PEAK_GBS,
+                "traffic": _pmc_traffic(f"{n4}-bus x {b4}"), "kernel_ms": ms4, "bytes_alg_per_scenario": bpa,
+                "converged_scenarios_per_s": conv4 / (ms4 / 1e3),
+                "mean_sweeps": float(o4["iters"].double().mean().item())}
+            del d4
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
             res["cpu_baseline"] = cb
