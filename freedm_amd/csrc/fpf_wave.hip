@@ -263,9 +263,10 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     int *const knode = pairs + pair_n;                                // [C][L] node of each slot
     double2 *const reg0 = (double2 *)(knode + C * L);                 // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
-    const int RS = (3 * C * L + 3 * XC + noff) | 1;                  // double2 per region (odd: V read-out banks)
+    const int RS = (3 * C * L + 3 * XC + noff + 3) | 1;              // double2 per region (odd: V read-out banks)
     double2 *const SL = reg0 + sc * RS;
     double2 *const X = SL + 3 * C * L;
+    double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
     // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
     // pair read of the scenario precedes the offset stores in its one wave's
     // program order), else after X
@@ -328,13 +329,13 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     __syncthreads();
     WSTAMP(1);
     if (DBG(8192)) return;
-    // this lane's block chain (lane b < nblk resolves block b), padded with the zero entry
-    int bp[2 * WAVE_BD];
+    // this lane's block chain (lane b < nblk resolves block b), padded with the zero
+    // entry; the two indices of a pair packed in one register (XC < 2^16)
+    int bp[WAVE_BD];
 #pragma unroll
     for (int j = 0; j < WAVE_BD; ++j) {
         const bool ok = j < bdepth && li < nblk;
-        bp[2 * j] = ok ? pairs[(2 * j) * nblk + li] : XC - 1;
-        bp[2 * j + 1] = ok ? pairs[(2 * j + 1) * nblk + li] : XC - 1;
+        bp[j] = ok ? pairs[(2 * j) * nblk + li] | (pairs[(2 * j + 1) * nblk + li] << 16) : (XC - 1) | ((XC - 1) << 16);
     }
     const double inv_s3 = 1.0 / f.s3;
     double2 sld_in[C][3];
@@ -361,16 +362,19 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 
     // the source voltage: V0 (DPF_return7.cpp:84-89), or this scenario's when the
     // caller supplies one (an area of the multi-area solve, fed from its boundary bus)
-    cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
-    if (o.vsrc && live) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p) v0[p] = mk(o.vsrc[(size_t)(2 * p) * B + s], o.vsrc[(size_t)(2 * p + 1) * B + s]);
-    }
     cx v[C][3];
+    {
+        cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+        if (o.vsrc && live) {
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+            for (int p = 0; p < 3; ++p) v0[p] = mk(o.vsrc[(size_t)(2 * p) * B + s], o.vsrc[(size_t)(2 * p + 1) * B + s]);
+        }
+        if (li < 3) stx(V0S, li, li == 0 ? v0[0] : (li == 1 ? v0[1] : v0[2]));
 #pragma unroll
-        for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
+    }
 
     // A scenario's results are recorded in its last sweep (converged, or the
     // mxitr-th); its lanes then sweep along without storing until the wave's
@@ -474,6 +478,9 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                 g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
                 if (any_fin) lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
             }
+#ifdef FPF_WAVE_SB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -504,7 +511,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         // stored as V0 - off so that V = (V0 - off) - Ginc is one subtraction per
         // slot; the chain's index pairs sit in registers (bp), all its reads issue together
         if (DBG(8)) {
-            if (li < 3) X[li * XC] = make_double2(v0[li].re, v0[li].im);
+            if (li < 3) X[li * XC] = V0S[li];
         } else if (nblk <= L && bdepth <= WAVE_BD) {
             if (li < nblk) {
                 cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
@@ -513,11 +520,11 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     if (j < bdepth) {   // uniform
 #pragma unroll
                         for (int p = 0; p < 3; ++p)
-                            of[p] = cadd(of[p], csub(ldx(X, p * XC + bp[2 * j]), ldx(X, p * XC + bp[2 * j + 1])));
+                            of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
                     }
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(v0[p], of[p]));
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(ldx(V0S, p), of[p]));
             }
         } else {
             for (int b = li; b < nblk; b += L) {
@@ -528,7 +535,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(v0[p], of[p]));
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(ldx(V0S, p), of[p]));
             }
         }
         wfence();
@@ -576,33 +583,41 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         stx(SL, p * nn + k, v[c][p]);
-                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
-                        const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
-                        mn = fmin(mn, m2);
-                        mx = fmax(mx, m2);
+                        if (FULL) {
+                            emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                            const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
+                            mn = fmin(mn, m2);
+                            mx = fmax(mx, m2);
+                        }
                     }
                 }
             }
             if (li == L - 1) {   // the lane holding Ib(0)
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
+                    const cx v0p = ldx(V0S, p);
                     // substation row 0: V0, Ib(0) = this sweep's total, no load
-                    stx(SL, p * nn + 0, v0[p]);
-                    if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0[p], mk(0, 0), ibo[p]);
+                    stx(SL, p * nn + 0, v0p);
+                    if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0p, mk(0, 0), ibo[p]);
                     if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
-                        const cx sb = cmul(cmul(v0[p], mk(f.s3, 0.0)), cconj(ibo[p]));
+                        const cx sb = cmul(cmul(v0p, mk(f.s3, 0.0)), cconj(ibo[p]));
                         o.s_in[(size_t)(2 * p) * B + s] = sb.re;
                         o.s_in[(size_t)(2 * p + 1) * B + s] = sb.im;
                     }
-                    const double m2 = fma(v0[p].re, v0[p].re, v0[p].im * v0[p].im);
-                    mn = fmin(mn, m2);
-                    mx = fmax(mx, m2);
+                    if (FULL) {
+                        const double m2 = fma(v0p.re, v0p.re, v0p.im * v0p.im);
+                        mn = fmin(mn, m2);
+                        mx = fmax(mx, m2);
+                    }
                 }
             }
-            if (!FULL || !f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
+            if (!FULL) {
+                // light outputs: V is in the region; the extremes are taken from there
+                // after the loop (fewer registers live across the sweep loop)
+                x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
+            } else if (!f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
                 // every Lnum_p + 1 = Nn: V_abc_list keeps every row, so the extremes are
                 // plain min/max; loss = s3 sum Re(drop conj(Ib))
-                // (|V|^2 compared, one sqrt each at the end: sqrt is monotonic)
                 x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
                 mn = sqrt(seg_reduce_min<L>(mn));
                 mx = sqrt(seg_reduce_max<L>(mx));
@@ -619,7 +634,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                 sl = seg_incl<L>(sl);
                 x = 0.0;
 #pragma unroll
-                for (int p = 0; p < 3; ++p) x += cmul(cmul(v0[p], mk(f.s3, 0.0)), cconj(ibo[p])).re;
+                for (int p = 0; p < 3; ++p) x += cmul(cmul(ldx(V0S, p), mk(f.s3, 0.0)), cconj(ibo[p])).re;
                 x -= sl;
                 mn = INFINITY;
                 mx = -INFINITY;
@@ -647,14 +662,19 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                 mx = seg_reduce_max<L>(mx);
             }
             if (li == L - 1) {
-                if (o.iters) o.iters[s] = it + 1;
-                if (o.status) o.status[s] = conv ? 0 : 1;
-                if (o.loss) o.loss[s] = x;
-                if (o.vmin) o.vmin[s] = mn;
-                if (o.vmax) o.vmax[s] = mx;
+                // (the output addresses formed here, not kept in registers across the loop)
+                int sf = s;
+                __asm__ volatile("" : "+v"(sf));
+                if (o.iters) o.iters[sf] = it + 1;
+                if (o.status) o.status[sf] = conv ? 0 : 1;
+                if (o.loss) o.loss[sf] = x;
+                if (FULL) {
+                    if (o.vmin) o.vmin[s] = mn;
+                    if (o.vmax) o.vmax[s] = mx;
+                    res[sc][1] = mn;
+                    res[sc][2] = mx;
+                }
                 res[sc][0] = x;
-                res[sc][1] = mn;
-                res[sc][2] = mx;
                 res[sc][3] = conv ? 0.0 : 1.0;
             }
             wfence();
@@ -663,6 +683,29 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         WSTAMP(3 + it);
     }
     WSTAMP(40);
+    if (!FULL && live && !DBG(128)) {
+        // every Lnum_p + 1 = Nn (no zeroed phases): V_abc_list keeps every row, so
+        // Vmin/Vmax are the plain extremes of |V| over the scenario's V in its
+        // region (|V|^2 compared, one sqrt each: sqrt is monotonic)
+        double mn = INFINITY, mx = -INFINITY;
+        for (int k = li; k < nn; k += L) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx vv = ldx(SL, p * nn + k);
+                const double m2 = fma(vv.re, vv.re, vv.im * vv.im);
+                mn = fmin(mn, m2);
+                mx = fmax(mx, m2);
+            }
+        }
+        mn = sqrt(seg_reduce_min<L>(mn));
+        mx = sqrt(seg_reduce_max<L>(mx));
+        if (li == L - 1) {
+            if (o.vmin) o.vmin[s] = mn;
+            if (o.vmax) o.vmax[s] = mx;
+            res[sc][1] = mn;
+            res[sc][2] = mx;
+        }
+    }
 
     // ---- fused batch aggregate [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over,
     // n_under, n_scen] over converged scenarios: the workgroup's partial in
@@ -754,7 +797,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk)) | 1);
+    const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 3) | 1);
     const size_t stage = 8 * 6 * (size_t)w.nl * (spb + 1);           // the loads, staged over the regions
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
     const size_t temp = TEMP_IN_LDS ? 16 * (9 * (size_t)w.C * L) : 0;
