@@ -383,6 +383,7 @@ struct WaveHost {
     bool ok = false;
     std::string why;
     int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0, wpb = 0, off_in_x = 0;
+    int temp_sym = 0;
     int wpb_big_batch = 0;
     std::vector<int32_t> row, node, info, blk, mref, pairs;
     std::vector<double> temp;
@@ -579,6 +580,31 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
             w.temp[((j * C + c) * L + lane) * 2 + 1] = h.tz[(size_t)nd.fw * 18 + 2 * j + 1];
         }
     }
+    // TEMP of the form [[zs zm zm][zm zs zm][zm zm zs]] on every branch (the
+    // transposed lines and transformers of load_system_data's Z): the drop of
+    // phase a is (zs - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3), 2 complex per slot
+    // instead of 9 (fast mode only; the rounding differs by a few ulp)
+    bool sym = !getenv("FPF_WAVE_NO_SYM");
+    for (int q = 0; q < n && sym; ++q) {
+        const double *t = &h.tz[(size_t)h.node[at[q]].fw * 18];
+        for (int j = 0; j < 9 && sym; ++j) {
+            const int ref = (j % 4 == 0) ? 0 : 1;   // diagonal j = 0, 4, 8; off-diagonal j = 1
+            sym = t[2 * j] == t[2 * ref] && t[2 * j + 1] == t[2 * ref + 1];
+        }
+    }
+    if (sym) {
+        std::vector<double> ts(2 * S * 2, 0.0);
+        for (int q = 0; q < n; ++q) {
+            const int c = q % C, lane = q / C;
+            const double *t = &h.tz[(size_t)h.node[at[q]].fw * 18];
+            ts[((0 * C + c) * L + lane) * 2 + 0] = t[0] - t[2];
+            ts[((0 * C + c) * L + lane) * 2 + 1] = t[1] - t[3];
+            ts[((1 * C + c) * L + lane) * 2 + 0] = t[2];
+            ts[((1 * C + c) * L + lane) * 2 + 1] = t[3];
+        }
+        w.temp.swap(ts);
+    }
+    w.temp_sym = sym ? 1 : 0;
     w.n = n;
     w.spw = spw;
     w.C = C;
@@ -600,6 +626,7 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     probe.bdepth = bdepth;
     probe.ncomp = ncomp;
     probe.off_in_x = w.off_in_x;
+    probe.temp_sym = w.temp_sym;
     const int big = spw * C <= 2 ? 16 : 8, small = big / 2;
     auto lds_at = [&](int wpb) { probe.wpb = wpb; return wave_lds_bytes(probe); };
     // Measured (profiles/r02a, 123-bus): two 8-scenario workgroups per CU are
@@ -1204,6 +1231,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.has_mask = wh.has_mask;
         w.wpb = wh.wpb;
         w.off_in_x = wh.off_in_x;
+        w.temp_sym = wh.temp_sym;
         w.dbg = getenv("FPF_WAVE_DBG") ? atoi(getenv("FPF_WAVE_DBG")) : 0;
         w.mxitr = o.mxitr;
         for (int p = 0; p < 3; ++p) w.K[p] = d.K[p];

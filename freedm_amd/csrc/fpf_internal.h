@@ -129,6 +129,9 @@ struct WaveDev {
     int32_t dbg;             // diagnostic ablations (FPF_WAVE_DBG; results are wrong when set)
     int32_t wpb;             // wavefronts per workgroup (16, 8 or 4; fpf_api.cpp: analyse_wave)
     int32_t off_in_x;        // 1: block offsets stored over X's first nblk entries (nblk <= L, depth <= 4)
+    int32_t stag_lo, stag_hi, stag_n;   // workgroups [lo, hi) start stag_n x 8 k cycles late (diagnostic)
+    int32_t temp_sym;        // 1: every branch's TEMP is [[zs zm zm][zm zs zm][zm zm zs]] (transposed
+                             //    line / transformer): slot_temp holds (zs - zm, zm) per slot
     double V0[6], s3, eps, lb_v, ub_v;
     const int32_t *slot_row;    // [C][L] Dl row of the slot's node (-1: empty slot)
     const int32_t *slot_node;   // [C][L] node id
@@ -137,8 +140,8 @@ struct WaveDev {
                                 //        node (its gather), 22-30 forward index + 1 (its store)
     const int32_t *slot_blk;    // [C][L] block of the slot's node
     const int32_t *slot_mref;   // [3][C][L] forward index of the nearest zeroed proper ancestor, -1 none
-    const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch (read
-                                // from global memory: L1/L2-resident, 18 KB for 128 slots)
+    const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch, row-major
+                                // (l, a); temp_sym: [2][C][L] (zs - zm, zm)
     const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) forward indices; pad = ncomp (zero)
 };
 

@@ -61,13 +61,16 @@ namespace fpf {
 
 #ifdef FPF_STAMPS
 // diagnostic build only: lane 0 of each of the first 64 wavefronts records
-// s_memtime at stage boundaries (never read by the kernel itself)
+// s_memtime at stage boundaries (never read by the kernel itself): [64][128],
+// 0 entry, 1 staged, 2 Sld set up, 4 + 8 it + k inside sweep it < 12 (k = 0 top,
+// 1 backward scan, 2 Ib, 3 convergence, 4 drops, 5 forward scan + stores,
+// 6 block offsets, 7 V), 120 after the loop, 121 V written out
 __device__ unsigned long long *fpf_wave_stamp_buf = nullptr;
 #define WSTAMP(idx)                                                                                   \
     do {                                                                                              \
         const int gw_ = blockIdx.x * WPB + (threadIdx.x >> 6);                                         \
-        if (fpf_wave_stamp_buf && (threadIdx.x & 63) == 0 && gw_ < 64 && (idx) < 64)                   \
-            fpf_wave_stamp_buf[gw_ * 64 + (idx)] = __builtin_amdgcn_s_memtime();                        \
+        if (fpf_wave_stamp_buf && (threadIdx.x & 63) == 0 && gw_ < 64 && (idx) < 128)                  \
+            fpf_wave_stamp_buf[gw_ * 128 + (idx)] = __builtin_amdgcn_s_memtime();                       \
     } while (0)
 extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr) {
     unsigned long long *p = (unsigned long long *)dptr;
@@ -239,6 +242,13 @@ __device__ __forceinline__ double seg_reduce_min(double x) {
 template <int L>
 __device__ __forceinline__ double seg_reduce_max(double x) { return -seg_reduce_min<L>(-x); }
 
+// tile of block b: the first 8 * (G / 8) blocks are dealt so that blocks on one
+// XCD (b, b + 8, ...) take consecutive tiles; the remainder keeps b
+__device__ __forceinline__ int xcd_tile(int b, int G) {
+    const int per = G >> 3;
+    return b < (per << 3) ? (b & 7) * per + (b >> 3) : b;
+}
+
 template <int SPW, int C, bool FULL, int WPB>
 __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
@@ -246,19 +256,26 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     constexpr int NT = WPB * 64;
     extern __shared__ double2 lds[];
     if (DBG(4096)) return;
+    if ((int)blockIdx.x >= f.stag_lo && (int)blockIdx.x < f.stag_hi)
+        for (int i = 0; i < f.stag_n; ++i) __builtin_amdgcn_s_sleep(127);
     WSTAMP(0);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int seg = lane / L, li = lane % L;
     const int sc = wv * SPW + seg;                 // scenario within the workgroup
-    const int s0 = blockIdx.x * SPB, s = s0 + sc;
+    // XCD-aware tile order: blocks b and b + 8 share an XCD (and its L2), so they
+    // get neighbouring tiles -- the 128-byte rows two 8-scenario tiles share are
+    // fetched into one L2 (MI355X_MICROARCH.md, workgroup placement)
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int s0 = tile * SPB, s = s0 + sc;
     const int nsb = min(SPB, B - s0);              // scenarios of this workgroup
     const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
     // LDS: per workgroup the block-chain table (and, in a diagnostic build, the
     // TEMP blocks); per scenario Sld (later V in node order), the gathered scan
     // values X ([3][XC], entry XC-1 = 0; backward and forward entries share it)
     // and the block offsets
-    double2 *const tl = lds;                                          // [9][C][L] if TEMP_IN_LDS
-    int *const pairs = (int *)(tl + (TEMP_IN_LDS ? 9 * C * L : 0));   // [bdepth][2][nblk]
+    const int ntm = f.temp_sym ? 2 : 9;                               // TEMP entries per slot
+    double2 *const tl = lds;                                          // [ntm][C][L] if TEMP_IN_LDS
+    int *const pairs = (int *)(tl + (TEMP_IN_LDS ? ntm * C * L : 0)); // [bdepth][2][nblk]
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
     int *const knode = pairs + pair_n;                                // [C][L] node of each slot
     double2 *const reg0 = (double2 *)(knode + C * L);                 // per-scenario regions
@@ -288,6 +305,34 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         double *stage = (double *)reg0;   // [6][nl][SPB + 1]: the pad spreads a slot's rows over the banks
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
+        if ((B & 1) == 0) {
+            // 16-byte loads (B even: every pair of scenarios is aligned), all of a
+            // thread's loads in flight at once for feeders up to ~128 rows
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            constexpr int U2 = 12, H = SPB / 2;
+            const int total2 = total / 2;
+            for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
+                d2v r[U2];
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    const int j = 2 * (i % H), fr = i / H;
+                    const bool ok = i < total2 && j < nsb;   // nsb is even
+                    const size_t ga = DBG(16384) ? (size_t)s0 * 6 * nl + 2 * (size_t)i : (size_t)fr * B + s0 + j;
+                    r[u] = __builtin_nontemporal_load((const d2v *)(pq + (ok ? ga : 0)));
+                    r[u] = ok ? r[u] : d2v{0.0, 0.0};
+                }
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    const int j = 2 * (i % H), fr = i / H;
+                    if (i < total2) {
+                        stage[fr * (SPB + 1) + j] = r[u].x;
+                        stage[fr * (SPB + 1) + j + 1] = r[u].y;
+                    }
+                }
+            }
+        } else
         for (int i0 = 0; i0 < total; i0 += U * NT) {
             double r[U];
 #pragma unroll
@@ -311,12 +356,12 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
             for (int u = 0; u < UT; ++u) {
                 const int i = u * NT + (int)threadIdx.x;
-                t[u] = ld_global2(f.slot_temp, i < 9 * C * L ? i : 0);
+                t[u] = ld_global2(f.slot_temp, i < ntm * C * L ? i : 0);
             }
 #pragma unroll
             for (int u = 0; u < UT; ++u) {
                 const int i = u * NT + (int)threadIdx.x;
-                if (i < 9 * C * L) tl[i] = t[u];
+                if (i < ntm * C * L) tl[i] = t[u];
             }
         }
         const int np2 = 2 * bdepth * nblk;
@@ -389,6 +434,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #endif
     WSTAMP(2);
     for (int it = 0; __ballot(!done) != 0; ++it) {
+        WSTAMP(4 + 8 * it);
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
 #pragma unroll
@@ -410,6 +456,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             sc6[2 * p + 1] = acc.im;
         }
         seg_incl_n<L>(sc6);
+        WSTAMP(5 + 8 * it);
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             const cx inc = mk(sc6[2 * p], sc6[2 * p + 1]);
@@ -440,6 +487,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             }
         }
 
+        WSTAMP(6 + 8 * it);
         // ---- convergence on the substation branch (:199-217): Ib(0) = the segment total;
         // max_p |Ib(0,p) - Ibo(p)| < eps compared as squares
         double err2 = 0.0;
@@ -455,6 +503,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
         // the loss terms are needed only in a scenario's last sweep
         const bool any_fin = __ballot(fin) != 0;
+        WSTAMP(7 + 8 * it);
 
         // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
         // Also Re(drop . conj(Ib)) per phase: on a feeder without zeroed phases
@@ -463,6 +512,21 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         // VVC loss needs neither IL nor Ib after this point
         cx g[C][3];
         double lp[3] = {0.0, 0.0, 0.0};
+        if (f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
+            // TEMP = [[zs zm zm][zm zs zm][zm zm zs]]: drop_a = (zs - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const cx d = ldx(tl, (0 * C + c) * L + li), m = ldx(tl, (1 * C + c) * L + li);
+                const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
+                const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx b = ib[c][a];
+                    g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
+                    if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
+                }
+            }
+        } else
 #pragma unroll
         for (int c = 0; c < C; ++c) {
 #pragma unroll
@@ -482,6 +546,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             __builtin_amdgcn_sched_barrier(0);
 #endif
         }
+        WSTAMP(8 + 8 * it);
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             cx acc = g[0][p];
@@ -507,6 +572,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             }
         }
         wfence();
+        WSTAMP(9 + 8 * it);
         // block offsets, one lane per block (block 0, node 1's chain, has none),
         // stored as V0 - off so that V = (V0 - off) - Ginc is one subtraction per
         // slot; the chain's index pairs sit in registers (bp), all its reads issue together
@@ -539,6 +605,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             }
         }
         wfence();
+        WSTAMP(10 + 8 * it);
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -569,6 +636,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                 }
         }
         wfence();
+        WSTAMP(11 + 8 * it);
 
         if (fin && !DBG(128)) {
             // ---- a scenario's last sweep: V in node order into its region (Sld is
@@ -680,9 +748,8 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             wfence();
         }
         done = done || fin;
-        WSTAMP(3 + it);
     }
-    WSTAMP(40);
+    WSTAMP(120);
     if (!FULL && live && !DBG(128)) {
         // every Lnum_p + 1 = Nn (no zeroed phases): V_abc_list keeps every row, so
         // Vmin/Vmax are the plain extremes of |V| over the scenario's V in its
@@ -731,7 +798,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             }
         }
         const double part[8] = {ls, mn, mx, nc, nnc, no, nu, (double)nsb};
-        double *dst = o.partials + 8 * (size_t)blockIdx.x;
+        double *dst = o.partials + 8 * (size_t)tile;   // folded in tile (scenario) order
         for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -752,14 +819,17 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
             for (int u = 0; u < UV; ++u) {
                 const int i = i0 + u * NT + (int)threadIdx.x;
                 const int j = i % SPB, r = i / SPB;   // r = p*nn + k
-                if (i < total && j < nsb) {
+                if (DBG(32768)) {   // ablation: contiguous [B][3 nn] re / im planes (scenario-major emulation)
+                    if (i < total && o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + (size_t)s0 * 3 * nn + i);
+                    if (i < total && o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + (size_t)s0 * 3 * nn + i);
+                } else if (i < total && j < nsb) {
                     if (o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + (size_t)r * B + s0 + j);
                     if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + (size_t)r * B + s0 + j);
                 }
             }
         }
     }
-    WSTAMP(41);
+    WSTAMP(121);
     if (agg) {
         __syncthreads();
         if (last_wg) {
@@ -800,7 +870,7 @@ size_t wave_lds_bytes(const WaveDev &w) {
     const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 3) | 1);
     const size_t stage = 8 * 6 * (size_t)w.nl * (spb + 1);           // the loads, staged over the regions
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
-    const size_t temp = TEMP_IN_LDS ? 16 * (9 * (size_t)w.C * L) : 0;
+    const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 2 : 9) * (size_t)w.C * L) : 0;
     return temp + pairs + std::max(regions, std::max(stage, agg));
 }
 
@@ -862,7 +932,12 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
             attr_done.insert(key);
         }
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(w.wpb * 64), lds, st, w, n_scen, pq, o);
+    WaveDev wl = w;
+    wl.stag_lo = wl.stag_hi = wl.stag_n = 0;
+    if (const char *e = getenv("FPF_WAVE_WG_STAGGER")) {   // experiments: "lo,hi,n"
+        if (sscanf(e, "%d,%d,%d", &wl.stag_lo, &wl.stag_hi, &wl.stag_n) != 3) wl.stag_lo = wl.stag_hi = wl.stag_n = 0;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(w.wpb * 64), lds, st, wl, n_scen, pq, o);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess && getenv("FPF_DEBUG")) {
         hipFuncAttributes fa{};

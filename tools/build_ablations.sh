@@ -7,11 +7,11 @@ cd "$(dirname "$0")/../freedm_amd/csrc"
 OUT=../lib/abl
 mkdir -p $OUT
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I../../include"
-OBJS="../lib/fpf_api.o ../lib/fpf_generic.o ../lib/fpf_tiled.o ../lib/fpf_rtc.o ../lib/fpf_selftest.o ../lib/fpf_vvc.o"
+OBJS="../lib/fpf_api.o ../lib/fpf_generic.o ../lib/fpf_tiled.o ../lib/fpf_rtc.o ../lib/fpf_selftest.o ../lib/fpf_vvc.o ../lib/fpf_multi.o ../lib/fpf_areas.o ../lib/fpf_areas_kernels.o ../lib/fpf_vvc_grad.o"
 for m in "$@"; do
   /opt/rocm/bin/hipcc $FLAGS -DFPF_WAVE_ABL=$m -c fpf_wave.hip -o $OUT/wave_$m.o &
 done
 wait
 for m in "$@"; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libfreedm_pf_$m.so $OBJS $OUT/wave_$m.o -lhiprtc
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libfreedm_pf_$m.so $OBJS $OUT/wave_$m.o -lhiprtc -lrccl
 done

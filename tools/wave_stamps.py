@@ -2,8 +2,10 @@
 (freedm_amd/lib/libfreedm_pf_stamps.so, `make -C freedm_amd/csrc stamps`).
 Shares only -- the stamp build's own timing is not quoted (cdna_hip_programming.md 7).
 
-Stamps (fpf_wave.hip WSTAMP): 0 entry, 1 loads/tables staged, 2 Sld set up,
-3 + it end of sweep it, 40 after the loop, 41 V written out.
+Stamps (fpf_wave.hip WSTAMP, [64 waves][128]): 0 entry, 1 loads/tables staged,
+2 Sld set up, 4 + 8 it + k inside sweep it (k: 0 top, 1 backward scan, 2 Ib
+gathered, 3 convergence, 4 drops, 5 forward scan + stores, 6 block offsets,
+7 V), 120 after the loop, 121 V written out.
 
     NN=123 B=4096 FPF_WAVE_GEOM=2,4 python tools/wave_stamps.py
 """
@@ -29,7 +31,7 @@ def main():
     f = synthetic_feeder(nn, nn)
     L = _lib.load()
     L.fpf_debug_set_wave_stamp_buffer.argtypes = [ctypes.c_void_p]
-    buf = torch.zeros(64 * 64, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(64 * 128, dtype=torch.int64, device="cuda")
     pf = PowerFlow(f, kernel="wave")
     pq = torch.from_numpy(scenario_loads(f, np.arange(B))).cuda()
     out = {"loss": torch.zeros(B, dtype=torch.float64, device="cuda"),
@@ -42,22 +44,29 @@ def main():
     assert L.fpf_debug_set_wave_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
     pf.solve_device(pq, out)
     torch.cuda.synchronize()
-    st = buf.view(64, 64).cpu().numpy().astype(np.int64)
-    rows = []
+    st = buf.view(64, 128).cpu().numpy().astype(np.int64)
+    phases = ["il+bw_scan", "ib_gather", "conv", "drops", "fw_scan+store", "blk_off", "v", "fin"]
+    rows, ph = [], []
     for w in range(64):
         s = st[w]
-        if s[0] == 0 or s[41] == 0:
+        if s[0] == 0 or s[121] == 0:
             continue
-        sw = [s[3 + i] for i in range(37) if s[3 + i] != 0]
-        d = {"staging": s[1] - s[0], "sld": s[2] - s[1], "sweeps": sw[-1] - s[2], "n_sweeps": len(sw),
-             "after_loop": s[40] - sw[-1], "v_out": s[41] - s[40], "total": s[41] - s[0]}
-        d["per_sweep"] = d["sweeps"] / len(sw)
+        tops = [4 + 8 * it for it in range(12) if s[4 + 8 * it] != 0]
+        n_sw = len(tops)
+        d = {"staging": s[1] - s[0], "sld": s[2] - s[1], "sweeps": s[120] - s[2], "n_sweeps": n_sw,
+             "v_out": s[121] - s[120], "total": s[121] - s[0]}
+        d["per_sweep"] = d["sweeps"] / n_sw
         rows.append(d)
-    keys = ["staging", "sld", "sweeps", "after_loop", "v_out", "total", "per_sweep", "n_sweeps"]
+        for i, t in enumerate(tops):
+            nxt = s[tops[i + 1]] if i + 1 < n_sw else s[120]
+            marks = [s[t + k] for k in range(8)] + [nxt]
+            ph.append([marks[k + 1] - marks[k] for k in range(8)])
+    keys = ["staging", "sld", "sweeps", "v_out", "total", "per_sweep", "n_sweeps"]
     mean = {k: float(np.mean([r[k] for r in rows])) for k in keys}
+    phm = np.mean(np.array(ph, dtype=np.float64), axis=0)
     print(json.dumps({"nn": nn, "B": B, "tile": pf.info["tile"], "waves": len(rows), "mean_cycles": mean,
-                      "share": {k: mean[k] / mean["total"] for k in ("staging", "sld", "sweeps", "after_loop",
-                                                                      "v_out")}}))
+                      "share": {k: mean[k] / mean["total"] for k in ("staging", "sld", "sweeps", "v_out")},
+                      "sweep_phase_cycles": {p: float(v) for p, v in zip(phases, phm)}}))
 
 
 if __name__ == "__main__":
