@@ -108,19 +108,22 @@ def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
     """The CPU oracle (oracle/ref_dpf.c, a scalar port of DPF_return7 + the VVC
     reductions) on this host: once on every usable CPU (value, cores) and once
     on a single core.  Bounded sample: `seconds` of the all-core leg plus
-    seconds/3 of the single-core leg over one chunk of the config-2 batch."""
+    3 x seconds/6 of the single-core leg over one chunk of the config-2 batch."""
     from oracle import oracle as O
     from freedm_amd import scenario_loads
     threads, cpu_info = usable_cpus()
     pq = scenario_loads(feeder, np.arange(chunk), seed=SCEN_SEED)
     v_all, passes, dt = _time_oracle(O, feeder, pq, threads, seconds)
     pq1 = np.ascontiguousarray(pq[:, :, :4096])
-    v_one, passes1, dt1 = _time_oracle(O, feeder, pq1, 1, max(1.0, seconds / 3))
+    # single core: best of three legs (a lone thread's rate on a shared host varies
+    # with what the other cores run; the best leg is the least disturbed)
+    legs = [_time_oracle(O, feeder, pq1, 1, max(1.0, seconds / 6)) for _ in range(3)]
+    v_one, passes1, dt1 = max(legs, key=lambda r: r[0])
     phys, logical = _host_cores()
     out = {"value": v_all, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
            "sample": f"{passes} passes x {chunk} scenarios of the config-2 batch (123-bus, seed {SCEN_SEED}), "
                      f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s; single core: "
-                     f"{passes1} passes x 4096 scenarios, {dt1:.1f} s",
+                     f"best of 3 legs of {passes1} passes x 4096 scenarios, {dt1:.1f} s",
            "single_core": {"value": v_one, "unit": "converged scenarios/s", "cores": 1},
            "parallel_efficiency": v_all / (v_one * threads),
            "cpu_model": _cpu_model(), "host_physical_cores": phys, "host_logical_cpus": logical}
@@ -165,6 +168,25 @@ def _loads_on_device(torch, dev, loads, feeder, ids, seed, chunk=8192):
         b = min(len(ids), a + chunk)
         out[:, :, a:b] = torch.from_numpy(loads(feeder, ids[a:b], seed=seed)).to(dev)
     return out
+
+
+def _copy_bandwidth(torch, dev, nbytes=1 << 30, reps=10):
+    """Device-to-device copy rate (read + write bytes / s) of a 1 GiB buffer:
+    the achievable-HBM reference the roofline's 8 TB/s spec is checked against."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    for _ in range(2):
+        b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
 
 
 def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
@@ -371,6 +393,13 @@ def main():
                 "converged_scenarios_per_s": conv4 / (ms4 / 1e3),
                 "mean_sweeps": float(o4["iters"].double().mean().item())}
             del d4
+            copy = _copy_bandwidth(torch, dev)
+            res["hbm_copy_check"] = {"device_copy_gbs": copy, "spec_gbs": HBM_PEAK_GBS,
+                                     "copy_frac_of_spec": copy / HBM_PEAK_GBS,
+                                     "config2_frac_of_copy": achieved / copy,
+                                     "config4_frac_of_copy": ach4 / copy,
+                                     "note": "torch copy_ of 1 GiB, read+write bytes; roofline.frac stays "
+                                             "against the 8 TB/s spec"}
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
             res["cpu_baseline"] = cb

@@ -11,6 +11,8 @@
 #include "fpf_internal.h"
 #include "fpf_math.hpp"
 
+#include <cstdlib>
+
 #pragma clang fp contract(off)
 
 namespace fpf {
@@ -236,11 +238,208 @@ __global__ __launch_bounds__(256) void dpf_generic_kernel(FeederDev f, int B,
     if (o.vmax) o.vmax[s] = vmax;
 }
 
+// ---------------------------------------------------------------------------
+// Three lanes per scenario, one per phase: the same op lists and the same
+// per-element operations in the same order as dpf_generic_kernel (bit-identical
+// results), three times the wavefronts.  At 65 536 scenarios the one-lane form
+// has one wavefront per SIMD and is bound by the memory requests it can keep in
+// flight; here a wavefront holds 21 scenarios x 3 phases (lane 63 idles) and the
+// state of slot k, field f (re/im) lives at base[(2k + f) * ld3 + 3 s + p], so a
+// wavefront's access is still one contiguous 504-byte run.  The phases meet
+// only where the reference mixes them: the branch product Ib . TEMP (the three
+// Ib of a branch by lane shuffles), the convergence test (max over phases) and
+// the per-scenario loss / Vmin / Vmax.
+namespace {
+struct Slots3 {
+    double *base;
+    size_t ld3;
+    int i;   // 3 s + p
+    __device__ __forceinline__ cx ld_(int k) const {
+        return mk(base[(size_t)(2 * k) * ld3 + i], base[(size_t)(2 * k + 1) * ld3 + i]);
+    }
+    __device__ __forceinline__ void st(int k, cx v) const {
+        base[(size_t)(2 * k) * ld3 + i] = v.re;
+        base[(size_t)(2 * k + 1) * ld3 + i] = v.im;
+    }
+};
+__device__ __forceinline__ cx shfl_cx(cx v, int src) { return mk(__shfl(v.re, src, 64), __shfl(v.im, src, 64)); }
+}  // namespace
+
+constexpr int G3_SPW = 21;   // scenarios per wavefront
+
+__global__ __launch_bounds__(256) void dpf_generic3_kernel(FeederDev f, int B, const double *__restrict__ pq,
+                                                           double *__restrict__ scr, size_t ld, OutDev o) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sw = lane / 3, p = lane - 3 * sw, g0 = 3 * sw;   // scenario in the wave, phase, group's first lane
+    const int s = (blockIdx.x * 4 + wv) * G3_SPW + sw;
+    if (lane >= 3 * G3_SPW || s >= B) return;   // no lane reads an idle lane: shuffles stay inside a group
+    const int nl = f.nl, nn = f.nn;
+    const size_t ld3 = 3 * ld;
+    const int i3 = 3 * s + p;
+    const Slots3 Sld{scr, ld3, i3};
+    const Slots3 V{scr + (size_t)nl * 2 * ld3, ld3, i3};
+    const Slots3 IL{scr + (size_t)nl * 4 * ld3, ld3, i3};
+    const Slots3 Ib{scr + (size_t)(2 * nl + nn) * 2 * ld3, ld3, i3};
+    const cx v0 = mk(f.V0[2 * p], f.V0[2 * p + 1]);
+
+    for (int j = 0; j < nl; ++j) {   // :46-50, :92-96
+        const cx sl = mk(pq[((size_t)(2 * p) * nl + j) * B + s], pq[((size_t)(2 * p + 1) * nl + j) * B + s]);
+        Sld.st(j, cdiv(sl, mk(f.s3, 0.0)));
+        V.st(j, v0);
+    }
+    for (int k = 0; k < nn; ++k) IL.st(k, mk(0, 0));
+    for (int k = 0; k < nn - 1; ++k) Ib.st(k, mk(0, 0));
+    cx ibo = mk(0, 0);
+    int iters = 0, status = 1;
+    auto store_il = [&]() {
+        int q = 0;
+        for (; q + 4 <= f.n_il; q += 4) {
+            IlOp op[4];
+            cx sl[4], vv[4];
+            for (int u = 0; u < 4; ++u) {
+                op[u] = f.il_ops[q + u];
+                sl[u] = Sld.ld_(op[u].row);
+                vv[u] = V.ld_(op[u].ndr);
+            }
+            for (int u = 0; u < 4; ++u) IL.st(op[u].ndr - 1, load_current(sl[u], vv[u]));
+        }
+        for (; q < f.n_il; ++q) {
+            const IlOp op = f.il_ops[q];
+            IL.st(op.ndr - 1, load_current(Sld.ld_(op.row), V.ld_(op.ndr)));
+        }
+    };
+    for (int it = 0; it < f.mxitr; ++it) {
+        // backward sweep :134-160 (as dpf_generic_kernel, one phase per lane)
+        cx ibl = mk(0, 0);
+        if (f.n_bw > 0) {
+            BwOp op = f.bw_ops[0];
+            IlOp w = f.bw_il[0];
+            cx sl = w.row < 0 ? mk(0, 0) : Sld.ld_(w.row), vv = w.row < 0 ? mk(0, 0) : V.ld_(w.ndr);
+            for (int q = 0; q < f.n_bw; ++q) {
+                const bool more = q + 1 < f.n_bw;
+                BwOp nx = op;
+                cx nsl = mk(0, 0), nvv = mk(0, 0);
+                if (more) {
+                    nx = f.bw_ops[q + 1];
+                    const IlOp wn = f.bw_il[q + 1];
+                    if (wn.row >= 0) {
+                        nsl = Sld.ld_(wn.row);
+                        nvv = V.ld_(wn.ndr);
+                    }
+                }
+                const bool has_il = f.bw_il[q].row >= 0;
+                const cx il = has_il ? load_current(sl, vv) : mk(0, 0);
+                const bool first = op.kind & 2;
+                const cx ib = first ? mk(0, 0) : Ib.ld_(op.idx);
+                if (op.kind & 1) {
+                    Ib.st(op.idx, cadd(ib, ibl));
+                    ibl = mk(0, 0);
+                } else {
+                    const cx x = cadd(cadd(ib, ibl), il);
+                    Ib.st(op.idx, x);
+                    ibl = x;
+                }
+                sl = nsl;
+                vv = nvv;
+                op = nx;
+            }
+        }
+        // convergence :199-210, the reference's max over the phases in phase order
+        const cx d = csub(Ib.ld_(0), ibo);
+        const double df = hypot(d.re, d.im);
+        const double d0 = __shfl(df, g0, 64), d1 = __shfl(df, g0 + 1, 64), d2 = __shfl(df, g0 + 2, 64);
+        double errmx = d0;
+        if (d1 > errmx) errmx = d1;
+        if (d2 > errmx) errmx = d2;
+        ibo = Ib.ld_(0);
+        const bool conv = errmx < f.eps;
+        if (conv || it + 1 == f.mxitr) store_il();
+        // forward sweep :163-195, software-pipelined as dpf_generic_kernel
+        if (f.n_fw > 0) {
+            FwOp op = f.fw_ops[0];
+            cx b = Ib.ld_(op.ib);
+            cx sv = op.src < 0 ? v0 : V.ld_(op.src);
+            for (int q = 0; q < f.n_fw; ++q) {
+                const bool more = q + 1 < f.n_fw;
+                FwOp nx = op;
+                cx nb = mk(0, 0), nsv = mk(0, 0);
+                if (more) {
+                    nx = f.fw_ops[q + 1];
+                    nb = Ib.ld_(nx.ib);
+                    if (!(nx.pad & 1)) nsv = nx.src < 0 ? v0 : V.ld_(nx.src);
+                }
+                const cx b0 = shfl_cx(b, g0), b1 = shfl_cx(b, g0 + 1), b2 = shfl_cx(b, g0 + 2);
+                cx rv = csub(sv, drop_col(f.tz + 18 * (size_t)q, b0, b1, b2, p));
+                if (op.mask & (1 << p)) rv = mk(0, 0);
+                V.st(op.dst, rv);
+                if (more && (nx.pad & 1)) nsv = rv;
+                b = nb;
+                sv = nsv;
+                op = nx;
+            }
+        }
+        iters = it + 1;
+        if (conv) { status = 0; break; }
+    }
+
+    // post-processing (:222-253) with the VVC reductions, per phase; the
+    // scenario's loss / Vmin / Vmax combine the phases in the reference's order
+    double acc1 = 0, acc2 = 0, pb0 = 0, mn = INFINITY, mx = -INFINITY;
+    int cnt = 0;
+    for (int k = 0; k < nn; ++k) {
+        const cx v = V.ld_(k);
+        const cx ib = Ib.ld_(k == 0 ? 0 : k - 1);
+        const cx il = IL.ld_(k == 0 ? nn - 1 : k - 1);
+        const cx sv = cmul(v, mk(f.s3, 0.0));
+        const cx sb = cmul(sv, cconj(ib));
+        const cx sl = cmul(sv, cconj(il));
+        const double mag = hypot(v.re, v.im);
+        const size_t o6 = ((size_t)(2 * p) * nn + k) * B + s, o6i = o6 + (size_t)nn * B;
+        if (o.vpolar) { o.vpolar[o6] = mag; o.vpolar[o6i] = polar_angle(v, p); }
+        if (o.pqb) { o.pqb[o6] = sb.re; o.pqb[o6i] = sb.im; }
+        if (o.pql) { o.pql[o6] = sl.re; o.pql[o6i] = sl.im; }
+        if (o.v_re) o.v_re[((size_t)p * nn + k) * B + s] = v.re;
+        if (o.v_im) o.v_im[((size_t)p * nn + k) * B + s] = v.im;
+        if (k & 1) acc2 += sl.re; else acc1 += sl.re;
+        if (k == 0) pb0 = sb.re;
+        if (mag != 0 && cnt < f.K[p]) {
+            mn = fmin(mn, mag);
+            mx = fmax(mx, mag);
+            ++cnt;
+        }
+    }
+    const double x = pb0 - (acc1 + acc2);
+    const double pmin = cnt < f.K[p] ? fmin(mn, 0.0) : mn;
+    const double pmax = cnt < f.K[p] ? fmax(mx, 0.0) : mx;
+    const double x0 = __shfl(x, g0, 64), x1 = __shfl(x, g0 + 1, 64), x2 = __shfl(x, g0 + 2, 64);
+    const double n0 = __shfl(pmin, g0, 64), n1 = __shfl(pmin, g0 + 1, 64), n2 = __shfl(pmin, g0 + 2, 64);
+    const double m0 = __shfl(pmax, g0, 64), m1 = __shfl(pmax, g0 + 1, 64), m2 = __shfl(pmax, g0 + 2, 64);
+    if (p != 0) return;
+    const double loss = ((0.0 + x0) + x2) + (0.0 + x1);
+    double vmin = n0, vmax = m0;
+    if (n1 < vmin) vmin = n1;
+    if (m1 > vmax) vmax = m1;
+    if (n2 < vmin) vmin = n2;
+    if (m2 > vmax) vmax = m2;
+    if (o.iters) o.iters[s] = iters;
+    if (o.status) o.status[s] = (int8_t)status;
+    if (o.loss) o.loss[s] = loss;
+    if (o.vmin) o.vmin[s] = vmin;
+    if (o.vmax) o.vmax[s] = vmax;
+}
+
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st) {
+    static const bool one_lane = getenv("FPF_GENERIC_ONE_LANE") != nullptr;   // experiments
     const int block = 256;
-    const int grid = (n_scen + block - 1) / block;
-    hipLaunchKernelGGL(dpf_generic_kernel, dim3(grid), dim3(block), 0, st, f, n_scen, pq, scratch, ld, o);
+    if (one_lane) {
+        const int grid = (n_scen + block - 1) / block;
+        hipLaunchKernelGGL(dpf_generic_kernel, dim3(grid), dim3(block), 0, st, f, n_scen, pq, scratch, ld, o);
+    } else {
+        const int per_block = 4 * G3_SPW;
+        const int grid = (n_scen + per_block - 1) / per_block;
+        hipLaunchKernelGGL(dpf_generic3_kernel, dim3(grid), dim3(block), 0, st, f, n_scen, pq, scratch, ld, o);
+    }
     return hipGetLastError();
 }
 
