@@ -145,17 +145,20 @@ def _cpu_model():
     return "unknown"
 
 
-def _pmc_traffic(workload: str):
+def _pmc_traffic(workload: str, key: str = "hbm_bytes_per_launch"):
     """Per-launch HBM bytes of the dominant kernel for `workload` ("123-bus x
     4096") from the committed rocprofv3 --pmc summaries
-    (profiles/pmc_traffic.json, tools/pmc_summary.py), or None."""
+    (profiles/pmc_traffic.json, tools/pmc_summary.py), or None.  key
+    "hbm_bytes_per_launch": the guide's correction (2 x FETCH_SIZE + WRITE_SIZE);
+    "hbm_bytes_per_launch_calibrated": the counters calibrated on known byte
+    counts in this kernel's access pattern (profiles/r02_cal)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
         e = d.get("by_workload", {}).get(workload)
         if e is None and d.get("workload") == workload:
             e = d
-        return e.get("hbm_bytes_per_launch") if e else None
+        return e.get(key) if e else None
     except (OSError, ValueError, AttributeError):
         return None
 
@@ -364,6 +367,7 @@ def main():
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_calibrated": _pmc_traffic(f"{n_nodes}-bus x {B}", "hbm_bytes_per_launch_calibrated"),
                          "kernel": {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
                                     "wave": "dpf_wave_kernel", "generic": "dpf_generic_kernel"}[pf.kernel],
                          "bytes_alg_per_scenario": bytes_launch / B, "kernel_ms": avg_kern_s * 1e3,
@@ -389,7 +393,9 @@ def main():
             res["roofline_config4"] = {
                 "workload": f"BASELINE config 4: {n4}-bus feeder, {b4} hosting scenarios per GPU per launch",
                 "bound": "hbm", "achieved": ach4, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach4 / HBM_PEAK_GBS,
-                "traffic": _pmc_traffic(f"{n4}-bus x {b4}"), "kernel_ms": ms4, "bytes_alg_per_scenario": bpa,
+                "traffic": _pmc_traffic(f"{n4}-bus x {b4}"),
+                "traffic_calibrated": _pmc_traffic(f"{n4}-bus x {b4}", "hbm_bytes_per_launch_calibrated"),
+                "kernel_ms": ms4, "bytes_alg_per_scenario": bpa,
                 "converged_scenarios_per_s": conv4 / (ms4 / 1e3),
                 "mean_sweeps": float(o4["iters"].double().mean().item())}
             del d4
