@@ -120,13 +120,26 @@ def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
     legs = [_time_oracle(O, feeder, pq1, 1, max(1.0, seconds / 6)) for _ in range(3)]
     v_one, passes1, dt1 = max(legs, key=lambda r: r[0])
     phys, logical = _host_cores()
+    # BASELINE config 1 end to end: one sequential vvc_main round of the reference
+    # (gradient + step-size search, 2m+1 DPF calls) on the demo feeder, one core
+    from freedm_amd.feeder import demo_feeder
+    d = demo_feeder()
+    O.vvc_main(d.Dl, d.Z)
+    t_round = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        r = O.vvc_main(d.Dl, d.Z)
+        t_round.append(time.perf_counter() - t0)
+    out_c1 = {"ms": min(t_round) * 1e3, "dpf_calls": int(r["calls"]), "stop_fwd": int(r["stop_fwd"]),
+              "note": "oracle/ref_vvc.c vvc_main (VoltVarCtrl.cpp:1141-1762), best of 5, one core"}
     out = {"value": v_all, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
            "sample": f"{passes} passes x {chunk} scenarios of the config-2 batch (123-bus, seed {SCEN_SEED}), "
                      f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s; single core: "
                      f"best of 3 legs of {passes1} passes x 4096 scenarios, {dt1:.1f} s",
            "single_core": {"value": v_one, "unit": "converged scenarios/s", "cores": 1},
            "parallel_efficiency": v_all / (v_one * threads),
-           "cpu_model": _cpu_model(), "host_physical_cores": phys, "host_logical_cpus": logical}
+           "cpu_model": _cpu_model(), "host_physical_cores": phys, "host_logical_cpus": logical,
+           "config1_vvc_main": out_c1}
     out.update(cpu_info)
     if phys:
         # not measured: what the whole host would give if the port scaled linearly
@@ -148,10 +161,8 @@ def _cpu_model():
 def _pmc_traffic(workload: str, key: str = "hbm_bytes_per_launch"):
     """Per-launch HBM bytes of the dominant kernel for `workload` ("123-bus x
     4096") from the committed rocprofv3 --pmc summaries
-    (profiles/pmc_traffic.json, tools/pmc_summary.py), or None.  key
-    "hbm_bytes_per_launch": the guide's correction (2 x FETCH_SIZE + WRITE_SIZE);
-    "hbm_bytes_per_launch_calibrated": the counters calibrated on known byte
-    counts in this kernel's access pattern (profiles/r02_cal)."""
+    (profiles/pmc_traffic.json, tools/pmc_summary.py), or None: the guide's
+    correction, 2 x FETCH_SIZE + WRITE_SIZE."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
@@ -367,7 +378,6 @@ def main():
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_calibrated": _pmc_traffic(f"{n_nodes}-bus x {B}", "hbm_bytes_per_launch_calibrated"),
                          "kernel": {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
                                     "wave": "dpf_wave_kernel", "generic": "dpf_generic_kernel"}[pf.kernel],
                          "bytes_alg_per_scenario": bytes_launch / B, "kernel_ms": avg_kern_s * 1e3,
@@ -394,7 +404,6 @@ def main():
                 "workload": f"BASELINE config 4: {n4}-bus feeder, {b4} hosting scenarios per GPU per launch",
                 "bound": "hbm", "achieved": ach4, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach4 / HBM_PEAK_GBS,
                 "traffic": _pmc_traffic(f"{n4}-bus x {b4}"),
-                "traffic_calibrated": _pmc_traffic(f"{n4}-bus x {b4}", "hbm_bytes_per_launch_calibrated"),
                 "kernel_ms": ms4, "bytes_alg_per_scenario": bpa,
                 "converged_scenarios_per_s": conv4 / (ms4 / 1e3),
                 "mean_sweeps": float(o4["iters"].double().mean().item())}
@@ -406,8 +415,29 @@ def main():
                                      "config4_frac_of_copy": ach4 / copy,
                                      "note": "torch copy_ of 1 GiB, read+write bytes; roofline.frac stays "
                                              "against the 8 TB/s spec"}
+        if world == 1 and args.config == 2 and not args.no_c4 and not args.nodes and not args.scenarios:
+            # BASELINE config 1: one whole VVC round (fpf_vvc_round: gradient on the
+            # host after a device solve, all m_max+1 step sizes as one batch, the
+            # reversal) on the demo feeder; host-synchronous, best of 20
+            from freedm_amd import demo_feeder
+            d1 = demo_feeder()
+            pf1 = PowerFlow(d1, device=local)
+            for _ in range(3):
+                r1 = pf1.vvc_round(d1.Dl)
+            tt = []
+            for _ in range(20):
+                t0 = time.perf_counter()
+                r1 = pf1.vvc_round(d1.Dl)
+                tt.append(time.perf_counter() - t0)
+            res["config1_vvc_round"] = {"gpu_ms": min(tt) * 1e3, "stop_fwd": r1["stop_fwd"], "sent": r1["sent"],
+                                        "candidates": 101, "kernel": pf1.kernel,
+                                        "note": "fpf_vvc_round on the 9-row demo feeder, host-synchronous"}
+            pf1.close()
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
+            if "config1_vvc_round" in res:
+                res["config1_vvc_round"]["cpu_ms"] = cb["config1_vvc_main"]["ms"]
+                res["config1_vvc_round"]["speedup"] = cb["config1_vvc_main"]["ms"] / res["config1_vvc_round"]["gpu_ms"]
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = value / cb["value"]
             res["speedup_vs_cpu_single_core"] = value / cb["single_core"]["value"]

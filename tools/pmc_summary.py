@@ -43,17 +43,6 @@ def main():
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
     hbm = (2 * fk + wk) * 1024
-    # calibrated on known byte counts (tools/ubench/traffic_cal, profiles/r02_cal):
-    # a pure read stream reports FETCH_SIZE = f x bytes (f = 0.375 for full-line
-    # streams, 0.75 for 64-byte row segments) and WRITE_SIZE = 0.25 x bytes; a
-    # pure write stream reports WRITE_SIZE = 1.0 x bytes.  The wave kernel's tiles
-    # read row segments, the generic kernel streams
-    cal = json.load(open(os.path.join(ROOT, "profiles", "r02_cal", "summary.json")))
-    pattern = "rd8" if "generic" in kname else "rd8s"
-    fr = cal[pattern]["FETCH_SIZE_bytes_ratio"]
-    wr_of_rd = cal[pattern]["WRITE_SIZE_bytes_ratio"]
-    rd_cal = fk * 1024 / fr
-    wr_cal = max(0.0, wk * 1024 - wr_of_rd * rd_cal)
     with open(os.path.join(dst, "kernel_stats.csv")) as f:
         avg_ns = next(float(r["AverageNs"]) for r in csv.DictReader(f) if kname in r["Name"])
     scen = b.get("config", {}).get("scenarios_per_gpu")
@@ -63,8 +52,6 @@ def main():
         "tag": tag, "kernel": kname, "launches_fetch": len(fetch), "launches_write": len(write),
         "FETCH_SIZE_KiB_per_launch": fk, "WRITE_SIZE_KiB_per_launch": wk,
         "hbm_bytes_per_launch": hbm, "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
-        "calibrated": {"read_bytes": rd_cal, "write_bytes": wr_cal, "total": rd_cal + wr_cal, "read_pattern": pattern,
-                       "source": "profiles/r02_cal/summary.json"},
         "rocprof_avg_kernel_ns": avg_ns, "bench_kernel_ms": b.get("roofline", {}).get("kernel_ms"),
         "bytes_alg_per_launch": (b.get("roofline", {}).get("bytes_alg_per_scenario") or 0) * (scen or 0),
         "workload": workload,
@@ -80,7 +67,6 @@ def main():
         d = {"by_workload": {d["workload"]: d} if "workload" in d else {}}
     d["by_workload"][workload] = {k: res[k] for k in ("tag", "kernel", "hbm_bytes_per_launch", "bytes_alg_per_launch",
                                                      "rocprof_avg_kernel_ns", "bench_kernel_ms")}
-    d["by_workload"][workload]["hbm_bytes_per_launch_calibrated"] = rd_cal + wr_cal
     json.dump(d, open(tp, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "bench_line"}, indent=1))
 
