@@ -580,27 +580,27 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
             w.temp[((j * C + c) * L + lane) * 2 + 1] = h.tz[(size_t)nd.fw * 18 + 2 * j + 1];
         }
     }
-    // TEMP of the form [[zs zm zm][zm zs zm][zm zm zs]] on every branch (the
-    // transposed lines and transformers of load_system_data's Z): the drop of
-    // phase a is (zs - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3), 2 complex per slot
-    // instead of 9 (fast mode only; the rounding differs by a few ulp)
+    // TEMP with one common off-diagonal value per branch, [[z1 zm zm][zm z2 zm]
+    // [zm zm z3]] (the transposed lines and transformers of load_system_data's
+    // Z): the drop of phase a is (z_a - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3) -- 4
+    // complex per slot instead of 9 (fast mode only; a few ulp of rounding)
     bool sym = !getenv("FPF_WAVE_NO_SYM");
     for (int q = 0; q < n && sym; ++q) {
         const double *t = &h.tz[(size_t)h.node[at[q]].fw * 18];
-        for (int j = 0; j < 9 && sym; ++j) {
-            const int ref = (j % 4 == 0) ? 0 : 1;   // diagonal j = 0, 4, 8; off-diagonal j = 1
-            sym = t[2 * j] == t[2 * ref] && t[2 * j + 1] == t[2 * ref + 1];
-        }
+        for (int j = 1; j < 9 && sym; ++j)
+            if (j % 4 != 0) sym = t[2 * j] == t[2] && t[2 * j + 1] == t[3];   // off-diagonal j = 1, 2, 3, 5, 6, 7
     }
     if (sym) {
-        std::vector<double> ts(2 * S * 2, 0.0);
+        std::vector<double> ts(4 * S * 2, 0.0);
         for (int q = 0; q < n; ++q) {
             const int c = q % C, lane = q / C;
             const double *t = &h.tz[(size_t)h.node[at[q]].fw * 18];
-            ts[((0 * C + c) * L + lane) * 2 + 0] = t[0] - t[2];
-            ts[((0 * C + c) * L + lane) * 2 + 1] = t[1] - t[3];
-            ts[((1 * C + c) * L + lane) * 2 + 0] = t[2];
-            ts[((1 * C + c) * L + lane) * 2 + 1] = t[3];
+            for (int a = 0; a < 3; ++a) {
+                ts[((a * C + c) * L + lane) * 2 + 0] = t[2 * (4 * a)] - t[2];
+                ts[((a * C + c) * L + lane) * 2 + 1] = t[2 * (4 * a) + 1] - t[3];
+            }
+            ts[((3 * C + c) * L + lane) * 2 + 0] = t[2];
+            ts[((3 * C + c) * L + lane) * 2 + 1] = t[3];
         }
         w.temp.swap(ts);
     }
@@ -1618,6 +1618,7 @@ extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const d
     w.ncomp = wh.ncomp;
     w.wpb = wh.wpb;
     w.off_in_x = wh.off_in_x;
+    w.temp_sym = wh.temp_sym;
     const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, wh.ok ? (int)wave_lds_bytes(w) : 0, wh.ncomp, wh.nblk, wh.bdepth};
     std::memcpy(out, v, sizeof(v));
     return FPF_OK;

@@ -130,8 +130,8 @@ struct WaveDev {
     int32_t wpb;             // wavefronts per workgroup (16, 8 or 4; fpf_api.cpp: analyse_wave)
     int32_t off_in_x;        // 1: block offsets stored over X's first nblk entries (nblk <= L, depth <= 4)
     int32_t stag_lo, stag_hi, stag_n;   // workgroups [lo, hi) start stag_n x 8 k cycles late (diagnostic)
-    int32_t temp_sym;        // 1: every branch's TEMP is [[zs zm zm][zm zs zm][zm zm zs]] (transposed
-                             //    line / transformer): slot_temp holds (zs - zm, zm) per slot
+    int32_t temp_sym;        // 1: every branch's TEMP has one common off-diagonal zm (transposed
+                             //    line / transformer): slot_temp holds (z_aa - zm) x 3, zm per slot
     double V0[6], s3, eps, lb_v, ub_v;
     const int32_t *slot_row;    // [C][L] Dl row of the slot's node (-1: empty slot)
     const int32_t *slot_node;   // [C][L] node id
@@ -141,7 +141,7 @@ struct WaveDev {
     const int32_t *slot_blk;    // [C][L] block of the slot's node
     const int32_t *slot_mref;   // [3][C][L] forward index of the nearest zeroed proper ancestor, -1 none
     const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch, row-major
-                                // (l, a); temp_sym: [2][C][L] (zs - zm, zm)
+                                // (l, a); temp_sym: [4][C][L] (z_aa - zm for a = 0..2, zm)
     const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) forward indices; pad = ncomp (zero)
 };
 

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     // TEMP blocks); per scenario Sld (later V in node order), the gathered scan
     // values X ([3][XC], entry XC-1 = 0; backward and forward entries share it)
     // and the block offsets
-    const int ntm = f.temp_sym ? 2 : 9;                               // TEMP entries per slot
+    const int ntm = f.temp_sym ? 4 : 9;                               // TEMP entries per slot
     double2 *const tl = lds;                                          // [ntm][C][L] if TEMP_IN_LDS
     int *const pairs = (int *)(tl + (TEMP_IN_LDS ? ntm * C * L : 0)); // [bdepth][2][nblk]
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
@@ -513,14 +513,15 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         cx g[C][3];
         double lp[3] = {0.0, 0.0, 0.0};
         if (f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
-            // TEMP = [[zs zm zm][zm zs zm][zm zm zs]]: drop_a = (zs - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
+            // one common off-diagonal zm: drop_a = (z_aa - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const cx d = ldx(tl, (0 * C + c) * L + li), m = ldx(tl, (1 * C + c) * L + li);
+                const cx m = ldx(tl, (3 * C + c) * L + li);
                 const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
                 const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
+                    const cx d = ldx(tl, (a * C + c) * L + li);
                     const cx b = ib[c][a];
                     g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
                     if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
@@ -870,7 +871,7 @@ size_t wave_lds_bytes(const WaveDev &w) {
     const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 3) | 1);
     const size_t stage = 8 * 6 * (size_t)w.nl * (spb + 1);           // the loads, staged over the regions
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
-    const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 2 : 9) * (size_t)w.C * L) : 0;
+    const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
     return temp + pairs + std::max(regions, std::max(stage, agg));
 }
 
