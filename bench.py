@@ -104,7 +104,7 @@ def _time_oracle(O, feeder, pq, threads: int, seconds: float):
     return n_conv / dt, passes, dt
 
 
-def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
+def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: bool = True):
     """The CPU oracle (oracle/ref_dpf.c, a scalar port of DPF_return7 + the VVC
     reductions) on this host: once on every usable CPU (value, cores) and once
     on a single core.  Bounded sample: `seconds` of the all-core leg plus
@@ -114,32 +114,36 @@ def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768):
     threads, cpu_info = usable_cpus()
     pq = scenario_loads(feeder, np.arange(chunk), seed=SCEN_SEED)
     v_all, passes, dt = _time_oracle(O, feeder, pq, threads, seconds)
-    pq1 = np.ascontiguousarray(pq[:, :, :4096])
+    pq1 = np.ascontiguousarray(pq[:, :, :min(4096, chunk)])
     # single core: best of three legs (a lone thread's rate on a shared host varies
     # with what the other cores run; the best leg is the least disturbed)
     legs = [_time_oracle(O, feeder, pq1, 1, max(1.0, seconds / 6)) for _ in range(3)]
     v_one, passes1, dt1 = max(legs, key=lambda r: r[0])
     phys, logical = _host_cores()
-    # BASELINE config 1 end to end: one sequential vvc_main round of the reference
-    # (gradient + step-size search, 2m+1 DPF calls) on the demo feeder, one core
-    from freedm_amd.feeder import demo_feeder
-    d = demo_feeder()
-    O.vvc_main(d.Dl, d.Z)
-    t_round = []
-    for _ in range(5):
-        t0 = time.perf_counter()
-        r = O.vvc_main(d.Dl, d.Z)
-        t_round.append(time.perf_counter() - t0)
-    out_c1 = {"ms": min(t_round) * 1e3, "dpf_calls": int(r["calls"]), "stop_fwd": int(r["stop_fwd"]),
-              "note": "oracle/ref_vvc.c vvc_main (VoltVarCtrl.cpp:1141-1762), best of 5, one core"}
+    out_c1 = None
+    if config1:
+        # BASELINE config 1 end to end: one sequential vvc_main round of the reference
+        # (gradient + step-size search, 2m+1 DPF calls) on the demo feeder, one core
+        from freedm_amd.feeder import demo_feeder
+        d = demo_feeder()
+        O.vvc_main(d.Dl, d.Z)
+        t_round = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            r = O.vvc_main(d.Dl, d.Z)
+            t_round.append(time.perf_counter() - t0)
+        out_c1 = {"ms": min(t_round) * 1e3, "dpf_calls": int(r["calls"]), "stop_fwd": int(r["stop_fwd"]),
+                  "note": "oracle/ref_vvc.c vvc_main (VoltVarCtrl.cpp:1141-1762), best of 5, one core"}
     out = {"value": v_all, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
-           "sample": f"{passes} passes x {chunk} scenarios of the config-2 batch (123-bus, seed {SCEN_SEED}), "
+           "sample": f"{passes} passes x {chunk} scenarios of the batch ({feeder.name}, seed {SCEN_SEED}), "
                      f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s; single core: "
-                     f"best of 3 legs of {passes1} passes x 4096 scenarios, {dt1:.1f} s",
+                     f"best of 3 legs of {passes1} passes x {pq1.shape[2]} scenarios, {dt1:.1f} s",
            "single_core": {"value": v_one, "unit": "converged scenarios/s", "cores": 1},
            "parallel_efficiency": v_all / (v_one * threads),
            "cpu_model": _cpu_model(), "host_physical_cores": phys, "host_logical_cpus": logical,
-           "config1_vvc_main": out_c1}
+           }
+    if out_c1:
+        out["config1_vvc_main"] = out_c1
     out.update(cpu_info)
     if phys:
         # not measured: what the whole host would give if the port scaled linearly
@@ -429,13 +433,32 @@ def main():
                 t0 = time.perf_counter()
                 r1 = pf1.vvc_round(d1.Dl)
                 tt.append(time.perf_counter() - t0)
+            # the host-buffer entry (fpf_solve_batch: PCIe copies in and out included;
+            # per-scenario scalars out, no V), one config-2 batch
+            pq_h = d_pqs[0].cpu().numpy()
+            pf.solve(pq_h, full=False)
+            th = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                rh = pf.solve(pq_h, full=False)
+                th.append(time.perf_counter() - t0)
+            res["host_buffer_path"] = {"scen_per_s": int((rh["status"] == 0).sum()) / min(th),
+                                       "ms_per_batch": min(th) * 1e3,
+                                       "note": "fpf_solve_batch with host buffers (26 MB H2D, scalars D2H), "
+                                               "best of 5; never the bench value"}
             res["config1_vvc_round"] = {"gpu_ms": min(tt) * 1e3, "stop_fwd": r1["stop_fwd"], "sent": r1["sent"],
                                         "candidates": 101, "kernel": pf1.kernel,
                                         "note": "fpf_vvc_round on the 9-row demo feeder, host-synchronous"}
             pf1.close()
+        if world == 1 and args.config == 3 and not args.no_cpu_baseline and not args.nodes:
+            # the 2048-bus feeder on the host: a bounded sample of 1024 scenarios
+            cb = cpu_baseline(feeder, seconds=args.cpu_seconds, chunk=1024, config1=False)
+            res["cpu_baseline"] = cb
+            res["speedup_vs_cpu"] = value / cb["value"]
+            res["speedup_vs_cpu_single_core"] = value / cb["single_core"]["value"]
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
-            if "config1_vvc_round" in res:
+            if "config1_vvc_round" in res and "config1_vvc_main" in cb:
                 res["config1_vvc_round"]["cpu_ms"] = cb["config1_vvc_main"]["ms"]
                 res["config1_vvc_round"]["speedup"] = cb["config1_vvc_main"]["ms"] / res["config1_vvc_round"]["gpu_ms"]
             res["cpu_baseline"] = cb
