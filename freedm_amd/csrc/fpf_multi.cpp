@@ -93,14 +93,24 @@ extern "C" void fpf_multi_destroy(fpf_multi *m) {
     delete m;
 }
 
-extern "C" const char *fpf_multi_last_error(const fpf_multi *m) { return m ? m->err.c_str() : "null context"; }
+// why the calling thread's last fpf_multi_create failed (there is no handle to carry it)
+static thread_local std::string g_create_err = "no error";
+
+extern "C" const char *fpf_multi_last_error(const fpf_multi *m) { return m ? m->err.c_str() : g_create_err.c_str(); }
 
 extern "C" int fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols, const double *z, int z_rows,
                                 int z_cols, const fpf_opts *opts, fpf_multi **out) {
-    if (!out || n_gpus < 1) return FPF_ERR_ARG;
+    if (!out || n_gpus < 1) {
+        g_create_err = "fpf_multi_create: out is NULL or n_gpus < 1";
+        return FPF_ERR_ARG;
+    }
     *out = nullptr;
     int avail = 0;
-    if (hipGetDeviceCount(&avail) != hipSuccess || avail < n_gpus) return FPF_ERR_ARG;
+    if (hipGetDeviceCount(&avail) != hipSuccess || avail < n_gpus) {
+        g_create_err = "fpf_multi_create: " + std::to_string(n_gpus) + " devices requested, " + std::to_string(avail) +
+                       " visible";
+        return FPF_ERR_ARG;
+    }
     fpf_multi *m = new fpf_multi();
     m->n = n_gpus;
     m->ctx.assign(n_gpus, nullptr);
@@ -114,18 +124,22 @@ extern "C" int fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
         int rc = fpf_ctx_create(d, &m->ctx[d]);
         if (rc == FPF_OK) rc = fpf_feeder_create(m->ctx[d], dl, nl, ncols, z, z_rows, z_cols, opts, &m->feeder[d]);
         if (rc != FPF_OK) {
+            g_create_err = "fpf_multi_create: device " + std::to_string(d) + ": " +
+                           (m->ctx[d] ? fpf_last_error(m->ctx[d]) : "context creation failed");
             fpf_multi_destroy(m);
             return rc;
         }
         if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&m->stream[d], hipStreamNonBlocking) != hipSuccess ||
             hipMalloc(&m->d_agg[d], 20 * sizeof(double)) != hipSuccess) {
+            g_create_err = "fpf_multi_create: device " + std::to_string(d) + ": stream / buffer allocation failed";
             fpf_multi_destroy(m);
             return FPF_ERR_HIP;
         }
     }
     std::vector<int> devs(n_gpus);
     for (int d = 0; d < n_gpus; ++d) devs[d] = d;
-    if (ncclCommInitAll(m->comm.data(), n_gpus, devs.data()) != ncclSuccess) {
+    if (const ncclResult_t nr = ncclCommInitAll(m->comm.data(), n_gpus, devs.data()); nr != ncclSuccess) {
+        g_create_err = std::string("fpf_multi_create: ncclCommInitAll: ") + ncclGetErrorString(nr);
         m->comm.assign(n_gpus, nullptr);
         fpf_multi_destroy(m);
         return FPF_ERR_HIP;
@@ -134,6 +148,7 @@ extern "C" int fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
     fpf_feeder_get_info(m->feeder[0], &in);
     m->nn = in.nn;
     m->nl = in.nl;
+    g_create_err = "no error";
     *out = m;
     return FPF_OK;
 }

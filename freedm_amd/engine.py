@@ -338,7 +338,7 @@ class MultiPowerFlow:
         rc = L.fpf_multi_create(n_gpus, dl.ctypes.data_as(_lib._dp), dl.shape[0], dl.shape[1],
                                 zbuf.ctypes.data_as(_lib._dp), Z.shape[0], Z.shape[1], C.byref(o), C.byref(h))
         if rc:
-            raise DPFError(rc, f"fpf_multi_create(n_gpus={n_gpus}) failed")
+            raise DPFError(rc, L.fpf_multi_last_error(None).decode())
         self.h = h
         f0 = C.c_void_p()
         L.fpf_multi_get_feeder(h, 0, C.byref(f0))

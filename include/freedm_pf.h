@@ -184,6 +184,7 @@ int         fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
                              const double *z, int z_rows, int z_cols,
                              const fpf_opts *opts, fpf_multi **out);
 void        fpf_multi_destroy(fpf_multi *m);
+/* m = NULL: why the calling thread's last fpf_multi_create failed */
 const char *fpf_multi_last_error(const fpf_multi *m);
 int         fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq,
                             const fpf_outputs *out, fpf_aggregate *agg);

@@ -67,3 +67,17 @@ def test_multi_one_gpu_equals_single(name, B):
     assert ag["loss_sum"] == pytest.approx(ref[0], rel=1e-12)
     assert ag == single["aggregate"]
     m.close()
+
+
+def test_multi_create_failure_reason():
+    """fpf_multi_create keeps why it failed (no handle exists to carry it):
+    here, more devices than the host has (none in this container)."""
+    import ctypes as C
+    from freedm_amd import _lib
+    L = _lib.load()
+    h = C.c_void_p()
+    z = np.zeros(2)
+    dl = np.zeros((1, 12))
+    rc = L.fpf_multi_create(4096, dl.ctypes.data_as(_lib._dp), 1, 12, z.ctypes.data_as(_lib._dp), 0, 0, None, C.byref(h))
+    assert rc < 0 and not h.value
+    assert b"4096 devices requested" in L.fpf_multi_last_error(None)
