@@ -164,6 +164,11 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
 /* Device-memory batch: every pointer (pq, out fields, d_agg) is device memory;
  * enqueued on `stream` (a hipStream_t; NULL = the NULL/default stream, as in
  * every HIP API) and returns without synchronising.  d_agg (8 doubles, fpf_aggregate layout) may be NULL.
+ * Launches that produce an aggregate (d_agg != NULL here, fpf_aggregate_device,
+ * fpf_solve_batch) share the feeder's partials and arrival ticket; the library
+ * serialises them across streams with an event per feeder (each waits for the
+ * previous one), so they may be enqueued on different streams. Solves without
+ * an aggregate on one feeder run concurrently.
  * Returns FPF_OK or an error (the non-converged count is in d_agg / status). */
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);
