@@ -269,20 +269,25 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     const int s0 = tile * SPB, s = s0 + sc;
     const int nsb = min(SPB, B - s0);              // scenarios of this workgroup
     const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
-    // LDS: per workgroup the block-chain table (and, in a diagnostic build, the
-    // TEMP blocks); per scenario Sld (later V in node order), the gathered scan
-    // values X ([3][XC], entry XC-1 = 0; backward and forward entries share it)
-    // and the block offsets
+    // LDS: per workgroup the TEMP values, the block-chain table and the slots'
+    // nodes; the staged loads STG [3][Nl + 1][SPB + 1] of (P, Q) / (bkva/3), one
+    // column per scenario (row Nl = 0 for empty slots; the +1 column spreads a
+    // slot's rows over the banks), read in place every sweep and overwritten by
+    // the scenario's V (node k at row k - 1) in its last sweep; per scenario the
+    // gathered scan values X ([3][XC], entry XC-1 = 0; backward and forward
+    // entries share it), the block offsets and the source voltage
     const int ntm = f.temp_sym ? 4 : 9;                               // TEMP entries per slot
     double2 *const tl = lds;                                          // [ntm][C][L] if TEMP_IN_LDS
     int *const pairs = (int *)(tl + (TEMP_IN_LDS ? ntm * C * L : 0)); // [bdepth][2][nblk]
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
     int *const knode = pairs + pair_n;                                // [C][L] node of each slot
-    double2 *const reg0 = (double2 *)(knode + C * L);                 // per-scenario regions
+    constexpr int SROW = SPB + 1;
+    const int PSTR = (nl + 1) * SROW;                                 // double2 per phase plane of STG
+    double2 *const stg = (double2 *)(knode + C * L);
+    double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
-    const int RS = (3 * C * L + 3 * XC + noff + 3) | 1;              // double2 per region (odd: V read-out banks)
-    double2 *const SL = reg0 + sc * RS;
-    double2 *const X = SL + 3 * C * L;
+    const int RS = (3 * XC + noff + 3) | 1;                          // double2 per region
+    double2 *const X = reg0 + sc * RS;
     double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
     // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
     // pair read of the scenario precedes the offset stores in its one wave's
@@ -290,19 +295,28 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
     double2 *const OFF = f.off_in_x ? X : X + 3 * XC;
     const int OS = f.off_in_x ? XC : nblk;
     const bool live = sc < nsb;
-    int si[C], row[C], bk[C];
+    int si[C], sb[C], bk[C];   // sb: the slot's (row, scenario) in a phase plane of STG
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        row[c] = f.slot_row[c * L + li];
+        const int r = f.slot_row[c * L + li];
+        sb[c] = (r < 0 ? nl : r) * SROW + sc;
         si[c] = f.slot_info[c * L + li];
         bk[c] = f.slot_blk[c * L + li];
     }
+    const double inv_s3 = 1.0 / f.s3;
 
     // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced (16 scenarios = one
-    // 128-byte line per row), U loads in flight per thread, staged over the
-    // per-scenario regions; then each slot picks its row
+    // 128-byte line per row), all of a thread's loads in flight, into STG scaled
+    // by 1/(bkva/3) (Sld, DPF_return7.cpp:46-50)
     {
-        double *stage = (double *)reg0;   // [6][nl][SPB + 1]: the pad spreads a slot's rows over the banks
+        double *const sd = (double *)stg;
+        // element (f, row, j) of pq -> STG[f / 2][row][j].{re, im}
+        auto spos = [&](int fr, int j) {
+            const int fq = fr / nl, r = fr - fq * nl;
+            return 2 * (((fq >> 1) * (nl + 1) + r) * SROW + j) + (fq & 1);
+        };
+        if ((int)threadIdx.x < 3 * SROW)   // the zero row of each phase plane
+            stg[((int)threadIdx.x / SROW) * PSTR + nl * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
         if ((B & 1) == 0) {
@@ -327,8 +341,9 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     const int i = i0 + u * NT + (int)threadIdx.x;
                     const int j = 2 * (i % H), fr = i / H;
                     if (i < total2) {
-                        stage[fr * (SPB + 1) + j] = r[u].x;
-                        stage[fr * (SPB + 1) + j + 1] = r[u].y;
+                        const int q = spos(fr, j);
+                        sd[q] = r[u].x * inv_s3;
+                        sd[q + 2] = r[u].y * inv_s3;
                     }
                 }
             }
@@ -346,7 +361,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + u * NT + (int)threadIdx.x;
-                if (i < total) stage[(i / SPB) * (SPB + 1) + i % SPB] = r[u];
+                if (i < total) sd[spos(i / SPB, i % SPB)] = r[u] * inv_s3;
             }
         }
         // the feeder tables: all loads in flight before the LDS stores
@@ -382,25 +397,6 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         const bool ok = j < bdepth && li < nblk;
         bp[j] = ok ? pairs[(2 * j) * nblk + li] | (pairs[(2 * j + 1) * nblk + li] << 16) : (XC - 1) | ((XC - 1) << 16);
     }
-    const double inv_s3 = 1.0 / f.s3;
-    double2 sld_in[C][3];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const double *stage = (const double *)reg0;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            // Sld = (P + jQ) / (bkva/3)  (:46-50)
-            sld_in[c][p] = make_double2(0.0, 0.0);
-            if (row[c] >= 0)
-                sld_in[c][p] = make_double2(stage[((2 * p) * nl + row[c]) * (SPB + 1) + sc] * inv_s3,
-                                            stage[((2 * p + 1) * nl + row[c]) * (SPB + 1) + sc] * inv_s3);
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) SL[(p * C + c) * L + li] = sld_in[c][p];
     if (li < 3) X[li * XC + XC - 1] = make_double2(0.0, 0.0);
     // per-scenario results for the workgroup aggregate: [sc][loss, vmin, vmax, status]
     __shared__ double res[SPB][4];
@@ -440,7 +436,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(SL, (p * C + c) * L + li), v[c][p]);
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(stg, p * PSTR + sb[c]), v[c][p]);
 
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of IL;
         // Einc is gathered at subtree ends only (leaves)
@@ -651,7 +647,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     const int k = knode[c * L + li];
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
-                        stx(SL, p * nn + k, v[c][p]);
+                        stx(stg, p * PSTR + (k - 1) * SROW + sc, v[c][p]);   // over the scenario's own Sld
                         if (FULL) {
                             emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
                             const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
@@ -665,8 +661,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     const cx v0p = ldx(V0S, p);
-                    // substation row 0: V0, Ib(0) = this sweep's total, no load
-                    stx(SL, p * nn + 0, v0p);
+                    // substation row 0: V0 (in V0S), Ib(0) = this sweep's total, no load
                     if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0p, mk(0, 0), ibo[p]);
                     if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
                         const cx sb = cmul(cmul(v0p, mk(f.s3, 0.0)), cconj(ibo[p]));
@@ -716,7 +711,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                         const int k = k0 + li;
                         double m = 0.0;
                         if (k < nn) {
-                            const cx vv = ldx(SL, p * nn + k);
+                            const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + (k - 1) * SROW + sc);
                             m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
                         }
                         const bool nz = k < nn && m != 0.0;
@@ -759,7 +754,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
         for (int k = li; k < nn; k += L) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const cx vv = ldx(SL, p * nn + k);
+                const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + (k - 1) * SROW + sc);
                 const double m2 = fma(vv.re, vv.re, vv.im * vv.im);
                 mn = fmin(mn, m2);
                 mx = fmax(mx, m2);
@@ -814,7 +809,9 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 #pragma unroll
             for (int u = 0; u < UV; ++u) {
                 const int i = i0 + u * NT + (int)threadIdx.x;
-                vv[u] = i < total ? reg0[(i % SPB) * RS + i / SPB] : make_double2(0.0, 0.0);
+                const int j = i % SPB, r = i / SPB, p = r / nn, k = r - p * nn;
+                vv[u] = i >= total ? make_double2(0.0, 0.0)
+                                   : (k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + (k - 1) * SROW + j]);
             }
 #pragma unroll
             for (int u = 0; u < UV; ++u) {
@@ -844,7 +841,7 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
                     a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
                 }
             }
-            double *sh = (double *)reg0;   // [8][NT] (the regions are dead)
+            double *sh = (double *)stg;   // [8][NT] (STG and the regions are dead)
 #pragma unroll
             for (int q = 0; q < 8; ++q) sh[q * NT + threadIdx.x] = a[q];
             __syncthreads();
@@ -868,11 +865,11 @@ __global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_k
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * ((3 * w.C * L + 3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 3) | 1);
-    const size_t stage = 8 * 6 * (size_t)w.nl * (spb + 1);           // the loads, staged over the regions
+    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 3) | 1);
+    const size_t stage = 16 * 3 * ((size_t)w.nl + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
     const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
-    return temp + pairs + std::max(regions, std::max(stage, agg));
+    return temp + pairs + std::max(stage + regions, agg);
 }
 
 int wave_scenarios_per_block(const WaveDev &w) { return w.wpb * w.spw; }
