@@ -208,7 +208,9 @@ constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deepe
 template <int SPW, int C>
 struct WaveGeom {
     static constexpr int L = 64 / SPW;                 // lanes per scenario
-    static constexpr int MINW = SPW * C <= 2 ? 4 : 2;  // waves per SIMD the registers allow
+    // waves per SIMD the registers allow (light outputs; the full-output variants of
+    // the larger geometries keep 2 and their registers)
+    static constexpr int MINW = SPW * C <= 2 ? 4 : (C <= 2 ? 3 : 2);
 };
 
 // the TEMP blocks are staged in LDS once per workgroup (a diagnostic build
@@ -250,7 +252,7 @@ __device__ __forceinline__ int xcd_tile(int b, int G) {
 }
 
 template <int SPW, int C, bool FULL, int WPB>
-__global__ __launch_bounds__(WPB * 64, (WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
+__global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
     constexpr int L = WaveGeom<SPW, C>::L, SPB = WPB * SPW;
     constexpr int NT = WPB * 64;
