@@ -1155,6 +1155,36 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         if (q > 0 && fw_dev[q].src >= 0 && fw_dev[q].src == fw_dev[q - 1].dst) fw_dev[q].pad = 1;
     }
     const size_t o_fw = push_blob(blob, fw_dev);
+    // generic kernel: the launch-time initialisation it can skip (FeederDev)
+    std::vector<int32_t> il_zero, ib_zero;
+    int v_init = 0;
+    {
+        const int nn = h.nn;
+        std::vector<char> il_w(nn, 0), ib_w(nn > 1 ? nn - 1 : 1, 0), v_w(nl, 0);
+        for (const auto &op : h.il)
+            if (op.ndr - 1 >= 0 && op.ndr - 1 < nn) il_w[op.ndr - 1] = 1;
+        for (const auto &op : h.bw)
+            if (op.idx >= 0 && op.idx < (int)ib_w.size()) ib_w[op.idx] = 1;
+        for (int k = 0; k < nn; ++k)
+            if (!il_w[k]) il_zero.push_back(k);
+        for (int k = 0; k < nn - 1; ++k)
+            if (!ib_w[k]) ib_zero.push_back(k);
+        // V: a forward source must have been written earlier in the list (else sweep
+        // 0 reads V0 there); every V a load current or the post-processing reads
+        // (nodes 1..nn-1) must have a forward writer
+        for (const auto &op : h.fw) {
+            if (op.src >= 0 && !v_w[op.src]) v_init = 1;
+            if (op.dst >= 0 && op.dst < nl) v_w[op.dst] = 1;
+        }
+        for (const auto &op : h.il)
+            if (op.ndr < 0 || op.ndr >= nl || !v_w[op.ndr]) v_init = 1;
+        for (int k = 1; k < nn; ++k)
+            if (k >= nl || !v_w[k]) v_init = 1;
+        if (nl > 0 && v_w[0]) v_init = 1;   // V(0) is stored once as V0 when v_init = 0
+    }
+    if (il_zero.empty()) il_zero.push_back(-1);
+    if (ib_zero.empty()) ib_zero.push_back(-1);
+    const size_t o_ilz = push_blob(blob, il_zero), o_ibz = push_blob(blob, ib_zero);
     const size_t o_node = push_blob(blob, h.node);
     const size_t o_node_rtc = push_blob(blob, h.node_rtc);
     const size_t o_sbw = push_blob(blob, h.seq_bw);
@@ -1195,6 +1225,11 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     d.il_ops = (const IlOp *)(base + o_il);
     d.bw_ops = (const BwOp *)(base + o_bw);
     d.bw_il = (const IlOp *)(base + o_bwil);
+    d.il_zero = (const int32_t *)(base + o_ilz);
+    d.ib_zero = (const int32_t *)(base + o_ibz);
+    d.n_il_zero = il_zero[0] < 0 ? 0 : (int)il_zero.size();
+    d.n_ib_zero = ib_zero[0] < 0 ? 0 : (int)ib_zero.size();
+    d.v_init = getenv("FPF_GENERIC_VINIT") ? 1 : v_init;
     d.fw_ops = (const FwOp *)(base + o_fw);
     d.node_ops = (const NodeOp *)(base + o_node);
     d.seq_bw = (const SeqBw *)(base + o_sbw);

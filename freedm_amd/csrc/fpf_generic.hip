@@ -276,19 +276,24 @@ __global__ __launch_bounds__(256) void dpf_generic3_kernel(FeederDev f, int B, c
     const int nl = f.nl, nn = f.nn;
     const size_t ld3 = 3 * ld;
     const int i3 = 3 * s + p;
-    const Slots3 Sld{scr, ld3, i3};
     const Slots3 V{scr + (size_t)nl * 2 * ld3, ld3, i3};
     const Slots3 IL{scr + (size_t)nl * 4 * ld3, ld3, i3};
     const Slots3 Ib{scr + (size_t)(2 * nl + nn) * 2 * ld3, ld3, i3};
     const cx v0 = mk(f.V0[2 * p], f.V0[2 * p + 1]);
+    // Sld(row) = (P + jQ) / (bkva/3) (:46-50), read from the caller's loads at every
+    // use (the same division, the same bits) instead of a scratch copy
+    const double *const pP = pq + (size_t)(2 * p) * nl * B + s, *const pQ = pP + (size_t)nl * B;
+    auto Sld = [&](int row) { return cdiv(mk(pP[(size_t)row * B], pQ[(size_t)row * B]), mk(f.s3, 0.0)); };
 
-    for (int j = 0; j < nl; ++j) {   // :46-50, :92-96
-        const cx sl = mk(pq[((size_t)(2 * p) * nl + j) * B + s], pq[((size_t)(2 * p + 1) * nl + j) * B + s]);
-        Sld.st(j, cdiv(sl, mk(f.s3, 0.0)));
-        V.st(j, v0);
+    // V(0..Nl-1) = V0 (:92-96): only where a read could see it (FeederDev.v_init)
+    if (f.v_init) {
+        for (int j = 0; j < nl; ++j) V.st(j, v0);
+    } else {
+        V.st(0, v0);
     }
-    for (int k = 0; k < nn; ++k) IL.st(k, mk(0, 0));
-    for (int k = 0; k < nn - 1; ++k) Ib.st(k, mk(0, 0));
+    // IL and Ib slots no op writes stay 0 (the ops rewrite all the others)
+    for (int q = 0; q < f.n_il_zero; ++q) IL.st(f.il_zero[q], mk(0, 0));
+    for (int q = 0; q < f.n_ib_zero; ++q) Ib.st(f.ib_zero[q], mk(0, 0));
     cx ibo = mk(0, 0);
     int iters = 0, status = 1;
     auto store_il = [&]() {
@@ -298,23 +303,26 @@ __global__ __launch_bounds__(256) void dpf_generic3_kernel(FeederDev f, int B, c
             cx sl[4], vv[4];
             for (int u = 0; u < 4; ++u) {
                 op[u] = f.il_ops[q + u];
-                sl[u] = Sld.ld_(op[u].row);
+                sl[u] = Sld(op[u].row);
                 vv[u] = V.ld_(op[u].ndr);
             }
             for (int u = 0; u < 4; ++u) IL.st(op[u].ndr - 1, load_current(sl[u], vv[u]));
         }
         for (; q < f.n_il; ++q) {
             const IlOp op = f.il_ops[q];
-            IL.st(op.ndr - 1, load_current(Sld.ld_(op.row), V.ld_(op.ndr)));
+            IL.st(op.ndr - 1, load_current(Sld(op.row), V.ld_(op.ndr)));
         }
     };
     for (int it = 0; it < f.mxitr; ++it) {
         // backward sweep :134-160 (as dpf_generic_kernel, one phase per lane)
         cx ibl = mk(0, 0);
+        // sweep 0 of a feeder without the V0 fill: every load current sees V0
+        const bool vconst = it == 0 && !f.v_init;
+        auto vload = [&](int ndr) { return vconst ? v0 : V.ld_(ndr); };
         if (f.n_bw > 0) {
             BwOp op = f.bw_ops[0];
             IlOp w = f.bw_il[0];
-            cx sl = w.row < 0 ? mk(0, 0) : Sld.ld_(w.row), vv = w.row < 0 ? mk(0, 0) : V.ld_(w.ndr);
+            cx sl = w.row < 0 ? mk(0, 0) : Sld(w.row), vv = w.row < 0 ? mk(0, 0) : vload(w.ndr);
             for (int q = 0; q < f.n_bw; ++q) {
                 const bool more = q + 1 < f.n_bw;
                 BwOp nx = op;
@@ -323,8 +331,8 @@ __global__ __launch_bounds__(256) void dpf_generic3_kernel(FeederDev f, int B, c
                     nx = f.bw_ops[q + 1];
                     const IlOp wn = f.bw_il[q + 1];
                     if (wn.row >= 0) {
-                        nsl = Sld.ld_(wn.row);
-                        nvv = V.ld_(wn.ndr);
+                        nsl = Sld(wn.row);
+                        nvv = vload(wn.ndr);
                     }
                 }
                 const bool has_il = f.bw_il[q].row >= 0;

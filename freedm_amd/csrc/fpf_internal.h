@@ -107,6 +107,12 @@ struct FeederDev {
     int32_t temp_lds;        // specialised layout: TEMP blocks staged in LDS
     const IlOp *bw_il;       // generic only, [n_bw]: the load-current op whose IL the
                              // branch op reads (the slot's last writer), row < 0: none
+    // generic kernel, what a launch must initialise: the IL / Ib slots no op ever
+    // writes (zeroed once), and whether V needs its V0 fill (v_init = 0: every V
+    // read is of a slot a forward op wrote earlier in the sweep or in the last
+    // sweep, so only V(0) is stored and sweep 0's load currents use V0)
+    int32_t n_il_zero, n_ib_zero, v_init;
+    const int32_t *il_zero, *ib_zero;
 };
 
 // Wave kernel (fpf_wave.hip, fast mode): SPW scenarios per wavefront, one

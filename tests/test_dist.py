@@ -76,3 +76,26 @@ def test_world2_gloo_study_aggregate():
         np.testing.assert_array_equal(g[1:], ref[1:])
         assert g[0] == pytest.approx(ref[0], rel=1e-13)
     assert got[0][7] == N_STUDY and got[0][3] + got[0][4] == N_STUDY
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_share_one_gpu():
+    """bench.py's multi-rank path with the HIP kernels: 2 ranks over gloo on the
+    box's GPU (ranks beyond the visible GPUs share them); the study aggregate
+    covers both ranks' shards."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FPF_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--no-c4", "--no-cpu-baseline", "--in-batches", "1"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2
+    agg = d["aggregate"]
+    assert agg["n_scen"] == 2 * 3 * 4096 and agg["n_conv"] == agg["n_scen"]
