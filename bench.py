@@ -162,7 +162,7 @@ def _cpu_model():
     return "unknown"
 
 
-def _pmc_traffic(workload: str, key: str = "hbm_bytes_per_launch"):
+def _pmc_traffic(workload: str, kernel: str | None = None, key: str = "hbm_bytes_per_launch"):
     """Per-launch HBM bytes of the dominant kernel for `workload` ("123-bus x
     4096") from the committed rocprofv3 --pmc summaries
     (profiles/pmc_traffic.json, tools/pmc_summary.py), or None: the guide's
@@ -173,6 +173,8 @@ def _pmc_traffic(workload: str, key: str = "hbm_bytes_per_launch"):
         e = d.get("by_workload", {}).get(workload)
         if e is None and d.get("workload") == workload:
             e = d
+        if e and kernel and e.get("kernel") != kernel:
+            return None   # measured on another kernel
         return e.get(key) if e else None
     except (OSError, ValueError, AttributeError):
         return None
@@ -357,12 +359,20 @@ def main():
     nb, nn = pf.info["nb"], pf.nn
     bpa = bytes_alg_per_scenario(nb, nn)
     k_sum = float(res["iters"][:args.steps].sum().item())
-    if args.config == 3:
+    # the dominant kernel: fast mode runs the wave kernel (<= 256 branches) or the
+    # wave-block kernel (257..2048, one scenario per workgroup), both with the
+    # state on chip; exact mode the tiled or the generic kernel
+    kname = {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
+             "wave": "dpf_wave_kernel" if nb <= 256 else "dpf_wblk_kernel", "generic": "dpf_generic3_kernel"}[pf.kernel]
+    if pf.kernel == "generic":
+        # the state streams through HBM every sweep (SURVEY 8(d) config 3 model)
         bytes_launch = bytes_alg_streaming(nb, nn, k_sum / args.steps, B)
+        model = "streaming (state through HBM every sweep)"
     else:
         bytes_launch = bpa * B
+        model = "state-resident (loads in, V and scalars out)"
     achieved = bytes_launch / avg_kern_s / 1e9
-    traffic = _pmc_traffic(f"{n_nodes}-bus x {B}")
+    traffic = _pmc_traffic(f"{n_nodes}-bus x {B}", kname)
     # algorithmic fp64 flops per scenario = 123 Nb k_s + 60 Nn, over
     # the timed launches, against the 78.6 TFLOP/s fp64 vector peak
     flops = 123.0 * nb * k_sum + 60.0 * nn * B * args.steps
@@ -388,9 +398,7 @@ def main():
                        "tile": pf.info["tile"], "specialized": pf.info["specialized"], "exact": bool(args.exact),
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
-                                    "wave": "dpf_wave_kernel", "generic": "dpf_generic_kernel"}[pf.kernel],
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "model": model,
                          "bytes_alg_per_scenario": bytes_launch / B, "kernel_ms": avg_kern_s * 1e3,
                          "fp64": {"achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": fp64_tflops / FP64_PEAK_TFLOPS,

@@ -385,17 +385,24 @@ struct WaveHost {
     int n = 0, spw = 0, C = 0, nblk = 0, bdepth = 0, ncomp = 0, has_rel = 0, has_mask = 0, wpb = 0, off_in_x = 0;
     int temp_sym = 0;
     int wpb_big_batch = 0;
+    int wps = 0;                     // wave-block kernel: wavefronts per scenario (0: per-wavefront kernel)
     std::vector<int32_t> row, node, info, blk, mref, pairs;
     std::vector<double> temp;
+    std::vector<double> lng, code_z;   // wave-block kernel: per slot lng, per code Zl (fpf_internal.h)
+    std::vector<int32_t> code;
 };
 
 void analyse_wave(const HostFeeder &h, WaveHost &w) {
     auto no = [&](const std::string &why) { w.ok = false; w.why = why; };
     if (!h.wf) return no("not well formed: " + h.wf_why);
     const int nl = h.nl, nn = h.nn, n = nn - 1;
-    int spw = 0, C = 0;
-    if (!wave_geometry(n, &spw, &C)) return no("more than 256 branches");
-    const int L = 64 / spw;
+    int spw = 0, C = 0, wps = 0;
+    if (!wave_geometry(n, &spw, &C)) {
+        // one scenario per workgroup of wps wavefronts (fpf_wblk.hip)
+        if (!wblk_geometry(n, &wps, &C)) return no("more than 2048 branches");
+        spw = 1;
+    }
+    const int L = wps ? 64 * wps : 64 / spw;
     std::vector<int> par(nn, -1), chain(nn, -1);
     std::vector<std::vector<int>> lat(nn);
     for (int m = 0; m < nl; ++m) {
@@ -434,6 +441,10 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     for (int q = n - 1; q > 0; --q) size[par[at[q]]] += size[at[q]];
     const int nblk = (int)bfirst.size();
     if (nblk > 511) return no("too many blocks");
+    if (wps) {
+        for (int k = 1; k < nn; ++k)
+            if (h.node[k].mask & 7) return no("wave-block kernel: zeroed phases (the generic kernel runs them)");
+    }
     // nearest zeroed proper ancestor per (node, phase)
     std::vector<std::array<int, 3>> mref(nn, {-1, -1, -1});
     int has_rel = 0, has_mask = 0;
@@ -538,11 +549,13 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
             if (comp[q] >= 0) comp[q] = renum[comp[q]];
         ncomp = top;   // holes allowed
     };
-    color_space(cb, nb_c, true);
-    color_space(cf, nf_c, false);
+    if (!wps) {   // (the bank colouring assumes one scenario within a wavefront)
+        color_space(cb, nb_c, true);
+        color_space(cf, nf_c, false);
+    }
     // entry ncomp of X is the permanent zero; in the common case the block
     // offsets are stored over X's first nblk entries (off_in_x, fpf_wave.hip)
-    const bool off_in_x = nblk <= L && maxd <= 4;   // = the kernel's register-resolved path (WAVE_BD)
+    const bool off_in_x = !wps && nblk <= L && maxd <= 4;   // = the kernel's register-resolved path (WAVE_BD)
     const int ncomp = std::max(std::max(nb_c, nf_c), off_in_x ? nblk : 0);
     if (ncomp > 510) return no("too many gathered positions");
     // off(b) = sum over b's block-ancestor chain of Ginc[tap] - Ginc[first - 1]
@@ -605,6 +618,34 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
         w.temp.swap(ts);
     }
     w.temp_sym = sym ? 1 : 0;
+    if (wps) {
+        // TEMP = lng * Zl(code), factorised (fpf_wblk.hip): per slot lng and code,
+        // per code Zl -- sym: every code's Zl has one common off-diagonal value
+        w.temp.clear();
+        w.lng.assign(S, 0.0);
+        w.code.assign(S, 0);
+        bool zsym = !getenv("FPF_WAVE_NO_SYM");
+        for (int q = 0; q < n; ++q) {
+            const int k = at[q], i = (q % C) * L + q / C;
+            const NodeOp &nd = h.node[k];
+            w.lng[i] = h.at(nd.row, 4);
+            w.code[i] = nd.code;
+            const cx *z = &h.zl[(size_t)nd.code * 9];
+            for (int j = 1; j < 9 && zsym; ++j)
+                if (j % 4 != 0) zsym = z[j].re == z[1].re && z[j].im == z[1].im;
+        }
+        const int ntz = zsym ? 4 : 9;
+        w.code_z.assign((size_t)h.ncode * ntz * 2, 0.0);
+        for (int cd = 0; cd < h.ncode; ++cd) {
+            const cx *z = &h.zl[(size_t)cd * 9];
+            for (int j = 0; j < ntz; ++j) {
+                const cx v = !zsym ? z[j] : (j < 3 ? csub(z[4 * j], z[1]) : z[1]);
+                w.code_z[((size_t)cd * ntz + j) * 2] = v.re;
+                w.code_z[((size_t)cd * ntz + j) * 2 + 1] = v.im;
+            }
+        }
+        w.temp_sym = zsym ? 1 : 0;
+    }
     w.n = n;
     w.spw = spw;
     w.C = C;
@@ -614,6 +655,21 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     w.has_rel = has_rel;
     w.has_mask = has_mask;
     w.off_in_x = off_in_x ? 1 : 0;
+    w.wps = wps;
+    if (wps) {
+        WaveDev probe{};
+        probe.wps = wps;
+        probe.nl = nl;
+        probe.nblk = nblk;
+        probe.bdepth = bdepth;
+        probe.ncomp = ncomp;
+        probe.temp_sym = w.temp_sym;
+        probe.ncode = h.ncode;
+        if (wblk_lds_bytes(probe) > WAVE_LDS_BUDGET) return no("wave-block kernel: the scenario's loads exceed LDS");
+        w.wpb = w.wpb_big_batch = wps;
+        w.ok = true;
+        return;
+    }
     // waves per workgroup: the smaller workgroup when two of them fit in a CU's
     // LDS (each then stages its loads and writes its V while the other sweeps;
     // the registers allow 2 waves per SIMD = 8 per CU for these geometries),
@@ -1247,6 +1303,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         const size_t o_blk = push_blob(wb, wh.blk);
         const size_t o_mref = push_blob(wb, wh.mref);
         const size_t o_tmp = push_blob(wb, wh.temp), o_pairs = push_blob(wb, wh.pairs);
+        const size_t o_lng = push_blob(wb, wh.lng), o_code = push_blob(wb, wh.code), o_cz = push_blob(wb, wh.code_z);
         e = hipMalloc(&f->d_wave, wb.size());
         if (e == hipSuccess) e = hipMemcpy(f->d_wave, wb.data(), wb.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
@@ -1282,7 +1339,12 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.slot_mref = (const int32_t *)(wbase + o_mref);
         w.slot_temp = (const double *)(wbase + o_tmp);
         w.blk_pairs = (const int32_t *)(wbase + o_pairs);
-        if (wave_lds_bytes(w) > WAVE_LDS_BUDGET) {
+        w.wps = wh.wps;
+        w.ncode = h.ncode;
+        w.slot_lng = (const double *)(wbase + o_lng);
+        w.slot_code = (const int32_t *)(wbase + o_code);
+        w.code_z = (const double *)(wbase + o_cz);
+        if ((w.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w)) > WAVE_LDS_BUDGET) {
             fpf_feeder_destroy(f);
             return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
         }
@@ -1492,7 +1554,7 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     if ((d_vsrc || d_s_in) && kern != FPF_KERNEL_WAVE)
         return fail(ctx, FPF_ERR_UNSUPPORTED, "per-scenario source voltages need the wave kernel");
     if (kern == FPF_KERNEL_WAVE) {
-        e = launch_wave(wave_dev_for(f, n_scen), n_scen, d_pq, o, st);
+        e = f->wdev.wps ? launch_wblk(f->wdev, n_scen, d_pq, o, st) : launch_wave(wave_dev_for(f, n_scen), n_scen, d_pq, o, st);
     } else if (kern == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {
             std::string err;
@@ -1654,7 +1716,10 @@ extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const d
     w.wpb = wh.wpb;
     w.off_in_x = wh.off_in_x;
     w.temp_sym = wh.temp_sym;
-    const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, wh.ok ? (int)wave_lds_bytes(w) : 0, wh.ncomp, wh.nblk, wh.bdepth};
+    w.wps = wh.wps;
+    w.ncode = h.ncode;
+    const int lds = !wh.ok ? 0 : (int)(wh.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w));
+    const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, lds, wh.ncomp, wh.nblk, wh.bdepth};
     std::memcpy(out, v, sizeof(v));
     return FPF_OK;
 }

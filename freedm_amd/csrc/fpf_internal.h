@@ -149,6 +149,15 @@ struct WaveDev {
     const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch, row-major
                                 // (l, a); temp_sym: [4][C][L] (z_aa - zm for a = 0..2, zm)
     const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) forward indices; pad = ncomp (zero)
+    // wave-block kernel (fpf_wblk.hip): one scenario per workgroup of wps
+    // wavefronts (L = 64 wps lanes, C slots per lane) for feeders of 257..2048
+    // branches; wps = 0: the per-wavefront kernel above.  TEMP = lng * Zl(code)
+    // factorised: per slot lng and code, per code Zl (temp_sym: z_aa - zm x 3, zm;
+    // else the 9 entries row-major (l, a))
+    int32_t wps, ncode;
+    const double *slot_lng;     // [C][L]
+    const int32_t *slot_code;   // [C][L] 0-based line code
+    const double *code_z;       // [ncode][4 or 9] complex
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -187,6 +196,9 @@ hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss
                             double *d_agg, double *partials, unsigned *ticket, hipStream_t st);
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wave_lds_bytes(const WaveDev &w);
+hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+size_t wblk_lds_bytes(const WaveDev &w);
+bool wblk_geometry(int n, int *wps, int *c);
 bool wave_geometry(int n, int *spw, int *c);
 int wave_scenarios_per_block(const WaveDev &w);
 bool wave_wpb_supported(int spw, int c, int wpb);

@@ -1,0 +1,504 @@
+// fpf_wblk.hip -- the wave-block kernel (fast mode, fpf_opts.exact = 0) for
+// feeders of 257..2048 branches (BASELINE config 3: the 2048-bus feeder): every
+// sweep of DPF_return7 (Broker/src/vvc/DPF_return7.cpp:104-217) as data-parallel
+// work over one workgroup of W wavefronts per scenario.
+//
+// The per-wavefront wave kernel (fpf_wave.hip) holds a scenario in one segment
+// of a wavefront; a 2048-bus scenario needs W = 8 wavefronts (512 lanes x C = 4
+// slots).  The layout is the same: the feeder tree in the depth-first order that
+// keeps every subtree and every block contiguous, node at position q in slot
+// q % C of lane q / C (lane = the workgroup's thread id), V in registers for the
+// whole solve.  What changes:
+//   * the two prefix scans per sweep (the backward sweep's subtree sums of IL,
+//     :134-160; the forward sweep's path sums of the drops, :163-195) are a DPP
+//     scan inside each wavefront plus a scan of the W wavefront totals (through
+//     LDS, one barrier) that every wave computes alike, so Ib(0) and with it the
+//     convergence test (:199-217) are the same in every wave of the workgroup;
+//   * LDS holds the scenario's loads (Sld, 3 x (Nl + 1) complex, ~105 KB for
+//     2048 buses: one workgroup per CU, 8 wavefronts = 2 per SIMD), the gathered
+//     scan values, the block offsets and the per-code impedances;
+//   * TEMP = lng * Zl(code) is factorised: a slot keeps its branch's lng in a
+//     register and reads Zl of its line code from a small LDS table (the 2048
+//     per-slot TEMP blocks would not fit next to Sld), one real scaling per
+//     phase more than the wave kernel's precomputed TEMP;
+//   * scenario s = blockIdx.x in XCD-aware order (the workgroups one XCD runs
+//     take consecutive scenarios, so the [row][B] lines of pq and V that
+//     neighbouring scenarios share meet in that XCD's L2).
+// Feeders with zeroed phases (phase masks) run the generic kernel instead.
+//
+// Arithmetic: as the wave kernel (prefix sums instead of the sequential chains,
+// FMA products, one-reciprocal division, Sld scaled by 1/(bkva/3)), checked at
+// the north-star bar (1e-10 relative on V, identical iteration counts) against
+// the oracle and the exact generic kernel in tests/test_gpu_wblk.py.
+#include <array>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <set>
+
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+#include "fpf_wave_common.h"
+
+namespace fpf {
+
+namespace {
+constexpr int WB_C = 4;   // slots per lane
+
+// the wavefront totals [W][8] (6 used: re/im per phase) summed over the waves
+// before wave wv (pre) and over all waves (tot): lane j < W reads wave j's
+// totals, a DPP scan over those lanes, the sums read back as wave-uniform
+// values.  Every wave computes the same scan, so tot (Ib(0) in the backward
+// sweep) is the same in every wave of the workgroup.
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+    return __hiloint2double(hi, lo);
+}
+template <int W, bool TOT>
+__device__ __forceinline__ void wave_prefix(const double *wt, int wv, int lane, double (&pre)[6], double (&tot)[6]) {
+    const int j = lane < W ? lane : 0;
+    const double2 *t2 = (const double2 *)(wt + 8 * j);
+    const double2 a = t2[0], b = t2[1], c = t2[2];
+    double t[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+#pragma unroll
+    for (int q = 0; q < 6; ++q) t[q] = lane < W ? t[q] : 0.0;
+    if (W > 1) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x111, 0xf, 0xf>(t[q]);
+    }
+    if (W > 2) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x112, 0xf, 0xf>(t[q]);
+    }
+    if (W > 4) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x114, 0xf, 0xf>(t[q]);
+    }
+    const int wu = __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        pre[q] = wu == 0 ? 0.0 : readlane_d(t[q], wu - 1);
+        if (TOT) tot[q] = readlane_d(t[q], W - 1);
+    }
+}
+}  // namespace
+
+template <int W, bool FULL>
+__global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
+                                                             OutDev o) {
+    constexpr int C = WB_C, L = 64 * W, NT = 64 * W;
+    extern __shared__ double2 lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int s = xcd_tile(blockIdx.x, gridDim.x);   // this workgroup's scenario
+    const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
+    const int ntz = f.temp_sym ? 4 : 9, PS = nl + 1;
+    // LDS: Zl per code | Sld [3][Nl + 1] (row Nl = 0 for empty slots; node k's V
+    // over row k - 1 in the last sweep) | X [3][XC] gathered scan values (entry
+    // XC - 1 = 0) | block offsets [3][nblk] | V0 [3] (+1 pad) | wave totals
+    // [2][W][8] (backward, forward; entries 6, 7: loss, Vmin, Vmax) | block chains
+    double2 *const zc = lds;
+    double2 *const stg = zc + f.ncode * ntz;
+    double2 *const X = stg + 3 * PS;
+    double2 *const OFF = X + 3 * XC;
+    double2 *const V0S = OFF + 3 * nblk;
+    double *const wtb = (double *)(V0S + 4);
+    double *const wtf = wtb + 8 * W;
+    int *const pairs = (int *)(wtf + 8 * W);   // [bdepth][2][nblk]
+
+    // ---- the scenario's loads P/Q [6][Nl] (column s of pq) into Sld scaled by
+    // 1/(bkva/3) (DPF_return7.cpp:46-50), all of a thread's loads in flight
+    {
+        const double inv_s3 = 1.0 / f.s3;
+        double *const sd = (double *)stg;
+        const int total = 6 * nl;
+        constexpr int U = 8;
+        for (int i0 = 0; i0 < total; i0 += U * NT) {
+            double r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT + tid;
+                r[u] = pq[(size_t)(i < total ? i : 0) * B + s];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT + tid;
+                if (i < total) {
+                    const int fq = i / nl, rr = i - fq * nl;
+                    sd[2 * ((fq >> 1) * PS + rr) + (fq & 1)] = r[u] * inv_s3;
+                }
+            }
+        }
+        for (int i = tid; i < f.ncode * ntz; i += NT) zc[i] = ld_global2(f.code_z, i);
+        for (int i = tid; i < 2 * bdepth * nblk; i += NT) pairs[i] = f.blk_pairs[i];
+        if (tid < 3) {
+            stg[tid * PS + nl] = make_double2(0.0, 0.0);
+            X[tid * XC + XC - 1] = make_double2(0.0, 0.0);
+            // the source voltage: V0 (:84-89), or this scenario's (an area of the
+            // multi-area solve, fed from its boundary bus)
+            double2 v0 = tid == 0 ? make_double2(f.V0[0], f.V0[1])
+                                  : (tid == 1 ? make_double2(f.V0[2], f.V0[3]) : make_double2(f.V0[4], f.V0[5]));
+            if (o.vsrc) v0 = make_double2(o.vsrc[(size_t)(2 * tid) * B + s], o.vsrc[(size_t)(2 * tid + 1) * B + s]);
+            V0S[tid] = v0;
+        }
+    }
+    int si[C], sb[C], bk[C], cz[C];
+    double lg[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int r = f.slot_row[c * L + tid];
+        sb[c] = r < 0 ? nl : r;
+        si[c] = f.slot_info[c * L + tid];
+        bk[c] = f.slot_blk[c * L + tid];
+        cz[c] = f.slot_code[c * L + tid] * ntz;
+        lg[c] = f.slot_lng[c * L + tid];
+    }
+    __syncthreads();
+
+    cx v[C][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const cx v0 = ldx(V0S, p);
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c][p] = v0;   // V(0..Nl-1) = V0  (:92-96)
+    }
+    cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    int it = 0;
+    bool conv = false;
+    for (;; ++it) {
+        // ---- load currents (:106-130)
+        cx il[C][3], ib[C][3];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<false>(ldx(stg, p * PS + sb[c]), v[c][p]);
+
+        // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of
+        // IL: lane-local prefix, wavefront scan, the totals of the waves before
+        double sc6[6], pre[6], tot6[6];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = il[0][p];
+            ib[0][p] = acc;
+#pragma unroll
+            for (int c = 1; c < C; ++c) { acc = cadd(acc, il[c][p]); ib[c][p] = acc; }
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<64>(sc6);
+        if (lane == 63) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) wtb[8 * wv + q] = sc6[q];
+        }
+        __syncthreads();
+        wave_prefix<W, true>(wtb, wv, lane, pre, tot6);
+        cx tot[3], exl[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx inc = mk(pre[2 * p] + sc6[2 * p], pre[2 * p + 1] + sc6[2 * p + 1]);
+            tot[p] = mk(tot6[2 * p], tot6[2 * p + 1]);   // Ib(0): every wave sums the same totals in the same order
+            exl[p] = csub(inc, ib[C - 1][p]);              // the lane's exclusive prefix
+#pragma unroll
+            for (int c = 0; c < C; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // Einc at this slot
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int ci = si_store_b(si[c]);
+            if (ci >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            // Ib = Einc[last] - Eexc; Eexc of slot c = Einc of slot c-1, of slot 0 the lane's prefix
+            cx eprev = exl[p];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const cx e = ib[c][p];
+                ib[c][p] = csub(ldx(X, p * XC + si_last(si[c])), eprev);
+                eprev = e;
+            }
+        }
+
+        // ---- convergence on the substation branch (:199-217), compared as squares;
+        // the same in every lane of the workgroup
+        double err2 = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const double dr = tot[p].re - ibo[p].re, di = tot[p].im - ibo[p].im;
+            err2 = fmax(err2, fma(dr, dr, di * di));
+            ibo[p] = tot[p];
+        }
+        conv = __builtin_amdgcn_readfirstlane(err2 < f.eps * f.eps ? 1 : 0) != 0;
+        const bool fin = conv || it == f.mxitr - 1;
+
+        // ---- branch drops lng * (Ib . Zl) (:163-178); in the last sweep also
+        // Re(drop . conj(Ib)) per phase for the VVC loss (fpf_wave.hip: the loss identity)
+        cx g[C][3];
+        double lp[3] = {0.0, 0.0, 0.0};
+        if (f.temp_sym) {
+            // one common off-diagonal zm: (Ib . Zl)_a = (z_aa - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const cx m = ldx(zc, cz[c] + 3);
+                const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
+                const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx d = ldx(zc, cz[c] + a);
+                    const cx b = ib[c][a];
+                    g[c][a] = mk(lg[c] * fma(d.re, b.re, fma(-d.im, b.im, ms.re)),
+                                 lg[c] * fma(d.re, b.im, fma(d.im, b.re, ms.im)));
+                    if (fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                cx tm[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) tm[j] = ldx(zc, cz[c] + j);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx t = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
+                    g[c][a] = mk(lg[c] * t.re, lg[c] * t.im);
+                    if (fin) lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
+                }
+            }
+        }
+
+        // ---- forward sweep (:163-195): V = V0 - A, A = Ginc + off(block)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = g[0][p];
+#pragma unroll
+            for (int c = 1; c < C; ++c) { acc = cadd(acc, g[c][p]); g[c][p] = acc; }
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<64>(sc6);
+        if (lane == 63) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) wtf[8 * wv + q] = sc6[q];
+        }
+        __syncthreads();
+        wave_prefix<W, false>(wtf, wv, lane, pre, tot6);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx ex = csub(mk(pre[2 * p] + sc6[2 * p], pre[2 * p + 1] + sc6[2 * p + 1]), g[C - 1][p]);
+#pragma unroll
+            for (int c = 0; c < C; ++c) g[c][p] = cadd(ex, g[c][p]);   // Ginc at this slot
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int ci = si_store_f(si[c]);
+            if (ci >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+            }
+        }
+        __syncthreads();
+        // block offsets, one thread per block, stored as V0 - off(b): off(b) = sum over
+        // b's block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
+        for (int b = tid; b < nblk; b += NT) {
+            cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+            for (int j = 0; j < bdepth; ++j) {
+                const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) v[c][p] = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
+
+        if (fin) {
+            // ---- the last sweep: V of node k over Sld row k - 1 (every Sld read of
+            // this sweep is behind the barriers above), the full outputs, and the
+            // wave's part of the VVC loss (VoltVarCtrl.cpp:1152-1161)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (si_valid(si[c])) {
+                    const int k = f.slot_node[c * L + tid];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        stx(stg, p * PS + k - 1, v[c][p]);
+                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                    }
+                }
+            }
+            const double x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
+            if (lane == 63) wtb[8 * wv + 6] = x;
+            break;
+        }
+    }
+    __syncthreads();
+
+    // ---- Vmin/Vmax (V_abc_list.cpp:7-81, VoltVarCtrl.cpp:1201-1207): no zeroed
+    // phases, so every Lnum_p + 1 = Nn and V_abc_list keeps every row -- the plain
+    // extremes of |V| (|V|^2 compared, one sqrt each)
+    {
+        double mn = INFINITY, mx = -INFINITY;
+        for (int k = tid; k < nn; k += NT) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PS + k - 1);
+                const double m2 = fma(vv.re, vv.re, vv.im * vv.im);
+                mn = fmin(mn, m2);
+                mx = fmax(mx, m2);
+            }
+        }
+        mn = seg_reduce_min<64>(mn);
+        mx = seg_reduce_max<64>(mx);
+        if (lane == 63) {
+            wtf[8 * wv + 6] = mn;
+            wtf[8 * wv + 7] = mx;
+        }
+    }
+    __syncthreads();
+
+    // ---- per-scenario results and the fused batch aggregate [loss_sum, vmin, vmax,
+    // n_conv, n_nonconv, n_over, n_under, n_scen]: the scenario's partial, published
+    // with agent-scope stores; one ticket per workgroup; the last to arrive folds
+    // the partials in scenario order (deterministic)
+    __shared__ int last_wg;
+    const bool agg = o.agg != nullptr;
+    if (tid == 0) {
+        double x = 0.0, mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            x += wtb[8 * w + 6];
+            mn = fmin(mn, wtf[8 * w + 6]);
+            mx = fmax(mx, wtf[8 * w + 7]);
+        }
+        x *= f.s3;
+        mn = sqrt(mn);
+        mx = sqrt(mx);
+        if (o.iters) o.iters[s] = it + 1;
+        if (o.status) o.status[s] = conv ? 0 : 1;
+        if (o.loss) o.loss[s] = x;
+        if (o.vmin) o.vmin[s] = mn;
+        if (o.vmax) o.vmax[s] = mx;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx v0p = ldx(V0S, p);
+            // substation row 0: V0, Ib(0) = the last sweep's total, no load
+            if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0p, mk(0, 0), ibo[p]);
+            if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
+                const cx sbv = cmul(cmul(v0p, mk(f.s3, 0.0)), cconj(ibo[p]));
+                o.s_in[(size_t)(2 * p) * B + s] = sbv.re;
+                o.s_in[(size_t)(2 * p + 1) * B + s] = sbv.im;
+            }
+        }
+        if (agg) {
+            const double part[8] = {conv ? x : 0.0, conv ? mn : INFINITY, conv ? mx : -INFINITY, conv ? 1.0 : 0.0,
+                                    conv ? 0.0 : 1.0, conv && mx > f.ub_v ? 1.0 : 0.0, conv && mn < f.lb_v ? 1.0 : 0.0,
+                                    1.0};
+            double *dst = o.partials + 8 * (size_t)s;
+            for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_wg = t == gridDim.x - 1;
+        }
+    }
+    // ---- V out: [3][Nn][B] re / im planes, column s
+    if (!FULL && (o.v_re || o.v_im)) {
+        for (int i = tid; i < 3 * nn; i += NT) {
+            const int p = i / nn, k = i - p * nn;
+            const double2 vv = k == 0 ? V0S[p] : stg[p * PS + k - 1];
+            if (o.v_re) o.v_re[(size_t)i * B + s] = vv.x;
+            if (o.v_im) o.v_im[(size_t)i * B + s] = vv.y;
+        }
+    }
+    if (agg) {
+        __syncthreads();
+        if (last_wg) {
+            // thread i folds scenarios i, i + NT, ... in order, then a fixed tree
+            double a[8] = {0, INFINITY, -INFINITY, 0, 0, 0, 0, 0};
+            for (unsigned b = tid; b < gridDim.x; b += NT) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const double r = __hip_atomic_load(o.partials + 8 * (size_t)b + q, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                    a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
+                }
+            }
+            double *sh = (double *)stg;   // [8][NT] (Sld / V and the rest are dead; wblk_lds_bytes covers it)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sh[q * NT + tid] = a[q];
+            __syncthreads();
+            for (int w = NT / 2; w > 0; w >>= 1) {
+                if (tid < w) {
+                    sh[0 * NT + tid] += sh[0 * NT + tid + w];
+                    sh[1 * NT + tid] = fmin(sh[1 * NT + tid], sh[1 * NT + tid + w]);
+                    sh[2 * NT + tid] = fmax(sh[2 * NT + tid], sh[2 * NT + tid + w]);
+#pragma unroll
+                    for (int q = 3; q < 8; ++q) sh[q * NT + tid] += sh[q * NT + tid + w];
+                }
+                __syncthreads();
+            }
+            if (tid < 8) o.agg[tid] = sh[tid * NT];
+            if (tid == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+size_t wblk_lds_bytes(const WaveDev &w) {
+    const size_t ntz = w.temp_sym ? 4 : 9, xc = (size_t)w.ncomp + 1, nt = 64 * (size_t)w.wps;
+    const size_t zc = 16 * (size_t)w.ncode * ntz;
+    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk + 4) + 8 * 16 * (size_t)w.wps +
+                        4 * 2 * (size_t)w.bdepth * w.nblk;
+    return zc + std::max(rest, 8 * 8 * nt);   // the last workgroup's fold reuses the space after zc
+}
+
+bool wblk_geometry(int n, int *wps, int *c) {
+    *c = WB_C;
+    for (int w = 2; w <= 8; w *= 2)
+        if (n <= 64 * w * WB_C) {
+            *wps = w;
+            return true;
+        }
+    return false;
+}
+
+namespace {
+typedef void (*WblkKernel)(WaveDev, int, const double *, OutDev);
+template <int W>
+WblkKernel pick_wblk(bool full) {
+    return full ? dpf_wblk_kernel<W, true> : dpf_wblk_kernel<W, false>;
+}
+}  // namespace
+
+hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
+    const bool full = o.vpolar || o.pqb || o.pql;
+    WblkKernel k = w.wps == 2 ? pick_wblk<2>(full) : (w.wps == 4 ? pick_wblk<4>(full) : (w.wps == 8 ? pick_wblk<8>(full) : nullptr));
+    if (!k || w.has_mask) return hipErrorInvalidValue;
+    // dynamic LDS above the default 64 KiB: a per-device setting, once per (device, variant)
+    static std::mutex mu;
+    static std::set<std::array<int, 3>> attr_done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        const std::array<int, 3> key = {dev, w.wps, (int)full};
+        if (!attr_done.count(key)) {
+            hipFuncAttributes fa{};
+            hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - (int)fa.sharedSizeBytes);
+            if (e != hipSuccess) return e;
+            attr_done.insert(key);
+        }
+    }
+    hipLaunchKernelGGL(k, dim3((unsigned)n_scen), dim3(64 * w.wps), wblk_lds_bytes(w), st, w, n_scen, pq, o);
+    return hipGetLastError();
+}
+
+}  // namespace fpf

@@ -53,8 +53,6 @@ def test_matches_golden(name, kernel, spec, exact):
     g = load_golden(name)
     if kernel == "tiled" and name == "g4_2048bus" and spec:
         pytest.skip("2048-bus: above the hipRTC size limit, covered by the interpreted tiled kernel")
-    if kernel == "wave" and name == "g4_2048bus":
-        pytest.skip("2048-bus: above the wave kernel's 256 branches")
     pf = _pf(g["Dl"], g["Z"], kernel=kernel, specialize=spec, exact=exact)
     assert pf.kernel == kernel
     if kernel == "tiled":
@@ -162,7 +160,9 @@ def test_auto_kernel_choice():
     assert _pf(g["Dl"], g["Z"]).kernel == "wave"            # fast mode (default)
     assert _pf(g["Dl"], g["Z"], exact=1).kernel == "tiled"  # the reference's roundings
     g4 = load_golden("g4_2048bus")
-    assert _pf(g4["Dl"], g4["Z"]).kernel == "generic"       # above the wave kernel's size, tile 1
+    pf4 = _pf(g4["Dl"], g4["Z"])                            # fast mode above 256 branches: the wave-block
+    assert pf4.kernel == "wave" and pf4.info["tile"] == 1    # kernel, one scenario per workgroup
+    assert _pf(g4["Dl"], g4["Z"], exact=1).kernel == "generic"   # exact: above the tiled kernel's size, tile 1
     f = F.demo_feeder()
     Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # 2->3 before 1->2: legal for the reference, not well formed
     pf = _pf(Dl, f.Z)
@@ -372,9 +372,9 @@ def test_track_counts_are_bit_identical(tracks, monkeypatch):
 
 
 def test_config3_full_size_against_oracle():
-    """BASELINE config 3 at its stated size: the 2048-bus feeder, 65 536
-    scenarios in one batch (auto kernel = the generic kernel at this batch
-    size).  The batch is built on the GPU from 1 024 seeded base scenarios
+    """BASELINE config 3 at its stated size in exact mode: the 2048-bus feeder,
+    65 536 scenarios in one batch (exact mode at this batch size = the generic
+    kernel; fast mode, the wave-block kernel, in tests/test_gpu_wblk.py).  The batch is built on the GPU from 1 024 seeded base scenarios
     (config-3 generator, seed 65536) times a per-scenario multiplier, so all
     65 536 differ; a strided sample of 65 scenarios is recomputed by the oracle
     with the same inputs: identical iteration counts and status, V bit-identical
@@ -389,7 +389,8 @@ def test_config3_full_size_against_oracle():
     s = np.arange(B, dtype=np.int64)
     mult = 0.9 + 0.2 * (((s * 2654435761) % 1000) / 1000.0)
     d_pq = torch.from_numpy(base).to(dev)[:, :, torch.from_numpy(s % NB).to(dev)] * torch.from_numpy(mult).to(dev)
-    pf = PowerFlow(f, device=0)
+    pf = PowerFlow(f, device=0, exact=1)
+    assert pf.kernel == "generic"
     nn = pf.nn
     out = {"v_re": torch.empty((3, nn, B), dtype=torch.float64, device=dev),
            "v_im": torch.empty((3, nn, B), dtype=torch.float64, device=dev),

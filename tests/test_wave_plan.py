@@ -34,13 +34,30 @@ def test_123bus_plan():
     assert p["ncomp"] <= 32 and p["bdepth"] <= 4
 
 
-@pytest.mark.parametrize("n", [9, 34, 65, 200, 257, 300])
+@pytest.mark.parametrize("n", [9, 34, 65, 200, 257, 300, 700, 1500, 2048, 2100])
 def test_plan_sizes(n):
-    """Every feeder of at most 256 branches gets a geometry whose L x C slots
-    hold its branches; above that the wave kernel declines."""
+    """Every feeder of at most 256 branches gets a per-wavefront geometry whose
+    L x C slots hold its branches; 257..2048 branches the wave-block kernel
+    (fpf_wblk.hip: one scenario per workgroup of wpb = 2, 4, 8 wavefronts, C = 4);
+    above that the wave kernels decline."""
     f = demo_feeder() if n == 9 else synthetic_feeder(n, n)
     nb = int((f.Dl[:, 0] != 0).sum())
     p = _plan(f)
-    assert p["ok"] == (1 if nb <= 256 else 0)
-    if p["ok"]:
+    assert p["ok"] == (1 if nb <= 2048 else 0)
+    if p["ok"] and nb <= 256:
         assert (64 // p["spw"]) * p["C"] >= nb and p["lds"] <= 159 * 1024
+    elif p["ok"]:
+        assert p["spw"] == 1 and p["C"] == 4 and p["wpb"] in (2, 4, 8)
+        assert 64 * p["wpb"] * 4 >= nb > 64 * (p["wpb"] // 2) * 4
+        assert p["lds"] <= 159 * 1024
+
+
+def test_2048bus_plan():
+    """BASELINE config 3's feeder: 8 wavefronts per scenario, the scenario's
+    loads (3 x (Nl + 1) complex) plus gathered scan values and block offsets in
+    one CU's LDS."""
+    f = synthetic_feeder(2048, 2048)
+    p = _plan(f)
+    assert p["ok"] == 1 and (p["spw"], p["C"], p["wpb"]) == (1, 4, 8)
+    assert 16 * 3 * (f.nl + 1) < p["lds"] <= 159 * 1024
+    assert p["ncomp"] <= 510 and p["nblk"] <= 511

@@ -1,6 +1,10 @@
 """Summarise a gpu_profile.sh run into profiles/<tag>/:
 
-    python tools/pmc_summary.py <tag> [kernel-name-substring]
+    python tools/pmc_summary.py <tag> [kernel-name-substring] [run-dir]
+
+(run-dir: a tools/gpu_wblk.sh-style directory holding prof/run_kernel_stats.csv,
+pmc_<COUNTER>/pmc_counter_collection.csv and the bench line bench_*.json;
+default: the gpu_profile.sh layout gpurun_out/prof_<tag>...)
 
 Copies the rocprofv3 kernel stats, and turns the separate FETCH_SIZE and
 WRITE_SIZE passes into per-launch HBM bytes of the dominant kernel, corrected
@@ -35,10 +39,18 @@ def main():
     out = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(out, f"prof_{tag}", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    bench = [ln for ln in open(os.path.join(out, f"prof_{tag}_bench.log")) if ln.startswith("{")]
-    fetch = per_launch(os.path.join(out, f"pmc_{tag}_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE", kname)
-    write = per_launch(os.path.join(out, f"pmc_{tag}_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE", kname)
+    if len(sys.argv) > 3:
+        run = sys.argv[3]
+        shutil.copy(os.path.join(run, "prof", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+        bfile = sorted(f for f in os.listdir(run) if f.startswith("bench") and f.endswith(".json"))[0]
+        bench = [ln for ln in open(os.path.join(run, bfile)) if ln.startswith("{")]
+        pmc = lambda c: os.path.join(run, f"pmc_{c}", "pmc_counter_collection.csv")
+    else:
+        shutil.copy(os.path.join(out, f"prof_{tag}", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+        bench = [ln for ln in open(os.path.join(out, f"prof_{tag}_bench.log")) if ln.startswith("{")]
+        pmc = lambda c: os.path.join(out, f"pmc_{tag}_{c}", "pmc_counter_collection.csv")
+    fetch = per_launch(pmc("FETCH_SIZE"), "FETCH_SIZE", kname)
+    write = per_launch(pmc("WRITE_SIZE"), "WRITE_SIZE", kname)
     b = json.loads(bench[-1]) if bench else {}
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
