@@ -41,6 +41,10 @@ FEEDER_NODES, FEEDER_SEED, SCEN_SEED = 123, 123, 4096
 CONFIGS = {2: (123, 123, 4096, 4096, "scenario"),
            3: (2048, 2048, 65536, 65536, "scenario"),
            4: (123, 123, 131072, 1 << 20, "hosting")}
+# batch layout each config is benched in (fpf_opts.layout; --layout overrides)
+# (measured, profiles/r02e_layout: config 3 17.5 -> 9.9 ms per launch and
+# config 4 1.14 -> 1.06 ms with [B][6][Nl]; config 2 39.4 vs 41.0 us)
+LAYOUT = {2: 0, 3: 1, 4: 1}
 
 
 def bytes_alg_per_scenario(nb: int, nn: int) -> int:
@@ -180,14 +184,15 @@ def _pmc_traffic(workload: str, kernel: str | None = None, key: str = "hbm_bytes
         return None
 
 
-def _loads_on_device(torch, dev, loads, feeder, ids, seed, chunk=8192):
+def _loads_on_device(torch, dev, loads, feeder, ids, seed, chunk=8192, layout=0):
     """[6][Nl][len(ids)] scenario loads of the global ids, generated on the host
     in chunks, scenario-fastest on the device."""
     out = torch.empty((6, feeder.nl, len(ids)), dtype=torch.float64, device=dev)
     for a in range(0, len(ids), chunk):
         b = min(len(ids), a + chunk)
         out[:, :, a:b] = torch.from_numpy(loads(feeder, ids[a:b], seed=seed)).to(dev)
-    return out
+    # FPF_LAYOUT_SCEN_MAJOR: [B][6][Nl], one scenario per contiguous block
+    return out if layout == 0 else out.permute(2, 0, 1).contiguous()
 
 
 def _copy_bandwidth(torch, dev, nbytes=1 << 30, reps=10):
@@ -216,8 +221,9 @@ def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
            "loss": torch.zeros(B, dtype=torch.float64, device=dev), "vmin": torch.zeros(B, dtype=torch.float64, device=dev),
            "vmax": torch.zeros(B, dtype=torch.float64, device=dev)}
     if want_v:
-        out.update(v_re=torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
-                   v_im=torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev))
+        sh = (B, 3, pf.nn) if pf.opts.layout == 1 else (3, pf.nn, B)
+        out.update(v_re=torch.zeros(sh, dtype=torch.float64, device=dev),
+                   v_im=torch.zeros(sh, dtype=torch.float64, device=dev))
     solve = pf.bind_device(d_pq, out, stream=stream)[0]
     for _ in range(warmup):
         solve()
@@ -244,6 +250,9 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-specialize", action="store_true")
     ap.add_argument("--exact", type=int, default=0, help="1: the reference's roundings (bit-identical mode)")
+    ap.add_argument("--layout", type=int, default=-1,
+                    help="batch layout: 0 [6][Nl][B] (scenario fastest), 1 [B][6][Nl] (scenario major); "
+                         "-1: the config's default (LAYOUT)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-v-out", action="store_true", help="diagnostic: do not request the V outputs")
@@ -279,8 +288,9 @@ def main():
         n_nodes, f_seed = args.nodes, args.nodes
     loads = {"scenario": scenario_loads, "hosting": hosting_loads}[model]
     feeder = synthetic_feeder(n_nodes, f_seed)
+    layout = LAYOUT[args.config] if args.layout < 0 else args.layout
     pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize,
-                   exact=args.exact)
+                   exact=args.exact, layout=layout)
     B = args.scenarios or b_cfg
     pf.reserve(B)
     from freedm_amd import dist as D
@@ -294,7 +304,7 @@ def main():
     for b in range(n_in):
         lo, hi = D.shard_range(rank, world, world * B)
         ids = np.arange(lo, hi) + b * world * B
-        d_pqs.append(_loads_on_device(torch, dev, loads, feeder, ids, s_seed))
+        d_pqs.append(_loads_on_device(torch, dev, loads, feeder, ids, s_seed, layout=layout))
     # per-scenario outputs of every timed step (the study's results); V is
     # overwritten step after step
     K = max(args.steps, 1)
@@ -303,8 +313,9 @@ def main():
            "loss": torch.zeros((K, B), dtype=torch.float64, device=dev),
            "vmin": torch.zeros((K, B), dtype=torch.float64, device=dev),
            "vmax": torch.zeros((K, B), dtype=torch.float64, device=dev)}
-    v_out = {} if args.no_v_out else {"v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
-                                      "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev)}
+    vsh = (B, 3, pf.nn) if layout == 1 else (3, pf.nn, B)
+    v_out = {} if args.no_v_out else {"v_re": torch.zeros(vsh, dtype=torch.float64, device=dev),
+                                      "v_im": torch.zeros(vsh, dtype=torch.float64, device=dev)}
     stream = torch.cuda.current_stream(dev)
     solves = [pf.bind_device(d_pqs[i % n_in], dict(v_out, **{k: t[i] for k, t in res.items()}), stream=stream)[0]
               for i in range(K)]
@@ -396,6 +407,7 @@ def main():
                        "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
                        "input_batches": n_in, "input_mib": n_in * batch_bytes / 2 ** 20,
                        "tile": pf.info["tile"], "specialized": pf.info["specialized"], "exact": bool(args.exact),
+                       "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][layout],
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "model": model,
@@ -414,9 +426,11 @@ def main():
             # one GPU's 131 072-scenario shard of the hosting study, 843 MB of inputs)
             n4, s4, b4, seed4, m4 = CONFIGS[4]
             ids4 = np.arange(b4)
-            d4 = _loads_on_device(torch, dev, hosting_loads, feeder, ids4, seed4)
-            pf.reserve(b4)
-            ms4, o4 = _kernel_ms(torch, pf, d4, b4, 5, 2, stream, dev)
+            lay4 = LAYOUT[4] if args.layout < 0 else args.layout
+            pf4 = PowerFlow(feeder, device=local, kernel=args.kernel, exact=args.exact, layout=lay4)
+            d4 = _loads_on_device(torch, dev, hosting_loads, feeder, ids4, seed4, layout=lay4)
+            pf4.reserve(b4)
+            ms4, o4 = _kernel_ms(torch, pf4, d4, b4, 5, 2, stream, dev)
             conv4 = int((o4["status"] == 0).sum().item())
             ach4 = bpa * b4 / (ms4 / 1e3) / 1e9
             res["roofline_config4"] = {
@@ -425,8 +439,10 @@ def main():
                 "traffic": _pmc_traffic(f"{n4}-bus x {b4}"),
                 "kernel_ms": ms4, "bytes_alg_per_scenario": bpa,
                 "converged_scenarios_per_s": conv4 / (ms4 / 1e3),
+                "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][lay4],
                 "mean_sweeps": float(o4["iters"].double().mean().item())}
             del d4
+            pf4.close()
             copy = _copy_bandwidth(torch, dev)
             res["hbm_copy_check"] = {"device_copy_gbs": copy, "spec_gbs": HBM_PEAK_GBS,
                                      "copy_frac_of_spec": copy / HBM_PEAK_GBS,

@@ -30,7 +30,8 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
 class FpfOpts(C.Structure):
     _fields_ = [("bkva", C.c_double), ("bkv", C.c_double), ("vo_kv", C.c_double), ("eps", C.c_double),
                 ("mxitr", C.c_int), ("kernel", C.c_int), ("lb_v", C.c_double), ("ub_v", C.c_double),
-                ("tile", C.c_int), ("specialize", C.c_int), ("exact", C.c_int), ("reserved", C.c_int * 5)]
+                ("tile", C.c_int), ("specialize", C.c_int), ("exact", C.c_int), ("layout", C.c_int),
+                ("reserved", C.c_int * 4)]
 
 
 class FpfFeederInfo(C.Structure):

@@ -73,6 +73,10 @@ struct fpf_feeder {
     hipEvent_t agg_event = nullptr;
     hipStream_t agg_stream = nullptr;
     bool agg_pending = false;
+    // scenario-major batches on the generic / tiled kernels: layout-0 copies of
+    // pq and the matrix outputs, transposed around the launch (fpf_layout.hip)
+    double *d_lay = nullptr;
+    size_t lay_bytes = 0;
     // auto choice between the interpreted tiled and the generic kernel, made
     // per batch (both table sets are built): tiled below AUTO_GENERIC_MIN_SCEN
     bool auto_batch = false;
@@ -1125,6 +1129,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
     if (opts) o = *opts;
     else fpf_opts_default(&o);
     if (o.mxitr < 1 || !(o.bkva > 0) || !(o.bkv > 0)) return fail(ctx, FPF_ERR_ARG, "bad fpf_opts");
+    if (o.layout != FPF_LAYOUT_SCEN_FASTEST && o.layout != FPF_LAYOUT_SCEN_MAJOR)
+        return fail(ctx, FPF_ERR_ARG, "fpf_opts.layout: FPF_LAYOUT_SCEN_FASTEST or FPF_LAYOUT_SCEN_MAJOR");
 
     HostFeeder h;
     h.nl = nl;
@@ -1411,6 +1417,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_partials);
     (void)hipFree(f->d_ticket);
     (void)hipFree(f->d_wave);
+    (void)hipFree(f->d_lay);
     if (f->agg_event) (void)hipEventDestroy(f->agg_event);
     if (f->rtc) rtc_release(f->rtc_kernel);
     if (f->rtc_ib) rtc_release(f->rtc_kernel_ib);
@@ -1496,11 +1503,12 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
 
 extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out,
                                       double *d_agg, void *stream) {
-    return fpf::solve_batch_device_ex(f, n_scen, d_pq, d_out, d_agg, stream, nullptr, nullptr);
+    return fpf::solve_batch_device_ex(f, n_scen, d_pq, d_out, d_agg, stream, nullptr, nullptr,
+                                      f ? f->opts.layout : 0);
 }
 
 int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
-                               void *stream, const double *d_vsrc, double *d_s_in) {
+                               void *stream, const double *d_vsrc, double *d_s_in, int layout) {
     if (!f || n_scen < 0 || (n_scen > 0 && !d_pq)) return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "bad arguments");
     fpf_ctx *ctx = f->ctx;
     if (n_scen == 0) return FPF_OK;
@@ -1529,9 +1537,40 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     o.ticket = nullptr;
     o.vsrc = d_vsrc;
     o.s_in = d_s_in;
+    o.smaj = layout == FPF_LAYOUT_SCEN_MAJOR ? 1 : 0;
     hipError_t e;
     bool agg_done = false;
     const int kern = kernel_for(f, n_scen);
+    // the generic and tiled kernels read and write [field][row][B] only: a
+    // scenario-major batch goes through layout-0 copies (transposed in here,
+    // the matrix outputs transposed back after the launch)
+    const size_t nB = (size_t)n_scen, nnl = 6 * (size_t)f->dev.nl, nn6 = 6 * (size_t)f->dev.nn, nn3 = 3 * (size_t)f->dev.nn;
+    struct Tr { double *user; double **dev; size_t rows; };
+    Tr tr[5] = {{u.vpolar, &o.vpolar, nn6}, {u.pqb, &o.pqb, nn6}, {u.pql, &o.pql, nn6}, {u.v_re, &o.v_re, nn3},
+                {u.v_im, &o.v_im, nn3}};
+    const bool transpose = o.smaj && kern != FPF_KERNEL_WAVE;
+    if (transpose) {
+        size_t need = nnl * nB;
+        for (const Tr &t : tr)
+            if (t.user) need += t.rows * nB;
+        if (need * sizeof(double) > f->lay_bytes) {
+            (void)hipFree(f->d_lay);
+            f->d_lay = nullptr;
+            f->lay_bytes = 0;
+            HIPCHK(ctx, hipMalloc(&f->d_lay, need * sizeof(double)));
+            f->lay_bytes = need * sizeof(double);
+        }
+        double *q = f->d_lay;
+        HIPCHK(ctx, launch_transpose(d_pq, q, nB, nnl, st));   // [B][6 Nl] -> [6 Nl][B]
+        d_pq = q;
+        q += nnl * nB;
+        for (Tr &t : tr)
+            if (t.user) {
+                *t.dev = q;
+                q += t.rows * nB;
+            }
+        o.smaj = 0;
+    }
     static const bool fused_agg = !getenv("FPF_FUSED_AGG") || atoi(getenv("FPF_FUSED_AGG")) != 0;
     const bool fuses_agg = (kern == FPF_KERNEL_TILED && f->rtc) || kern == FPF_KERNEL_WAVE;
     if (d_agg && fused_agg && fuses_agg) {
@@ -1572,6 +1611,9 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
         e = launch_generic(f->dev, n_scen, d_pq, f->d_scratch, f->scratch_ld, o, st);
     }
     if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("solve launch: ") + hipGetErrorString(e));
+    if (transpose)
+        for (const Tr &t : tr)
+            if (t.user) HIPCHK(ctx, launch_transpose(*t.dev, t.user, t.rows, nB, st));   // [rows][B] -> [B][rows]
     if (agg_done) HIPCHK(ctx, agg_after(f, st));
     if (d_agg && !agg_done) {
         e = launch_aggregate(n_scen, o.status, o.loss, o.vmin, o.vmax, f->dev.lb_v, f->dev.ub_v, d_agg, nullptr,
@@ -1605,6 +1647,11 @@ extern "C" int fpf_aggregate_device(fpf_feeder *f, int n_scen, const signed char
 
 extern "C" int fpf_solve_batch(fpf_feeder *f, int n_scen, const double *pq, const fpf_outputs *out,
                                fpf_aggregate *agg) {
+    return fpf::solve_batch_host(f, n_scen, pq, out, agg, f ? f->opts.layout : 0);
+}
+
+int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf_outputs *out, fpf_aggregate *agg,
+                          int layout) {
     if (!f || n_scen < 0 || (n_scen > 0 && !pq)) return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "bad arguments");
     fpf_ctx *ctx = f->ctx;
     if (n_scen == 0) {
@@ -1650,7 +1697,8 @@ extern "C" int fpf_solve_batch(fpf_feeder *f, int n_scen, const double *pq, cons
     d.loss = (double *)dptr(8);
     d.vmin = (double *)dptr(9);
     d.vmax = (double *)dptr(10);
-    int rc = fpf_solve_batch_device(f, n_scen, (const double *)dptr(0), &d, f->d_agg, (void *)ctx->stream);
+    int rc = fpf::solve_batch_device_ex(f, n_scen, (const double *)dptr(0), &d, f->d_agg, (void *)ctx->stream, nullptr,
+                                        nullptr, layout);
     if (rc) return rc;
     for (int i = 1; i < 11; ++i)
         if (parts[i].host)

@@ -280,6 +280,7 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
     else fpf_opts_default(&o);
     o.kernel = FPF_KERNEL_WAVE;
     o.exact = 0;
+    o.layout = FPF_LAYOUT_SCEN_FASTEST;   // fpf_areas_solve's arrays are [field][row][B] (include/freedm_pf.h)
     for (Area &A : a->area) {
         const int rc = fpf_feeder_create(ctx, A.dl.data(), A.nl, ncols, z, z_rows, z_cols, &o, &A.feeder);
         if (rc != FPF_OK) {
@@ -389,7 +390,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
             o.vmin = A.d_vmin;
             o.vmax = A.d_vmax;
             rc = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)st, A.parent >= 0 ? A.d_vsrc : nullptr,
-                                       A.d_sin);
+                                       A.d_sin, FPF_LAYOUT_SCEN_FASTEST);
             if (rc < 0) return afail(a, rc, std::string("area solve: ") + fpf_last_error(a->ctx));
         }
         // the boundary voltages' largest move this iteration (the first always moves)

@@ -176,6 +176,10 @@ struct OutDev {
     // entering at the source [6][B] = PQb row 0 (P1 Q1 P2 Q2 P3 Q3, kW / kVAr)
     const double *vsrc;
     double *s_in;
+    // batch layout (fpf_opts.layout) of pq and the matrix outputs: 0 [field][row][B],
+    // 1 [B][field][row] (the wave kernels read / write it natively; the host
+    // transposes around the generic and tiled kernels, fpf_layout.hip)
+    int32_t smaj;
 };
 
 #ifndef __HIPCC_RTC__
@@ -186,7 +190,11 @@ int ctx_device(const fpf_ctx *ctx);   // the HIP device of a context
 // fpf_solve_batch_device with the wave kernel's two extra per-scenario arrays
 // (OutDev::vsrc, OutDev::s_in; both device memory, may be NULL)
 int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
-                          void *stream, const double *d_vsrc, double *d_s_in);
+                          void *stream, const double *d_vsrc, double *d_s_in, int layout);
+// fpf_solve_batch in an explicit batch layout (internal callers build their own
+// batches in FPF_LAYOUT_SCEN_FASTEST whatever the feeder's fpf_opts.layout)
+int solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf_outputs *out, fpf_aggregate *agg,
+                     int layout);
 // launchers (fpf_generic.hip, fpf_tiled.hip, fpf_rtc.cpp)
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st);
@@ -196,6 +204,7 @@ hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss
                             double *d_agg, double *partials, unsigned *ticket, hipStream_t st);
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wave_lds_bytes(const WaveDev &w);
+hipError_t launch_transpose(const double *in, double *out, size_t rows, size_t cols, hipStream_t st);
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wblk_lds_bytes(const WaveDev &w);
 bool wblk_geometry(int n, int *wps, int *c);

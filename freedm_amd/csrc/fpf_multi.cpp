@@ -32,6 +32,7 @@ struct fpf_multi {
     std::vector<char *> d_stage;
     std::vector<size_t> stage_bytes;
     int nn = 0, nl = 0;
+    int layout = FPF_LAYOUT_SCEN_FASTEST;   // fpf_opts.layout of the host arrays
     std::string err;
 };
 
@@ -148,6 +149,7 @@ extern "C" int fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
     fpf_feeder_get_info(m->feeder[0], &in);
     m->nn = in.nn;
     m->nl = in.nl;
+    m->layout = opts ? opts->layout : FPF_LAYOUT_SCEN_FASTEST;
     g_create_err = "no error";
     *out = m;
     return FPF_OK;
@@ -159,9 +161,10 @@ extern "C" int fpf_multi_get_feeder(fpf_multi *m, int device, fpf_feeder **out) 
     return FPF_OK;
 }
 
-// Every pointer of `out` and pq is host memory laid out for the whole batch
-// ([field][row][n_scen], scenario fastest); device d reads and writes the
-// columns [lo_d, hi_d) of it with 2-D copies.
+// Every pointer of `out` and pq is host memory laid out for the whole batch;
+// device d reads and writes scenarios [lo_d, hi_d) of it: the columns of
+// [field][row][n_scen] (2-D copies) or one contiguous block of
+// [n_scen][field][row] (the scenario-major layout).
 extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const fpf_outputs *out,
                                fpf_aggregate *agg) {
     if (!m || n_scen < 0 || (n_scen > 0 && !pq)) return mfail(m, FPF_ERR_ARG, "fpf_multi_solve: bad arguments");
@@ -201,7 +204,17 @@ extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const
             m->stage_bytes[d] = total;
         }
         char *sb = m->d_stage[d];
-        MHIP(m, hipMemcpy2DAsync(sb, nd * 8, pq + lo, B * 8, nd * 8, 6 * nl, hipMemcpyHostToDevice, st));
+        // scenarios [lo, lo + nd) of a [rows][B] (or, scenario-major, [B][rows]) host array
+        auto copy = [&](void *dst, const void *src, size_t rows, size_t esz, hipMemcpyKind kind, bool to_host) {
+            if (m->layout == FPF_LAYOUT_SCEN_MAJOR || rows == 1) {
+                const size_t off = (size_t)lo * rows * esz, n = nd * rows * esz;
+                return to_host ? hipMemcpyAsync((char *)dst + off, src, n, kind, st)
+                               : hipMemcpyAsync(dst, (const char *)src + off, n, kind, st);
+            }
+            return to_host ? hipMemcpy2DAsync((char *)dst + lo * esz, B * esz, src, nd * esz, nd * esz, rows, kind, st)
+                           : hipMemcpy2DAsync(dst, nd * esz, (const char *)src + lo * esz, B * esz, nd * esz, rows, kind, st);
+        };
+        MHIP(m, copy(sb, pq, 6 * nl, 8, hipMemcpyHostToDevice, false));
         void *dp[10];
         for (int i = 0; i < 10; ++i) dp[i] = mats[i].host ? (void *)(sb + offs[i + 1]) : nullptr;
         fpf_outputs o;
@@ -218,9 +231,7 @@ extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const
         const int rc = fpf_solve_batch_device(m->feeder[d], (int)nd, (const double *)sb, &o, m->d_agg[d], (void *)st);
         if (rc < 0) return mfail(m, rc, std::string("device ") + std::to_string(d) + ": " + fpf_last_error(m->ctx[d]));
         for (int i = 0; i < 10; ++i)
-            if (mats[i].host)
-                MHIP(m, hipMemcpy2DAsync((char *)mats[i].host + lo * mats[i].esz, B * mats[i].esz, dp[i],
-                                         nd * mats[i].esz, nd * mats[i].esz, mats[i].rows, hipMemcpyDeviceToHost, st));
+            if (mats[i].host) MHIP(m, copy(mats[i].host, dp[i], mats[i].rows, mats[i].esz, hipMemcpyDeviceToHost, true));
     }
     // the one collective: [loss_sum .. n_scen] summed, vmin min'd, vmax max'd
     MNCCL(m, ncclGroupStart());

@@ -7,6 +7,7 @@
 // candidate is independent, so all m_max + 1 of them go to the GPU as one batch
 // and the reference's stop rule runs over the returned losses.
 #include "../../include/freedm_pf.h"
+#include "fpf_internal.h"
 
 #include <cstring>
 #include <vector>
@@ -60,7 +61,7 @@ extern "C" int fpf_vvc_line_search(fpf_feeder *feeder, const double *ctrl_dl, in
     out.loss = res->loss;
     out.vmin = res->vmin;
     out.vmax = res->vmax;
-    const int rc = fpf_solve_batch(feeder, M, pq.data(), &out, 0);
+    const int rc = fpf::solve_batch_host(feeder, M, pq.data(), &out, nullptr, FPF_LAYOUT_SCEN_FASTEST);
     if (rc < 0) return rc;
     res->first_nonconv = -1;
     for (int m = 0; m < M; ++m)

@@ -170,7 +170,36 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             stg[((int)threadIdx.x / SROW) * PSTR + nl * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
-        if ((B & 1) == 0) {
+        if (o.smaj) {
+            // scenario-major layout: the tile's nsb scenarios are one contiguous
+            // block of nsb x 6 Nl doubles, read with 16-byte loads (6 Nl is even)
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            constexpr int U2 = 12;
+            const int per = 6 * nl, total2 = DBG(256) ? 0 : nsb * (per / 2);
+            const d2v *src = (const d2v *)(pq + (size_t)s0 * per);
+            for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
+                d2v r[U2];
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    r[u] = __builtin_nontemporal_load(src + (i < total2 ? i : 0));
+                }
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    if (i < total2) {
+                        const int e = 2 * i, j = e / per, fr = e - j * per;   // fr, fr + 1: one scenario
+                        sd[spos(fr, j)] = r[u].x * inv_s3;
+                        sd[spos(fr + 1, j)] = r[u].y * inv_s3;
+                    }
+                }
+            }
+            // a partial last tile: zero loads in the columns of its missing scenarios
+            for (int i = threadIdx.x; i < (SPB - nsb) * per; i += NT) {
+                const int j = nsb + i / per, fr = i % per;
+                sd[spos(fr, j)] = 0.0;
+            }
+        } else if ((B & 1) == 0) {
             // 16-byte loads (B even: every pair of scenarios is aligned), all of a
             // thread's loads in flight at once for feeders up to ~128 rows
             typedef double d2v __attribute__((ext_vector_type(2)));
@@ -652,7 +681,16 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         last_wg = t == gridDim.x - 1;
     }
     // ---- the workgroup's V, coalesced: consecutive scenarios of one (phase, node)
-    if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
+    if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj) {
+        // scenario-major layout: the tile's V is one contiguous [nsb][3][Nn] block
+        const int per = 3 * nn, total = nsb * per;
+        for (int i = threadIdx.x; i < total; i += NT) {
+            const int j = i / per, r = i - j * per, p = r / nn, k = r - p * nn;
+            const double2 vv = k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + (k - 1) * SROW + j];
+            if (o.v_re) __builtin_nontemporal_store(vv.x, o.v_re + (size_t)s0 * per + i);
+            if (o.v_im) __builtin_nontemporal_store(vv.y, o.v_im + (size_t)s0 * per + i);
+        }
+    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
         constexpr int UV = 4;
         const int total = 3 * nn * SPB;
         for (int i0 = 0; i0 < total; i0 += UV * NT) {

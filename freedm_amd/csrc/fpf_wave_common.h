@@ -114,12 +114,15 @@ __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn,
     const cx sl = cmul(sv, cconj(il));
     const cx sb = cmul(sv, cconj(ib));
     const double mag = sqrt(fma(v.re, v.re, v.im * v.im));
-    const size_t o6 = ((size_t)(2 * p) * nn + k) * B + s, o6i = o6 + (size_t)nn * B;
+    // [field][row][B], or [B][field][row] (o.smaj)
+    const size_t o6 = o.smaj ? s * 6 * nn + (size_t)(2 * p) * nn + k : ((size_t)(2 * p) * nn + k) * B + s;
+    const size_t o6i = o6 + (o.smaj ? (size_t)nn : (size_t)nn * B);
+    const size_t o3 = o.smaj ? s * 3 * nn + (size_t)p * nn + k : ((size_t)p * nn + k) * B + s;
     if (o.vpolar) { o.vpolar[o6] = mag; o.vpolar[o6i] = polar_angle(v, p); }
     if (o.pqb) { o.pqb[o6] = sb.re; o.pqb[o6i] = sb.im; }
     if (o.pql) { o.pql[o6] = sl.re; o.pql[o6i] = sl.im; }
-    if (o.v_re) o.v_re[((size_t)p * nn + k) * B + s] = v.re;
-    if (o.v_im) o.v_im[((size_t)p * nn + k) * B + s] = v.im;
+    if (o.v_re) o.v_re[o3] = v.re;
+    if (o.v_im) o.v_im[o3] = v.im;
     return make_double2(sl.re, mag);
 }
 }  // namespace

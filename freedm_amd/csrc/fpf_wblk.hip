@@ -42,6 +42,15 @@
 
 namespace fpf {
 
+// diagnostic ablation builds (tools/build_ablations.sh wblk <bits>): results are
+// wrong when set.  1: every workgroup stages column s & 15 (L2-resident loads);
+// 2: no V write-out; 4: stop after staging.  Compiled out of the product.
+#ifdef FPF_WBLK_ABL
+#define WABL(bit) (FPF_WBLK_ABL & (bit))
+#else
+#define WABL(bit) 0
+#endif
+
 namespace {
 constexpr int WB_C = 4;   // slots per lane
 
@@ -106,19 +115,45 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
     double *const wtf = wtb + 8 * W;
     int *const pairs = (int *)(wtf + 8 * W);   // [bdepth][2][nblk]
 
-    // ---- the scenario's loads P/Q [6][Nl] (column s of pq) into Sld scaled by
-    // 1/(bkva/3) (DPF_return7.cpp:46-50), all of a thread's loads in flight
+    // ---- the scenario's loads P/Q [6][Nl] (column s of pq, or its contiguous
+    // block in the scenario-major layout) into Sld scaled by 1/(bkva/3)
+    // (DPF_return7.cpp:46-50), all of a thread's loads in flight
     {
         const double inv_s3 = 1.0 / f.s3;
         double *const sd = (double *)stg;
         const int total = 6 * nl;
         constexpr int U = 8;
+        if (o.smaj) {
+            // one contiguous block of 6 Nl doubles (16-byte aligned: 6 Nl is even)
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            const d2v *src = (const d2v *)(pq + (WABL(1) ? (size_t)(s & 15) : (size_t)s) * total);
+            const int total2 = total / 2;
+            for (int i0 = 0; i0 < total2; i0 += U * NT) {
+                d2v r[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + u * NT + tid;
+                    r[u] = __builtin_nontemporal_load(src + (i < total2 ? i : 0));
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + u * NT + tid;
+                    if (i < total2) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int e = 2 * i + h, fq = e / nl, rr = e - fq * nl;
+                            sd[2 * ((fq >> 1) * PS + rr) + (fq & 1)] = (h ? r[u].y : r[u].x) * inv_s3;
+                        }
+                    }
+                }
+            }
+        } else
         for (int i0 = 0; i0 < total; i0 += U * NT) {
             double r[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + u * NT + tid;
-                r[u] = pq[(size_t)(i < total ? i : 0) * B + s];
+                r[u] = pq[(size_t)(i < total ? i : 0) * B + (WABL(1) ? (s & 15) : s)];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -154,6 +189,7 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
         lg[c] = f.slot_lng[c * L + tid];
     }
     __syncthreads();
+    if (WABL(4)) return;
 
     cx v[C][3];
 #pragma unroll
@@ -407,13 +443,21 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
             last_wg = t == gridDim.x - 1;
         }
     }
-    // ---- V out: [3][Nn][B] re / im planes, column s
-    if (!FULL && (o.v_re || o.v_im)) {
+    // ---- V out: [3][Nn][B] re / im planes, column s (or the scenario's
+    // contiguous [3][Nn] block in the scenario-major layout)
+    if (!FULL && (o.v_re || o.v_im) && !WABL(2)) {
+        const size_t base = o.smaj ? (size_t)s * 3 * nn : (size_t)s, step = o.smaj ? 1 : (size_t)B;
         for (int i = tid; i < 3 * nn; i += NT) {
             const int p = i / nn, k = i - p * nn;
             const double2 vv = k == 0 ? V0S[p] : stg[p * PS + k - 1];
-            if (o.v_re) o.v_re[(size_t)i * B + s] = vv.x;
-            if (o.v_im) o.v_im[(size_t)i * B + s] = vv.y;
+            double *const re = o.v_re + base + (size_t)i * step, *const im = o.v_im + base + (size_t)i * step;
+            if (o.smaj) {   // streaming rows of one block
+                if (o.v_re) __builtin_nontemporal_store(vv.x, re);
+                if (o.v_im) __builtin_nontemporal_store(vv.y, im);
+            } else {        // 8 bytes of lines the neighbouring scenarios' workgroups share (L2)
+                if (o.v_re) *re = vv.x;
+                if (o.v_im) *im = vv.y;
+            }
         }
     }
     if (agg) {

@@ -83,6 +83,20 @@ class VPQ:
     vmax: float
 
 
+def _host_batch(pq, nl: int, nn: int, smaj: bool, full: bool):
+    """Check a host batch's shape for the layout; allocate the host results."""
+    pq = np.ascontiguousarray(pq, dtype=np.float64)
+    if pq.ndim != 3 or (pq.shape[1:] if smaj else pq.shape[:2]) != (6, nl):
+        raise ValueError(f"pq must be [B][6][{nl}]" if smaj else f"pq must be [6][{nl}][B]")
+    B = pq.shape[0] if smaj else pq.shape[2]
+    r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
+         "vmin": np.zeros(B), "vmax": np.zeros(B)}
+    if full:
+        sh6, sh3 = ((B, 6, nn), (B, 3, nn)) if smaj else ((6, nn, B), (3, nn, B))
+        r.update(Vpolar=np.zeros(sh6), PQb=np.zeros(sh6), PQL=np.zeros(sh6), V_re=np.zeros(sh3), V_im=np.zeros(sh3))
+    return pq, B, r
+
+
 class PowerFlow:
     """Batched DPF_return7 on one GPU for one feeder."""
 
@@ -133,19 +147,11 @@ class PowerFlow:
     # ------------------------------------------------------------------ host batch
     def solve(self, pq: np.ndarray, full: bool = True) -> dict:
         """Solve B scenarios.  pq: [6][Nl][B] float64 (P1 Q1 P2 Q2 P3 Q3 of each
-        Dl row, scenario fastest).  Returns per-scenario arrays ([col][row][B])
-        and the batch aggregate."""
+        Dl row, scenario fastest), or [B][6][Nl] for a feeder made with layout=1
+        (FPF_LAYOUT_SCEN_MAJOR).  Returns per-scenario arrays ([col][row][B], or
+        [B][col][row]) and the batch aggregate."""
         L = _lib.load()
-        pq = np.ascontiguousarray(pq, dtype=np.float64)
-        if pq.ndim != 3 or pq.shape[:2] != (6, self.nl):
-            raise ValueError(f"pq must be [6][{self.nl}][B]")
-        B = pq.shape[2]
-        nn = self.nn
-        r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
-             "vmin": np.zeros(B), "vmax": np.zeros(B)}
-        if full:
-            r.update(Vpolar=np.zeros((6, nn, B)), PQb=np.zeros((6, nn, B)), PQL=np.zeros((6, nn, B)),
-                     V_re=np.zeros((3, nn, B)), V_im=np.zeros((3, nn, B)))
+        pq, B, r = _host_batch(pq, self.nl, self.nn, self.opts.layout == 1, full)
         out = _lib.FpfOutputs(_ptr(r.get("Vpolar")), _ptr(r.get("PQb")), _ptr(r.get("PQL")), _ptr(r.get("V_re")),
                               _ptr(r.get("V_im")), _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]),
                               _ptr(r["vmin"]), _ptr(r["vmax"]))
@@ -163,7 +169,7 @@ class PowerFlow:
         pq: [6][Nl][B] float64 on the device; out: dict with any of
         vpolar/pqb/pql/v_re/v_im/iters/status/loss/vmin/vmax; agg: 8 float64."""
         L = _lib.load()
-        B = int(pq.shape[2])
+        B = int(pq.shape[0] if self.opts.layout == 1 else pq.shape[2])
         g = out.get
         o = _lib.FpfOutputs(_ptr(g("vpolar")), _ptr(g("pqb")), _ptr(g("pql")), _ptr(g("v_re")), _ptr(g("v_im")),
                             _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")))
@@ -179,7 +185,7 @@ class PowerFlow:
         and return (solve, aggregate) zero-argument callables -- the per-call host
         cost is then one foreign call each."""
         L = _lib.load()
-        B = int(pq.shape[2])
+        B = int(pq.shape[0] if self.opts.layout == 1 else pq.shape[2])
         g = out.get
         o = _lib.FpfOutputs(_ptr(g("vpolar")), _ptr(g("pqb")), _ptr(g("pql")), _ptr(g("v_re")), _ptr(g("v_im")),
                             _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")))
@@ -329,6 +335,7 @@ class MultiPowerFlow:
         self.feeder = feeder
         self.n_gpus = n_gpus
         o = _lib.default_opts(kernel=kernel, **opts)
+        self.opts = o
         dl = np.asfortranarray(feeder.Dl, dtype=np.float64)
         Z = np.asarray(feeder.Z, dtype=np.complex128)
         zbuf = np.zeros(max(2 * Z.size, 2))
@@ -361,15 +368,7 @@ class MultiPowerFlow:
     def solve(self, pq: np.ndarray, full: bool = True) -> dict:
         """Same arguments and results as PowerFlow.solve, over all the GPUs."""
         L = _lib.load()
-        pq = np.ascontiguousarray(pq, dtype=np.float64)
-        if pq.ndim != 3 or pq.shape[:2] != (6, self.nl):
-            raise ValueError(f"pq must be [6][{self.nl}][B]")
-        B, nn = pq.shape[2], self.nn
-        r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
-             "vmin": np.zeros(B), "vmax": np.zeros(B)}
-        if full:
-            r.update(Vpolar=np.zeros((6, nn, B)), PQb=np.zeros((6, nn, B)), PQL=np.zeros((6, nn, B)),
-                     V_re=np.zeros((3, nn, B)), V_im=np.zeros((3, nn, B)))
+        pq, B, r = _host_batch(pq, self.nl, self.nn, self.opts.layout == 1, full)
         out = _lib.FpfOutputs(_ptr(r.get("Vpolar")), _ptr(r.get("PQb")), _ptr(r.get("PQL")), _ptr(r.get("V_re")),
                               _ptr(r.get("V_im")), _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]),
                               _ptr(r["vmin"]), _ptr(r["vmax"]))

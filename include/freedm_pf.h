@@ -94,8 +94,17 @@ typedef struct fpf_opts {
                           conj(S)V/|V|^2 and the branch products with FMA -- within a few
                           ulp (north-star bar: 1e-10 relative on V, same iteration counts).
                           The generic and interpreted kernels are always exact. */
-    int    reserved[5];
+    int    layout;     /* batch layout of pq and the matrix outputs (FPF_LAYOUT_*):
+                          SCEN_FASTEST (0, default) pq [6][Nl][B], outputs [col][row][B];
+                          SCEN_MAJOR (1) pq [B][6][Nl] -- the reference's per-call load
+                          columns P1 Q1 P2 Q2 P3 Q3 of Dl (DPF_return7.cpp:46-50), one
+                          scenario after another -- and outputs [B][col][row].  The
+                          per-scenario scalars are [B] either way; B = 1 is the same. */
+    int    reserved[4];
 } fpf_opts;
+
+#define FPF_LAYOUT_SCEN_FASTEST 0   /* [field][row][B]: a workgroup of consecutive scenarios reads rows */
+#define FPF_LAYOUT_SCEN_MAJOR   1   /* [B][field][row]: one scenario is one contiguous block            */
 
 typedef struct fpf_feeder_info {
     int nl;            /* rows of Dl                                  */
@@ -114,7 +123,8 @@ typedef struct fpf_feeder_info {
     int reserved[3];
 } fpf_feeder_info;
 
-/* Per-scenario outputs; every pointer may be NULL (= not produced). */
+/* Per-scenario outputs; every pointer may be NULL (= not produced).  Shapes
+ * for FPF_LAYOUT_SCEN_FASTEST; FPF_LAYOUT_SCEN_MAJOR swaps B to the front. */
 typedef struct fpf_outputs {
     double      *vpolar;   /* [6][Nn][B]  |Va| angA |Vb| angB |Vc| angC (deg)  */
     double      *pqb;      /* [6][Nn][B]  branch P/Q (kW, kVAr)                */
@@ -182,7 +192,7 @@ int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double 
  * RCCL all-reduce (sum of the 8 fields, min of vmin, max of vmax) -- the only
  * exchange: per-scenario results go straight back to the caller's host arrays
  * at their global index.  pq / out / agg as fpf_solve_batch (host memory, the
- * whole batch's layout).  Returns >= 0 (non-converged scenarios) or FPF_ERR_*.
+ * whole batch's layout, either fpf_opts.layout).  Returns >= 0 (non-converged scenarios) or FPF_ERR_*.
  * With n_gpus = 1 the results equal fpf_solve_batch's bit for bit. */
 typedef struct fpf_multi fpf_multi;
 int         fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
@@ -214,7 +224,8 @@ void        fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate 
  * solver tolerances).  out (host): v_re / v_im in the feeder's numbering,
  * iters = outer iterations, status, loss (sum of the areas' branch losses),
  * vmin / vmax; vpolar / pqb / pql must be NULL.  fpf_areas_last_error also
- * reports the last outer iteration's largest boundary move. */
+ * reports the last outer iteration's largest boundary move.  pq and out are
+ * always FPF_LAYOUT_SCEN_FASTEST (opts.layout is ignored). */
 typedef struct fpf_areas fpf_areas;
 int         fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncols,
                              const double *z, int z_rows, int z_cols,
