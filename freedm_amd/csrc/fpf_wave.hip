@@ -174,7 +174,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // scenario-major layout: the tile's nsb scenarios are one contiguous
             // block of nsb x 6 Nl doubles, read with 16-byte loads (6 Nl is even)
             typedef double d2v __attribute__((ext_vector_type(2)));
-            constexpr int U2 = 12;
+            constexpr int U2 = 16;
             const int per = 6 * nl, total2 = DBG(256) ? 0 : nsb * (per / 2);
             const d2v *src = (const d2v *)(pq + (size_t)s0 * per);
             for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // 16-byte loads (B even: every pair of scenarios is aligned), all of a
             // thread's loads in flight at once for feeders up to ~128 rows
             typedef double d2v __attribute__((ext_vector_type(2)));
-            constexpr int U2 = 12, H = SPB / 2;
+            constexpr int U2 = 16, H = SPB / 2;
             const int total2 = total / 2;
             for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
                 d2v r[U2];

@@ -44,7 +44,7 @@ namespace fpf {
 
 // diagnostic ablation builds (tools/build_ablations.sh wblk <bits>): results are
 // wrong when set.  1: every workgroup stages column s & 15 (L2-resident loads);
-// 2: no V write-out; 4: stop after staging.  Compiled out of the product.
+// 2: no V write-out; 4: stop after staging; 8: no barrier after the X stores (2 of 5 per sweep).  Compiled out of the product.
 #ifdef FPF_WBLK_ABL
 #define WABL(bit) (FPF_WBLK_ABL & (bit))
 #else
@@ -122,21 +122,21 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
         const double inv_s3 = 1.0 / f.s3;
         double *const sd = (double *)stg;
         const int total = 6 * nl;
-        constexpr int U = 8;
+        constexpr int U = 8, U2 = 16;   // U2: every 16-byte load of a thread in flight (2048 buses: 13 per thread)
         if (o.smaj) {
             // one contiguous block of 6 Nl doubles (16-byte aligned: 6 Nl is even)
             typedef double d2v __attribute__((ext_vector_type(2)));
             const d2v *src = (const d2v *)(pq + (WABL(1) ? (size_t)(s & 15) : (size_t)s) * total);
             const int total2 = total / 2;
-            for (int i0 = 0; i0 < total2; i0 += U * NT) {
-                d2v r[U];
+            for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
+                d2v r[U2];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
+                for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + tid;
                     r[u] = __builtin_nontemporal_load(src + (i < total2 ? i : 0));
                 }
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
+                for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + tid;
                     if (i < total2) {
 #pragma unroll
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
                 for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
             }
         }
-        __syncthreads();
+        if (!WABL(8)) __syncthreads();
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             // Ib = Einc[last] - Eexc; Eexc of slot c = Einc of slot c-1, of slot 0 the lane's prefix
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
                 for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
             }
         }
-        __syncthreads();
+        if (!WABL(8)) __syncthreads();
         // block offsets, one thread per block, stored as V0 - off(b): off(b) = sum over
         // b's block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
         for (int b = tid; b < nblk; b += NT) {
