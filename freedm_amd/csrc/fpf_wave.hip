@@ -166,6 +166,8 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             const int fq = fr / nl, r = fr - fq * nl;
             return 2 * (((fq >> 1) * (nl + 1) + r) * SROW + j) + (fq & 1);
         };
+        // the same for a known (field, row)
+        auto spos2 = [&](int fq, int r, int j) { return 2 * (((fq >> 1) * (nl + 1) + r) * SROW + j) + (fq & 1); };
         if ((int)threadIdx.x < 3 * SROW)   // the zero row of each phase plane
             stg[((int)threadIdx.x / SROW) * PSTR + nl * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
         constexpr int U = 8;
@@ -177,6 +179,11 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             constexpr int U2 = 16;
             const int per = 6 * nl, total2 = DBG(256) ? 0 : nsb * (per / 2);
             const d2v *src = (const d2v *)(pq + (size_t)s0 * per);
+            // element e = 2 i of the block: scenario j = e / per, (field, row) of
+            // e % per -- walked 2 NT elements per load, no division per element
+            int j = 2 * (int)threadIdx.x / per;
+            RowWalk w;
+            w.init(2 * (int)threadIdx.x - j * per, 2 * NT, nl);
             for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
                 d2v r[U2];
 #pragma unroll
@@ -187,11 +194,12 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + (int)threadIdx.x;
-                    if (i < total2) {
-                        const int e = 2 * i, j = e / per, fr = e - j * per;   // fr, fr + 1: one scenario
-                        sd[spos(fr, j)] = r[u].x * inv_s3;
-                        sd[spos(fr + 1, j)] = r[u].y * inv_s3;
+                    if (i < total2) {   // e and e + 1 belong to one scenario (per is even)
+                        sd[spos2(w.fq, w.rr, j)] = r[u].x * inv_s3;
+                        sd[w.rr + 1 < nl ? spos2(w.fq, w.rr + 1, j) : spos2(w.fq + 1, 0, j)] = r[u].y * inv_s3;
                     }
+                    w.next();
+                    while (w.fq >= 6) { w.fq -= 6; ++j; }
                 }
             }
             // a partial last tile: zero loads in the columns of its missing scenarios
@@ -204,27 +212,35 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // thread's loads in flight at once for feeders up to ~128 rows
             typedef double d2v __attribute__((ext_vector_type(2)));
             constexpr int U2 = 16, H = SPB / 2;
+            static_assert(NT % H == 0, "a thread keeps its scenario pair");
             const int total2 = total / 2;
+            // pair i: scenarios j, j + 1 with j = 2 (i % H), the same for all of a
+            // thread's loads; (field, row) i / H walked NT / H rows per load
+            const int j = 2 * ((int)threadIdx.x % H);
+            RowWalk w, w2;   // the loads' walk, and the same walk again for the stores
+            w.init((int)threadIdx.x / H, NT / H, nl);
+            w2 = w;
             for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
                 d2v r[U2];
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + (int)threadIdx.x;
-                    const int j = 2 * (i % H), fr = i / H;
+                    const int fr = w.fq * nl + w.rr;
                     const bool ok = i < total2 && j < nsb;   // nsb is even
                     const size_t ga = DBG(16384) ? (size_t)s0 * 6 * nl + 2 * (size_t)i : (size_t)fr * B + s0 + j;
                     r[u] = __builtin_nontemporal_load((const d2v *)(pq + (ok ? ga : 0)));
                     r[u] = ok ? r[u] : d2v{0.0, 0.0};
+                    w.next();
                 }
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + (int)threadIdx.x;
-                    const int j = 2 * (i % H), fr = i / H;
                     if (i < total2) {
-                        const int q = spos(fr, j);
+                        const int q = spos2(w2.fq, w2.rr, j);
                         sd[q] = r[u].x * inv_s3;
                         sd[q + 2] = r[u].y * inv_s3;
                     }
+                    w2.next();
                 }
             }
         } else
@@ -684,23 +700,36 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj) {
         // scenario-major layout: the tile's V is one contiguous [nsb][3][Nn] block
         const int per = 3 * nn, total = nsb * per;
+        // element i: scenario j = i / per, (phase p, node k) of i % per, walked NT apart
+        int j = (int)threadIdx.x / per;
+        RowWalk w;
+        w.init((int)threadIdx.x - j * per, NT, nn);
+        while (w.fq >= 3) { w.fq -= 3; ++j; }
         for (int i = threadIdx.x; i < total; i += NT) {
-            const int j = i / per, r = i - j * per, p = r / nn, k = r - p * nn;
+            const int p = w.fq, k = w.rr;
             const double2 vv = k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + (k - 1) * SROW + j];
             if (o.v_re) __builtin_nontemporal_store(vv.x, o.v_re + (size_t)s0 * per + i);
             if (o.v_im) __builtin_nontemporal_store(vv.y, o.v_im + (size_t)s0 * per + i);
+            w.next();
+            while (w.fq >= 3) { w.fq -= 3; ++j; }
         }
     } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
         constexpr int UV = 4;
+        static_assert(NT % SPB == 0, "a thread keeps its scenario");
         const int total = 3 * nn * SPB;
+        // element i: scenario j = i % SPB (the same for all of a thread's
+        // elements), (phase, node) of i / SPB walked NT / SPB apart
+        RowWalk w;
+        w.init((int)threadIdx.x / SPB, NT / SPB, nn);
         for (int i0 = 0; i0 < total; i0 += UV * NT) {
             double2 vv[UV];
 #pragma unroll
             for (int u = 0; u < UV; ++u) {
                 const int i = i0 + u * NT + (int)threadIdx.x;
-                const int j = i % SPB, r = i / SPB, p = r / nn, k = r - p * nn;
+                const int j = (int)threadIdx.x % SPB, p = w.fq, k = w.rr;
                 vv[u] = i >= total ? make_double2(0.0, 0.0)
                                    : (k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + (k - 1) * SROW + j]);
+                w.next();
             }
 #pragma unroll
             for (int u = 0; u < UV; ++u) {

@@ -156,6 +156,25 @@ __device__ __forceinline__ double seg_reduce_min(double x) {
 template <int L>
 __device__ __forceinline__ double seg_reduce_max(double x) { return -seg_reduce_min<L>(-x); }
 
+// (field, row) of a flat index f * n + r, advanced by a fixed step without a
+// division per step (the step split once as a * n + b): the staging and
+// write-out loops visit a thread's elements NT (or 2 NT) indices apart
+struct RowWalk {
+    int fq, rr, a, b, n;
+    __device__ __forceinline__ void init(int fr, int step, int n_) {
+        n = n_;
+        fq = fr / n;
+        rr = fr - fq * n;
+        a = step / n;
+        b = step - a * n;
+    }
+    __device__ __forceinline__ void next() {
+        rr += b;
+        fq += a;
+        if (rr >= n) { rr -= n; ++fq; }
+    }
+};
+
 // tile of block b: the first 8 * (G / 8) blocks are dealt so that blocks on one
 // XCD (b, b + 8, ...) take consecutive tiles; the remainder keeps b
 __device__ __forceinline__ int xcd_tile(int b, int G) {

@@ -128,39 +128,47 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
             typedef double d2v __attribute__((ext_vector_type(2)));
             const d2v *src = (const d2v *)(pq + (WABL(1) ? (size_t)(s & 15) : (size_t)s) * total);
             const int total2 = total / 2;
+            // element e = 2 i: (field, row) walked 2 NT elements per load
+            RowWalk w;
+            w.init(2 * tid, 2 * NT, nl);
             for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
                 d2v r[U2];
+                int q0[U2], q1[U2];
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + tid;
                     r[u] = __builtin_nontemporal_load(src + (i < total2 ? i : 0));
+                    q0[u] = 2 * ((w.fq >> 1) * PS + w.rr) + (w.fq & 1);
+                    const int f1 = w.rr + 1 < nl ? w.fq : w.fq + 1, r1 = w.rr + 1 < nl ? w.rr + 1 : 0;
+                    q1[u] = 2 * ((f1 >> 1) * PS + r1) + (f1 & 1);
+                    w.next();
                 }
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + tid;
                     if (i < total2) {
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int e = 2 * i + h, fq = e / nl, rr = e - fq * nl;
-                            sd[2 * ((fq >> 1) * PS + rr) + (fq & 1)] = (h ? r[u].y : r[u].x) * inv_s3;
-                        }
+                        sd[q0[u]] = r[u].x * inv_s3;
+                        sd[q1[u]] = r[u].y * inv_s3;
                     }
                 }
             }
-        } else
-        for (int i0 = 0; i0 < total; i0 += U * NT) {
-            double r[U];
+        } else {
+            RowWalk w;   // (field, row) of element i, walked NT per load
+            w.init(tid, NT, nl);
+            for (int i0 = 0; i0 < total; i0 += U * NT) {
+                double r[U];
+                int q[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * NT + tid;
-                r[u] = pq[(size_t)(i < total ? i : 0) * B + (WABL(1) ? (s & 15) : s)];
-            }
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + u * NT + tid;
+                    r[u] = pq[(size_t)(i < total ? i : 0) * B + (WABL(1) ? (s & 15) : s)];
+                    q[u] = 2 * ((w.fq >> 1) * PS + w.rr) + (w.fq & 1);
+                    w.next();
+                }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * NT + tid;
-                if (i < total) {
-                    const int fq = i / nl, rr = i - fq * nl;
-                    sd[2 * ((fq >> 1) * PS + rr) + (fq & 1)] = r[u] * inv_s3;
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + u * NT + tid;
+                    if (i < total) sd[q[u]] = r[u] * inv_s3;
                 }
             }
         }
@@ -447,8 +455,10 @@ __global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, c
     // contiguous [3][Nn] block in the scenario-major layout)
     if (!FULL && (o.v_re || o.v_im) && !WABL(2)) {
         const size_t base = o.smaj ? (size_t)s * 3 * nn : (size_t)s, step = o.smaj ? 1 : (size_t)B;
-        for (int i = tid; i < 3 * nn; i += NT) {
-            const int p = i / nn, k = i - p * nn;
+        RowWalk w;   // (phase, node) of element i = p Nn + k, walked NT apart
+        w.init(tid, NT, nn);
+        for (int i = tid; i < 3 * nn; i += NT, w.next()) {
+            const int p = w.fq, k = w.rr;
             const double2 vv = k == 0 ? V0S[p] : stg[p * PS + k - 1];
             double *const re = o.v_re + base + (size_t)i * step, *const im = o.v_im + base + (size_t)i * step;
             if (o.smaj) {   // streaming rows of one block
