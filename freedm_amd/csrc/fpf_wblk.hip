@@ -93,10 +93,10 @@ __device__ __forceinline__ void wave_prefix(const double *wt, int wv, int lane, 
 }
 }  // namespace
 
-template <int W, bool FULL>
-__global__ __launch_bounds__(W * 64, 2) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
+template <int W, bool FULL, int C>
+__global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
                                                              OutDev o) {
-    constexpr int C = WB_C, L = 64 * W, NT = 64 * W;
+    constexpr int L = 64 * W, NT = 64 * W;
     extern __shared__ double2 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int s = xcd_tile(blockIdx.x, gridDim.x);   // this workgroup's scenario
@@ -512,9 +512,12 @@ size_t wblk_lds_bytes(const WaveDev &w) {
 }
 
 bool wblk_geometry(int n, int *wps, int *c) {
-    *c = WB_C;
+    // C = 4 slots per lane, 2 wavefronts per SIMD; FPF_WBLK_C=8 (experiments):
+    // 8 slots per lane, half the wavefronts, 1 per SIMD (AGPRs hold the rest)
+    const char *e = getenv("FPF_WBLK_C");
+    *c = (e && atoi(e) == 8) ? 8 : WB_C;
     for (int w = 2; w <= 8; w *= 2)
-        if (n <= 64 * w * WB_C) {
+        if (n <= 64 * w * *c) {
             *wps = w;
             return true;
         }
@@ -523,15 +526,17 @@ bool wblk_geometry(int n, int *wps, int *c) {
 
 namespace {
 typedef void (*WblkKernel)(WaveDev, int, const double *, OutDev);
-template <int W>
+template <int W, int C>
 WblkKernel pick_wblk(bool full) {
-    return full ? dpf_wblk_kernel<W, true> : dpf_wblk_kernel<W, false>;
+    return full ? dpf_wblk_kernel<W, true, C> : dpf_wblk_kernel<W, false, C>;
 }
 }  // namespace
 
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
     const bool full = o.vpolar || o.pqb || o.pql;
-    WblkKernel k = w.wps == 2 ? pick_wblk<2>(full) : (w.wps == 4 ? pick_wblk<4>(full) : (w.wps == 8 ? pick_wblk<8>(full) : nullptr));
+    WblkKernel k = nullptr;
+    if (w.C == WB_C) k = w.wps == 2 ? pick_wblk<2, WB_C>(full) : (w.wps == 4 ? pick_wblk<4, WB_C>(full) : (w.wps == 8 ? pick_wblk<8, WB_C>(full) : nullptr));
+    else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full) : (w.wps == 4 ? pick_wblk<4, 8>(full) : nullptr);
     if (!k || w.has_mask) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB: a per-device setting, once per (device, variant)
     static std::mutex mu;
@@ -540,7 +545,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> lk(mu);
-        const std::array<int, 3> key = {dev, w.wps, (int)full};
+        const std::array<int, 3> key = {dev, w.wps * 16 + w.C, (int)full};
         if (!attr_done.count(key)) {
             hipFuncAttributes fa{};
             hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
