@@ -443,6 +443,37 @@ def main():
                 "mean_sweeps": float(o4["iters"].double().mean().item())}
             del d4
             pf4.close()
+            # BASELINE config 3 beside it: the 2048-bus feeder x 65 536 scenarios on
+            # the wave-block kernel (scenario-major), 1024 seeded scenarios x a
+            # per-scenario load multiplier so all 65 536 differ (tests/test_gpu_wblk.py);
+            # `python bench.py --config 3` generates every scenario and adds its CPU leg
+            n3, s3f, b3, seed3, _ = CONFIGS[3]
+            f3 = synthetic_feeder(n3, s3f)
+            pf3 = PowerFlow(f3, device=local, kernel=args.kernel, exact=args.exact, layout=LAYOUT[3])
+            base3 = torch.from_numpy(scenario_loads(f3, np.arange(1024), seed=seed3)).to(dev)
+            ids3 = torch.arange(b3, device=dev)
+            mult3 = 0.9 + 0.2 * ((ids3 * 2654435761) % 1000).double() / 1000.0
+            d3 = base3[:, :, ids3 % 1024] * mult3
+            if LAYOUT[3] == 1:
+                d3 = d3.permute(2, 0, 1).contiguous()
+            del base3
+            pf3.reserve(b3)
+            ms3, o3 = _kernel_ms(torch, pf3, d3, b3, 3, 1, stream, dev)
+            conv3 = int((o3["status"] == 0).sum().item())
+            bpa3 = bytes_alg_per_scenario(pf3.info["nb"], pf3.nn)
+            ach3 = bpa3 * b3 / (ms3 / 1e3) / 1e9
+            k3 = "dpf_wblk_kernel" if pf3.kernel == "wave" else {"generic": "dpf_generic3_kernel"}.get(pf3.kernel, pf3.kernel)
+            res["roofline_config3"] = {
+                "workload": f"BASELINE config 3: {n3}-bus feeder, {b3} scenarios per GPU per launch",
+                "bound": "hbm", "achieved": ach3, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach3 / HBM_PEAK_GBS,
+                "traffic": _pmc_traffic(f"{n3}-bus x {b3}", k3), "kernel": k3,
+                "model": "state-resident (loads in, V and scalars out)" if pf3.kernel == "wave" else
+                         "state-resident bytes; this kernel streams its state (see --config 3)", "kernel_ms": ms3,
+                "bytes_alg_per_scenario": bpa3, "converged_scenarios_per_s": conv3 / (ms3 / 1e3),
+                "mean_sweeps": float(o3["iters"].double().mean().item()),
+                "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][LAYOUT[3]]}
+            del d3, o3
+            pf3.close()
             copy = _copy_bandwidth(torch, dev)
             res["hbm_copy_check"] = {"device_copy_gbs": copy, "spec_gbs": HBM_PEAK_GBS,
                                      "copy_frac_of_spec": copy / HBM_PEAK_GBS,

@@ -24,7 +24,9 @@
 //   * scenario s = blockIdx.x in XCD-aware order (the workgroups one XCD runs
 //     take consecutive scenarios, so the [row][B] lines of pq and V that
 //     neighbouring scenarios share meet in that XCD's L2).
-// Feeders with zeroed phases (phase masks) run the generic kernel instead.
+// Zeroed phases (line codes with a zero self-impedance, :180-192) as in the
+// wave kernel: V = 0 on the phase, the path restarting below a zeroed ancestor,
+// the loss over PQL and the general V_abc_list extremes (full-output variant).
 //
 // Arithmetic: as the wave kernel (prefix sums instead of the sequential chains,
 // FMA products, one-reciprocal division, Sld scaled by 1/(bkva/3)), checked at
@@ -113,7 +115,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double2 *const V0S = OFF + 3 * nblk;
     double *const wtb = (double *)(V0S + 4);
     double *const wtf = wtb + 8 * W;
-    int *const pairs = (int *)(wtf + 8 * W);   // [bdepth][2][nblk]
+    double *const vx = wtf + 8 * W;             // [3][2] per-phase Vmin / Vmax (zeroed phases)
+    int *const pairs = (int *)(vx + 8);         // [bdepth][2][nblk]
 
     // ---- the scenario's loads P/Q [6][Nl] (column s of pq, or its contiguous
     // block in the scenario-major layout) into Sld scaled by 1/(bkva/3)
@@ -215,7 +218,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<false>(ldx(stg, p * PS + sb[c]), v[c][p]);
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(stg, p * PS + sb[c]), v[c][p]);   // 0 on a zeroed phase
 
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of
         // IL: lane-local prefix, wavefront scan, the totals of the waves before
@@ -360,7 +363,32 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) v[c][p] = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
+            for (int p = 0; p < 3; ++p) {
+                const cx vr = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
+                if (FULL) g[c][p] = vr;
+                v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
+            }
+        if (FULL && f.has_rel) {
+            // below a zeroed ancestor m: V(k,p) = A(m) - A(k) = Vr(k) - Vr(m), Vr = V0 - A
+            // before the zeroing (held in g); the forward entries (block offsets are
+            // read) carry Vr now
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int ci = si_store_f(si[c]);
+                if (ci >= 0) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const int mr = f.slot_mref[(p * C + c) * L + tid];
+                    if (mr >= 0 && !((si_mask(si[c]) >> p) & 1)) v[c][p] = csub(g[c][p], ldx(X, p * XC + mr));
+                }
+        }
 
         if (fin) {
             // ---- the last sweep: V of node k over Sld row k - 1 (every Sld read of
@@ -377,17 +405,58 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     }
                 }
             }
-            const double x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
+            double x;
+            if (FULL && f.has_mask) {
+                // zeroed phases: the reference's sum over PQL (the loss identity needs
+                // every phase live); the wave's part of sum Re(V conj(IL))
+                x = 0.0;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        if (si_valid(si[c])) x = fma(v[c][p].re, il[c][p].re, fma(v[c][p].im, il[c][p].im, x));
+                x = seg_incl<64>(x);
+            } else {
+                x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
+            }
             if (lane == 63) wtb[8 * wv + 6] = x;
             break;
         }
     }
     __syncthreads();
 
-    // ---- Vmin/Vmax (V_abc_list.cpp:7-81, VoltVarCtrl.cpp:1201-1207): no zeroed
-    // phases, so every Lnum_p + 1 = Nn and V_abc_list keeps every row -- the plain
-    // extremes of |V| (|V|^2 compared, one sqrt each)
-    {
+    // ---- Vmin/Vmax (V_abc_list.cpp:7-81, VoltVarCtrl.cpp:1201-1207)
+    if (FULL && f.has_mask) {
+        // general V_abc_list: per phase the first K_p nonzero |V| in node order,
+        // zero padded; one wave per phase, 64 nodes per step (ballot ranks)
+        for (int p = wv; p < 3; p += W) {
+            const int K = f.K[p];
+            int cnt = 0;
+            double mn = INFINITY, mx = -INFINITY;
+            for (int k0 = 0; k0 < nn; k0 += 64) {
+                const int k = k0 + lane;
+                double m = 0.0;
+                if (k < nn) {
+                    const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PS + k - 1);
+                    m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
+                }
+                const bool nz = k < nn && m != 0.0;
+                const unsigned long long bal = __ballot(nz);
+                const int rank = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+                if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
+                cnt += __popcll(bal);
+            }
+            if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+            mn = seg_reduce_min<64>(mn);
+            mx = seg_reduce_max<64>(mx);
+            if (lane == 63) {
+                vx[2 * p] = mn;
+                vx[2 * p + 1] = mx;
+            }
+        }
+    } else {
+        // no zeroed phases: every Lnum_p + 1 = Nn and V_abc_list keeps every row --
+        // the plain extremes of |V| (|V|^2 compared, one sqrt each)
         double mn = INFINITY, mx = -INFINITY;
         for (int k = tid; k < nn; k += NT) {
 #pragma unroll
@@ -421,9 +490,19 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             mn = fmin(mn, wtf[8 * w + 6]);
             mx = fmax(mx, wtf[8 * w + 7]);
         }
-        x *= f.s3;
-        mn = sqrt(mn);
-        mx = sqrt(mx);
+        if (FULL && f.has_mask) {
+            // PQb(0).re - sum_k PQL(k).re, V0 conj(Ib(0)) of the last sweep
+            double sb0 = 0.0;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sb0 += cmul(cmul(ldx(V0S, p), mk(f.s3, 0.0)), cconj(ibo[p])).re;
+            x = sb0 - f.s3 * x;
+            mn = fmin(fmin(vx[0], vx[2]), vx[4]);
+            mx = fmax(fmax(vx[1], vx[3]), vx[5]);
+        } else {
+            x *= f.s3;
+            mn = sqrt(mn);
+            mx = sqrt(mx);
+        }
         if (o.iters) o.iters[s] = it + 1;
         if (o.status) o.status[s] = conv ? 0 : 1;
         if (o.loss) o.loss[s] = x;
@@ -506,7 +585,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 size_t wblk_lds_bytes(const WaveDev &w) {
     const size_t ntz = w.temp_sym ? 4 : 9, xc = (size_t)w.ncomp + 1, nt = 64 * (size_t)w.wps;
     const size_t zc = 16 * (size_t)w.ncode * ntz;
-    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk + 4) + 8 * 16 * (size_t)w.wps +
+    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk + 4) + 8 * 16 * (size_t)w.wps + 64 +
                         4 * 2 * (size_t)w.bdepth * w.nblk;
     return zc + std::max(rest, 8 * 8 * nt);   // the last workgroup's fold reuses the space after zc
 }
@@ -533,11 +612,13 @@ WblkKernel pick_wblk(bool full) {
 }  // namespace
 
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
-    const bool full = o.vpolar || o.pqb || o.pql;
+    // the full-output variant keeps IL and Ib of the last sweep (Vpolar / PQb /
+    // PQL), and the zeroed-phase paths
+    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
     WblkKernel k = nullptr;
     if (w.C == WB_C) k = w.wps == 2 ? pick_wblk<2, WB_C>(full) : (w.wps == 4 ? pick_wblk<4, WB_C>(full) : (w.wps == 8 ? pick_wblk<8, WB_C>(full) : nullptr));
     else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full) : (w.wps == 4 ? pick_wblk<4, 8>(full) : nullptr);
-    if (!k || w.has_mask) return hipErrorInvalidValue;
+    if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB: a per-device setting, once per (device, variant)
     static std::mutex mu;
     static std::set<std::array<int, 3>> attr_done;

@@ -73,6 +73,77 @@ def test_wblk_nonconvergent_and_mixed_sweeps():
     _check_full(r, c)
 
 
+def _masked_feeder(n=700, seed=700, restart=False):
+    """Synthetic feeder with zeroed phases: a phase-B-only line code on every row
+    of two laterals (phases A and C zeroed there, DPF_return7.cpp:180-192); with
+    restart, on the first row only of the second (its three-phase rows below
+    restart from a zeroed ancestor -- not a physical feeder, but a table the
+    reference solves); the loads of phases A and C removed on both laterals."""
+    f = F.synthetic_feeder(n, seed)
+    Dl = f.Dl.copy()
+    Z = np.vstack([f.Z, np.diag([0, 0.3 + 0.8j, 0])])
+    code = Z.shape[0] // 3
+    seps = np.flatnonzero(Dl[:, 0] == 0)
+
+    def block(i):
+        return seps[i] + 1, (seps[i + 1] if i + 1 < len(seps) else Dl.shape[0])
+    a, b = block(3)
+    Dl[a:b, 3] = code
+    Dl[a:b, [6, 7, 10, 11]] = 0
+    a, b = block(7)
+    if restart:
+        Dl[a, 3] = code
+    else:
+        Dl[a:b, 3] = code
+    Dl[a:b, [6, 7, 10, 11]] = 0
+    return F.Feeder(Dl, Z, name=f"synthetic-{n}bus-zeroed-phases")
+
+
+@pytest.mark.parametrize("n", [700, 2048])
+def test_wblk_zeroed_phases(n):
+    """Zeroed phases on the wave-block kernel (the full-output variant): V = 0
+    on the zeroed phases and the -180/+180 angle pattern, the restart below a
+    zeroed ancestor, the loss over PQL and the general V_abc_list extremes
+    (Lnum_p + 1 < Nn), against the oracle."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    from test_gpu_parity import _fast_mode_outputs_match
+    f = _masked_feeder(n, n)
+    pq = F.scenario_loads(f, np.arange(24), pv_frac=0.0)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (c["status"] == 0).all()
+    assert (c["Vpolar"][0::2] == 0).any()                      # some (node, phase) zeroed
+    nn = int((f.Dl[:, 0] != 0).sum()) + 1
+    assert min(O.lnum(f.Dl, f.Z)) + 1 < nn                     # V_abc_list drops rows
+    pf = PowerFlow(f)
+    assert pf.kernel == "wave" and pf.info["tile"] == 1
+    r = pf.solve(pq)
+    assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+    assert _vrel(r["V_re"], r["V_im"], c["V_re"], c["V_im"]) <= 1e-10   # zeroed entries: exactly 0 in both
+    _close(r["loss"], c["loss"], 1e-8)
+    np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
+    np.testing.assert_allclose(r["vmax"], c["vmax"], rtol=1e-10)
+    _fast_mode_outputs_match(r, c, c["status"] == 0)
+
+
+def test_wblk_declines_restart_below_zeroed_phase():
+    """A live phase below a zeroed ancestor (V(k) = A(m) - A(k), a small
+    difference of two prefix sums over up to 2048 positions) stays on the
+    generic kernel, bit-identical to the oracle; the per-wavefront wave kernel
+    (<= 256 branches) keeps it (G6, test_gpu_parity.py)."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = _masked_feeder(2048, 2048, restart=True)
+    pq = F.scenario_loads(f, np.arange(8), pv_frac=0.0)
+    pf = PowerFlow(f)
+    assert pf.kernel == "generic"
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (r["iters"] == c["iters"]).all()
+    np.testing.assert_array_equal(r["V_re"], c["V_re"])
+    np.testing.assert_array_equal(r["V_im"], c["V_im"])
+
+
 def test_config3_wblk_full_size():
     """BASELINE config 3 at its stated size on the default (fast) path: 65 536
     scenarios of the 2048-bus feeder in one launch of the wave-block kernel,
