@@ -408,12 +408,13 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // one common off-diagonal zm: drop_a = (z_aa - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const cx m = ldx(tl, (3 * C + c) * L + li);
+                // (ablation 65536: wave-uniform TEMP from the kernel arguments, no LDS reads)
+                const cx m = DBG(65536) ? mk(f.lb_v * 1e-3, f.ub_v * 1e-3) : ldx(tl, (3 * C + c) * L + li);
                 const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
                 const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
-                    const cx d = ldx(tl, (a * C + c) * L + li);
+                    const cx d = DBG(65536) ? mk(f.eps * (a + 1), f.V0[0] * 1e-3) : ldx(tl, (a * C + c) * L + li);
                     const cx b = ib[c][a];
                     g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
                     if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
