@@ -471,7 +471,14 @@ def main():
                          "state-resident bytes; this kernel streams its state (see --config 3)", "kernel_ms": ms3,
                 "bytes_alg_per_scenario": bpa3, "converged_scenarios_per_s": conv3 / (ms3 / 1e3),
                 "mean_sweeps": float(o3["iters"].double().mean().item()),
-                "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][LAYOUT[3]]}
+                "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][LAYOUT[3]],
+                # SURVEY 8(d) priced config 3 with its state streaming through HBM
+                # (2.16 MB per scenario at 5 sweeps: 3.70 M scen/s at 100 % of 8 TB/s);
+                # this kernel keeps the state on chip, so that rate is exceeded
+                "survey_streaming_roofline_scen_per_s": HBM_PEAK_GBS * 1e9 / (
+                    bytes_alg_streaming(pf3.info["nb"], pf3.nn, float(o3["iters"].double().mean().item()), 1)),
+                "vs_survey_streaming_roofline": (conv3 / (ms3 / 1e3)) / (HBM_PEAK_GBS * 1e9 / bytes_alg_streaming(
+                    pf3.info["nb"], pf3.nn, float(o3["iters"].double().mean().item()), 1))}
             del d3, o3
             pf3.close()
             copy = _copy_bandwidth(torch, dev)
