@@ -64,10 +64,12 @@ def test_scenario_major_light_outputs_on_device(n):
         np.testing.assert_array_equal(b["v_im"], a["v_im"].transpose(2, 0, 1))
 
 
-def test_multi_scenario_major():
-    """fpf_multi_solve over the scenario-major host arrays (contiguous shards)."""
+@pytest.mark.parametrize("n", [123, 700])
+def test_multi_scenario_major(n):
+    """fpf_multi_solve over the scenario-major host arrays (contiguous shards),
+    on the wave kernel and on the wave-block kernel."""
     from freedm_amd import MultiPowerFlow, PowerFlow
-    f = F.synthetic_feeder(123, 123)
+    f = F.synthetic_feeder(n, n)
     pq = np.ascontiguousarray(F.scenario_loads(f, np.arange(50)).transpose(2, 0, 1))
     r = MultiPowerFlow(f, 1, layout=1).solve(pq)
     s = PowerFlow(f, layout=1).solve(pq)
