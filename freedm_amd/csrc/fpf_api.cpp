@@ -77,6 +77,9 @@ struct fpf_feeder {
     // pq and the matrix outputs, transposed around the launch (fpf_layout.hip)
     double *d_lay = nullptr;
     size_t lay_bytes = 0;
+    // host-API results: pinned staging, one device-to-host copy for small outputs
+    void *h_stage = nullptr;
+    size_t h_stage_bytes = 0;
     // auto choice between the interpreted tiled and the generic kernel, made
     // per batch (both table sets are built): tiled below AUTO_GENERIC_MIN_SCEN
     bool auto_batch = false;
@@ -1419,6 +1422,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_ticket);
     (void)hipFree(f->d_wave);
     (void)hipFree(f->d_lay);
+    (void)hipHostFree(f->h_stage);
     if (f->agg_event) (void)hipEventDestroy(f->agg_event);
     if (f->rtc) rtc_release(f->rtc_kernel);
     if (f->rtc_ib) rtc_release(f->rtc_kernel_ib);
@@ -1664,13 +1668,14 @@ int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf
     std::memset(&none, 0, sizeof(none));
     const fpf_outputs &u = out ? *out : none;
     const size_t B = (size_t)n_scen, nn = (size_t)f->info.nn, nl = (size_t)f->info.nl;
-    // staging layout: pq | vpolar | pqb | pql | v_re | v_im | iters | status | loss | vmin | vmax
+    // staging layout: pq | vpolar | pqb | pql | v_re | v_im | iters | status | loss | vmin | vmax | aggregate
     struct Part { void *host; size_t bytes; size_t off; };
-    Part parts[11] = {
+    double h_agg[8];
+    Part parts[12] = {
         {(void *)pq, 6 * nl * B * 8, 0}, {u.vpolar, 6 * nn * B * 8, 0}, {u.pqb, 6 * nn * B * 8, 0},
         {u.pql, 6 * nn * B * 8, 0},      {u.v_re, 3 * nn * B * 8, 0},  {u.v_im, 3 * nn * B * 8, 0},
         {u.iters, 4 * B, 0},             {u.status, B, 0},             {u.loss, 8 * B, 0},
-        {u.vmin, 8 * B, 0},              {u.vmax, 8 * B, 0}};
+        {u.vmin, 8 * B, 0},              {u.vmax, 8 * B, 0},           {h_agg, sizeof(h_agg), 0}};
     size_t total = 0;
     for (Part &p : parts) {
         if (!p.host) continue;
@@ -1698,15 +1703,35 @@ int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf
     d.loss = (double *)dptr(8);
     d.vmin = (double *)dptr(9);
     d.vmax = (double *)dptr(10);
-    int rc = fpf::solve_batch_device_ex(f, n_scen, (const double *)dptr(0), &d, f->d_agg, (void *)ctx->stream, nullptr,
-                                        nullptr, layout);
+    int rc = fpf::solve_batch_device_ex(f, n_scen, (const double *)dptr(0), &d, (double *)dptr(11), (void *)ctx->stream,
+                                        nullptr, nullptr, layout);
     if (rc) return rc;
-    for (int i = 1; i < 11; ++i)
-        if (parts[i].host)
-            HIPCHK(ctx, hipMemcpyAsync(parts[i].host, dptr(i), parts[i].bytes, hipMemcpyDeviceToHost, ctx->stream));
-    double h_agg[8];
-    HIPCHK(ctx, hipMemcpyAsync(h_agg, f->d_agg, sizeof(h_agg), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    // the outputs are one contiguous region after pq: small ones (a VVC round's
+    // solves, a batch's per-scenario scalars) come back in one copy into pinned
+    // memory -- each copy costs tens of microseconds of latency -- large ones
+    // straight into the caller's arrays
+    size_t o0 = total;
+    for (int i = 1; i < 12; ++i)
+        if (parts[i].host) o0 = std::min(o0, parts[i].off);
+    const size_t obytes = total - o0;
+    if (obytes <= (size_t)4 << 20) {
+        if (obytes > f->h_stage_bytes) {
+            (void)hipHostFree(f->h_stage);
+            f->h_stage = nullptr;
+            f->h_stage_bytes = 0;
+            HIPCHK(ctx, hipHostMalloc(&f->h_stage, std::max(obytes, (size_t)1 << 16)));
+            f->h_stage_bytes = std::max(obytes, (size_t)1 << 16);
+        }
+        HIPCHK(ctx, hipMemcpyAsync(f->h_stage, sb + o0, obytes, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        for (int i = 1; i < 12; ++i)
+            if (parts[i].host) std::memcpy(parts[i].host, (char *)f->h_stage + (parts[i].off - o0), parts[i].bytes);
+    } else {
+        for (int i = 1; i < 12; ++i)
+            if (parts[i].host)
+                HIPCHK(ctx, hipMemcpyAsync(parts[i].host, dptr(i), parts[i].bytes, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
     if (agg) std::memcpy(agg, h_agg, sizeof(h_agg));
     return (int)h_agg[4];   // non-converged count
 }
