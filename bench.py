@@ -515,6 +515,26 @@ def main():
                                        "ms_per_batch": min(th) * 1e3,
                                        "note": "fpf_solve_batch with host buffers (26 MB H2D, scalars D2H), "
                                                "best of 5; never the bench value"}
+            # BASELINE config 5: the multi-area solve (fpf_areas_*) of the 123-bus
+            # feeder cut into 3 areas, one config-2 batch, host buffers, tolerance
+            # 1e-12, beside the monolithic host-buffer solve of the same batch
+            from freedm_amd import AreaPowerFlow
+            from freedm_amd.feeder import subtree_node_areas
+            pq_a = pq_h if layout == 0 else np.ascontiguousarray(pq_h.transpose(1, 2, 0))   # areas: [6][Nl][B]
+            ap = AreaPowerFlow(feeder, subtree_node_areas(feeder, [30, 60]), device=local)
+            ra = ap.solve(pq_a, tol=1e-12)
+            ta = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                ra = ap.solve(pq_a, tol=1e-12)
+                ta.append(time.perf_counter() - t0)
+            res["config5_areas"] = {"areas": len(ap.area_nodes), "area_nodes": ap.area_nodes, "scenarios": int(B),
+                                    "ms_per_batch": min(ta) * 1e3, "outer_iterations": int(ra["iters"].max()),
+                                    "converged": int((ra["status"] == 0).sum()),
+                                    "monolithic_host_ms": min(th) * 1e3,
+                                    "note": "fpf_areas_solve, host buffers, boundary exchange to 1e-12 p.u.; "
+                                            "tests/test_areas.py checks V against the monolithic solve to 1e-10"}
+            ap.close()
             res["config1_vvc_round"] = {"gpu_ms": min(tt) * 1e3, "stop_fwd": r1["stop_fwd"], "sent": r1["sent"],
                                         "candidates": 101, "kernel": pf1.kernel,
                                         "note": "fpf_vvc_round on the 9-row demo feeder, host-synchronous"}
