@@ -329,10 +329,41 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         WSTAMP(4 + 8 * it);
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
+#ifndef FPF_WAVE_GROUP
+#define FPF_WAVE_GROUP 1   // measured: 1 (grouped) -1.7 % on configs 2 and 4 against 0; 2 (pipelined) alike
+#endif
+#if FPF_WAVE_GROUP == 0
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(stg, p * PSTR + sb[c]), v[c][p]);
+#else
+        {
+            // a slot's three Sld reads issued together (FPF_WAVE_GROUP 2: the next
+            // slot's before this slot's arithmetic); scheduling barriers keep the
+            // groups, so the register allocator cannot fall back to one read in
+            // flight at a time
+            cx sl[3], sn[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sl[p] = ldx(stg, p * PSTR + sb[0]);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) sn[p] = ldx(stg, p * PSTR + sb[c + 1]);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(sl[p], v[c][p]);
+                if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) sn[p] = ldx(stg, p * PSTR + sb[c + 1]);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) sl[p] = sn[p];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#endif
 
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of IL;
         // Einc is gathered at subtree ends only (leaves)
@@ -406,6 +437,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         double lp[3] = {0.0, 0.0, 0.0};
         if (f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
             // one common off-diagonal zm: drop_a = (z_aa - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
+#if FPF_WAVE_GROUP == 0
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 // (ablation 65536: wave-uniform TEMP from the kernel arguments, no LDS reads)
@@ -420,6 +452,36 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
                 }
             }
+#else
+            // a slot's four TEMP reads issued together (2: the next slot's first)
+            cx tq[4], tn[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) tn[j] = ldx(tl, (j * C + c + 1) * L + li);
+                }
+                const cx m = tq[3];
+                const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
+                const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx d = tq[a];
+                    const cx b = ib[c][a];
+                    g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
+                    if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
+                }
+                if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) tn[j] = ldx(tl, (j * C + c + 1) * L + li);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) tq[j] = tn[j];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
         } else
 #pragma unroll
         for (int c = 0; c < C; ++c) {
