@@ -247,7 +247,10 @@ long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
 /* Diagnostics (no device needed): the wave kernel's plan for this feeder.
  * out[0..7] = {accepted (1/0), scenarios per wavefront, slots per lane,
  * wavefronts per workgroup, LDS bytes per workgroup, gathered scan entries,
- * blocks, block-chain depth}.  Returns FPF_OK or FPF_ERR_*. */
+ * blocks, block-chain depth}.  Feeders of 257..2048 branches get the
+ * wave-block kernel's plan: one scenario per workgroup of (wavefronts per
+ * workgroup) wavefronts, reported with 1 scenario per wavefront.
+ * Returns FPF_OK or FPF_ERR_*. */
 int         fpf_feeder_wave_plan(const double *dl, int nl, int ncols,
                                  const double *z, int z_rows, int z_cols,
                                  const fpf_opts *opts, int out[8]);
