@@ -13,6 +13,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libfreedm_pf.so")
 
+ABI_VERSION = 2   # include/freedm_pf.h FPF_ABI_VERSION
 FPF_OK, FPF_ERR_ARG, FPF_ERR_TOPOLOGY, FPF_ERR_HIP, FPF_ERR_NOMEM, FPF_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
 FPF_CONVERGED, FPF_NONCONVERGED = 0, 1
 FPF_KERNEL_AUTO, FPF_KERNEL_GENERIC, FPF_KERNEL_TILED, FPF_KERNEL_WAVE = 0, 1, 2, 3
@@ -23,7 +24,7 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_rtc_source",
            "fpf_selftest_division", "fpf_vvc_line_search", "fpf_feeder_wave_plan",
            "fpf_multi_create", "fpf_multi_destroy", "fpf_multi_last_error", "fpf_multi_solve", "fpf_multi_get_feeder",
-           "fpf_multi_shard", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
+           "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_round"]
 
 
@@ -31,7 +32,7 @@ class FpfOpts(C.Structure):
     _fields_ = [("bkva", C.c_double), ("bkv", C.c_double), ("vo_kv", C.c_double), ("eps", C.c_double),
                 ("mxitr", C.c_int), ("kernel", C.c_int), ("lb_v", C.c_double), ("ub_v", C.c_double),
                 ("tile", C.c_int), ("specialize", C.c_int), ("exact", C.c_int), ("layout", C.c_int),
-                ("reserved", C.c_int * 4)]
+                ("no_guard", C.c_int), ("reserved", C.c_int * 3)]
 
 
 class FpfFeederInfo(C.Structure):
@@ -52,7 +53,7 @@ _dp = C.POINTER(C.c_double)
 class FpfOutputs(C.Structure):
     _fields_ = [("vpolar", C.c_void_p), ("pqb", C.c_void_p), ("pql", C.c_void_p), ("v_re", C.c_void_p),
                 ("v_im", C.c_void_p), ("iters", C.c_void_p), ("status", C.c_void_p), ("loss", C.c_void_p),
-                ("vmin", C.c_void_p), ("vmax", C.c_void_p)]
+                ("vmin", C.c_void_p), ("vmax", C.c_void_p), ("errmx", C.c_void_p), ("guard", C.c_void_p)]
 
 
 class FpfAggregate(C.Structure):
@@ -136,6 +137,8 @@ def load(path: str | None = None):
         L.fpf_multi_get_feeder.restype = C.c_int
         L.fpf_multi_shard.argtypes = [C.c_int, C.c_int, C.c_long, C.POINTER(C.c_long), C.POINTER(C.c_long)]
         L.fpf_multi_shard.restype = C.c_int
+        L.fpf_multi_schedule.argtypes = [C.c_int, C.c_long, C.c_long, C.POINTER(C.c_long), C.c_long]
+        L.fpf_multi_schedule.restype = C.c_long
         L.fpf_aggregate_fold.argtypes = [C.POINTER(FpfAggregate), C.c_int, C.POINTER(FpfAggregate)]
         L.fpf_aggregate_fold.restype = None
     if hasattr(L, "fpf_areas_create") or path == LIB_PATH:
@@ -161,7 +164,7 @@ def load(path: str | None = None):
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
                  "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device"):
         getattr(L, name).restype = C.c_int
-    if L.fpf_abi_version() != 1:
+    if L.fpf_abi_version() != ABI_VERSION:
         raise RuntimeError("libfreedm_pf ABI mismatch")
     _lib = L
     return L

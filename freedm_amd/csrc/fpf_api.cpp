@@ -83,7 +83,25 @@ struct fpf_feeder {
     // auto choice between the interpreted tiled and the generic kernel, made
     // per batch (both table sets are built): tiled below AUTO_GENERIC_MIN_SCEN
     bool auto_batch = false;
+    // convergence guard of the fast kernels (fpf_opts.no_guard = 0): the scenarios
+    // flagged in the guard band [flag_cap] and their count (0 between solves: the
+    // fixup kernel resets it), and the fixup kernel's scratch (fixup_scratch_ld columns)
+    bool guard = false;
+    unsigned *d_flag_count = nullptr;
+    int32_t *d_flag_ids = nullptr;
+    int flag_cap = 0;
+    double *d_fix_scratch = nullptr;
 };
+
+// The guard band of the fast kernels' convergence test (fpf_opts.no_guard).
+// Ib(0) is a sum of the Nb load currents; the reference adds them in row order
+// (a recursive sum, rounding error <= (Nb - 1) u sum |IL|, u = 2^-53), the fast
+// kernels as a lane-local prefix plus a DPP scan (height <= 16: <= 16 u sum |IL|),
+// and their IL differ by a few u (one refined reciprocal vs __divdc3, <= 8 u
+// |IL|).  errmx compares this sweep's Ib(0) with the last one's, so its two
+// evaluations differ by at most about 2 (Nb + 24) u sum_k |IL_k|_1 (the iterates'
+// own differences, ~Nb u |V0 - V|, are smaller still); the band is twice that.
+static double guard_factor(int nb) { return 4.0 * (nb + 24) * 0x1p-53; }
 
 static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
     if (ctx) ctx->err = msg;
@@ -1358,6 +1376,18 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             fpf_feeder_destroy(f);
             return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
         }
+        if (!o.no_guard) {
+            f->guard = true;
+            w.guard_k = guard_factor(wh.n);
+            const size_t ld = fixup_scratch_ld(), per = (size_t)6 * (2 * d.nl + 2 * d.nn - 1);
+            e = hipMalloc(&f->d_flag_count, sizeof(unsigned));
+            if (e == hipSuccess) e = hipMemset(f->d_flag_count, 0, sizeof(unsigned));
+            if (e == hipSuccess) e = hipMalloc(&f->d_fix_scratch, sizeof(double) * per * ld);
+            if (e != hipSuccess) {
+                fpf_feeder_destroy(f);
+                return fail(ctx, FPF_ERR_HIP, std::string("guard buffers: ") + hipGetErrorString(e));
+            }
+        }
         f->wdev_big = w;
         f->wdev_big.wpb = wh.wpb_big_batch;
     }
@@ -1423,6 +1453,9 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_wave);
     (void)hipFree(f->d_lay);
     (void)hipHostFree(f->h_stage);
+    (void)hipFree(f->d_flag_count);
+    (void)hipFree(f->d_flag_ids);
+    (void)hipFree(f->d_fix_scratch);
     if (f->agg_event) (void)hipEventDestroy(f->agg_event);
     if (f->rtc) rtc_release(f->rtc_kernel);
     if (f->rtc_ib) rtc_release(f->rtc_kernel_ib);
@@ -1470,6 +1503,13 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
     if (!f || max_scen < 0) return FPF_ERR_ARG;
     fpf_ctx *ctx = f->ctx;
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (f->guard && max_scen > f->flag_cap) {   // the flag list holds every scenario of a batch
+        (void)hipFree(f->d_flag_ids);
+        f->d_flag_ids = nullptr;
+        f->flag_cap = 0;
+        HIPCHK(ctx, hipMalloc(&f->d_flag_ids, sizeof(int32_t) * std::max(max_scen, 1)));
+        f->flag_cap = max_scen;
+    }
     const bool need_scratch = kernel_for(f, max_scen) == FPF_KERNEL_GENERIC;
     if (max_scen <= f->cap) {
         if (!need_scratch || (f->d_scratch && f->scratch_ld >= (size_t)max_scen)) return FPF_OK;
@@ -1506,6 +1546,41 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
     return FPF_OK;
 }
 
+// device views of a batch's outputs; the per-scenario scalars the caller does
+// not ask for go to the feeder's own buffers (the aggregate reads them)
+static OutDev outdev_from(const fpf_feeder *f, const fpf_outputs &u, int layout) {
+    OutDev o;
+    std::memset(&o, 0, sizeof(o));
+    o.vpolar = u.vpolar;
+    o.pqb = u.pqb;
+    o.pql = u.pql;
+    o.v_re = u.v_re;
+    o.v_im = u.v_im;
+    o.iters = u.iters ? (int32_t *)u.iters : f->d_iters;
+    o.status = u.status ? (int8_t *)u.status : f->d_status;
+    o.loss = u.loss ? u.loss : f->d_loss;
+    o.vmin = u.vmin ? u.vmin : f->d_vmin;
+    o.vmax = u.vmax ? u.vmax : f->d_vmax;
+    o.smaj = layout == FPF_LAYOUT_SCEN_MAJOR ? 1 : 0;
+    o.errmx = u.errmx;
+    o.guard = (int8_t *)u.guard;
+    return o;
+}
+
+int fpf::fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
+                            void *stream, int layout) {
+    fpf_ctx *ctx = f->ctx;
+    if (!f->guard) return FPF_OK;
+    fpf_outputs none;
+    std::memset(&none, 0, sizeof(none));
+    OutDev o = outdev_from(f, d_out ? *d_out : none, layout);
+    o.agg = d_agg;
+    o.flag_count = f->d_flag_count;
+    o.flag_ids = f->d_flag_ids;
+    HIPCHK(ctx, launch_fixup(f->dev, n_scen, d_pq, f->d_fix_scratch, fixup_scratch_ld(), o, (hipStream_t)stream));
+    return FPF_OK;
+}
+
 extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out,
                                       double *d_agg, void *stream) {
     return fpf::solve_batch_device_ex(f, n_scen, d_pq, d_out, d_agg, stream, nullptr, nullptr,
@@ -1513,7 +1588,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
 }
 
 int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
-                               void *stream, const double *d_vsrc, double *d_s_in, int layout) {
+                               void *stream, const double *d_vsrc, double *d_s_in, int layout, unsigned *d_flag_out) {
     if (!f || n_scen < 0 || (n_scen > 0 && !d_pq)) return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "bad arguments");
     fpf_ctx *ctx = f->ctx;
     if (n_scen == 0) return FPF_OK;
@@ -1526,23 +1601,9 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     fpf_outputs none;
     std::memset(&none, 0, sizeof(none));
     const fpf_outputs &u = d_out ? *d_out : none;
-    OutDev o;
-    o.vpolar = u.vpolar;
-    o.pqb = u.pqb;
-    o.pql = u.pql;
-    o.v_re = u.v_re;
-    o.v_im = u.v_im;
-    o.iters = u.iters ? (int32_t *)u.iters : f->d_iters;
-    o.status = u.status ? (int8_t *)u.status : f->d_status;
-    o.loss = u.loss ? u.loss : f->d_loss;
-    o.vmin = u.vmin ? u.vmin : f->d_vmin;
-    o.vmax = u.vmax ? u.vmax : f->d_vmax;
-    o.agg = nullptr;
-    o.partials = nullptr;
-    o.ticket = nullptr;
+    OutDev o = outdev_from(f, u, layout);
     o.vsrc = d_vsrc;
     o.s_in = d_s_in;
-    o.smaj = layout == FPF_LAYOUT_SCEN_MAJOR ? 1 : 0;
     hipError_t e;
     bool agg_done = false;
     const int kern = kernel_for(f, n_scen);
@@ -1597,8 +1658,27 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     }
     if ((d_vsrc || d_s_in) && kern != FPF_KERNEL_WAVE)
         return fail(ctx, FPF_ERR_UNSUPPORTED, "per-scenario source voltages need the wave kernel");
+    // the convergence guard: the fast kernel flags, the exact fixup kernel re-solves
+    // (areas with per-scenario sources have no exact counterpart: no guard there)
+    const bool guarded = kern == FPF_KERNEL_WAVE && f->guard && !d_vsrc && !d_s_in;
+    if (guarded) {
+        if (f->flag_cap < n_scen) {
+            int rc = fpf_feeder_reserve(f, n_scen);
+            if (rc) return rc;
+        }
+        o.flag_count = f->d_flag_count;
+        o.flag_ids = f->d_flag_ids;
+        o.flag_out = agg_done ? d_flag_out : nullptr;
+    }
     if (kern == FPF_KERNEL_WAVE) {
-        e = f->wdev.wps ? launch_wblk(f->wdev, n_scen, d_pq, o, st) : launch_wave(wave_dev_for(f, n_scen), n_scen, d_pq, o, st);
+        WaveDev w = f->wdev.wps ? f->wdev : wave_dev_for(f, n_scen);
+        if (!guarded) w.guard_k = 0.0;
+        e = w.wps ? launch_wblk(w, n_scen, d_pq, o, st) : launch_wave(w, n_scen, d_pq, o, st);
+        // the exact re-solve of flagged scenarios: enqueued after every fast solve
+        // (it exits at once when none was flagged), unless the host API defers it
+        // until it has read the count (d_flag_out)
+        if (e == hipSuccess && guarded && !(d_flag_out && agg_done))
+            e = launch_fixup(f->dev, n_scen, d_pq, f->d_fix_scratch, fixup_scratch_ld(), o, st);
     } else if (kern == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {
             std::string err;
@@ -1668,14 +1748,20 @@ int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf
     std::memset(&none, 0, sizeof(none));
     const fpf_outputs &u = out ? *out : none;
     const size_t B = (size_t)n_scen, nn = (size_t)f->info.nn, nl = (size_t)f->info.nl;
-    // staging layout: pq | vpolar | pqb | pql | v_re | v_im | iters | status | loss | vmin | vmax | aggregate
+    // staging layout: pq | vpolar | pqb | pql | v_re | v_im | iters | status | loss | vmin | vmax | errmx |
+    // guard | aggregate | guard count (the count of scenarios the fast kernel flagged
+    // for the exact re-solve comes back with the results: no extra launch or copy
+    // when none was)
+    constexpr int NP = 15;
     struct Part { void *host; size_t bytes; size_t off; };
     double h_agg[8];
-    Part parts[12] = {
+    unsigned h_flag[2] = {0, 0};
+    Part parts[NP] = {
         {(void *)pq, 6 * nl * B * 8, 0}, {u.vpolar, 6 * nn * B * 8, 0}, {u.pqb, 6 * nn * B * 8, 0},
         {u.pql, 6 * nn * B * 8, 0},      {u.v_re, 3 * nn * B * 8, 0},  {u.v_im, 3 * nn * B * 8, 0},
         {u.iters, 4 * B, 0},             {u.status, B, 0},             {u.loss, 8 * B, 0},
-        {u.vmin, 8 * B, 0},              {u.vmax, 8 * B, 0},           {h_agg, sizeof(h_agg), 0}};
+        {u.vmin, 8 * B, 0},              {u.vmax, 8 * B, 0},           {u.errmx, 8 * B, 0},
+        {u.guard, B, 0},                 {h_agg, sizeof(h_agg), 0},    {h_flag, sizeof(h_flag), 0}};
     size_t total = 0;
     for (Part &p : parts) {
         if (!p.host) continue;
@@ -1703,34 +1789,54 @@ int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf
     d.loss = (double *)dptr(8);
     d.vmin = (double *)dptr(9);
     d.vmax = (double *)dptr(10);
-    int rc = fpf::solve_batch_device_ex(f, n_scen, (const double *)dptr(0), &d, (double *)dptr(11), (void *)ctx->stream,
-                                        nullptr, nullptr, layout);
+    d.errmx = (double *)dptr(11);
+    d.guard = (signed char *)dptr(12);
+    // the guard count: written by the fast kernel's aggregating workgroup (only a
+    // guarded fast solve does; else it stays 0)
+    const bool guarded = f->guard && kernel_for(f, n_scen) == FPF_KERNEL_WAVE;
+    HIPCHK(ctx, hipMemsetAsync(dptr(14), 0, sizeof(h_flag), ctx->stream));
+    int rc = fpf::solve_batch_device_ex(f, n_scen, (const double *)dptr(0), &d, (double *)dptr(13), (void *)ctx->stream,
+                                        nullptr, nullptr, layout, guarded ? (unsigned *)dptr(14) : nullptr);
     if (rc) return rc;
     // the outputs are one contiguous region after pq: small ones (a VVC round's
     // solves, a batch's per-scenario scalars) come back in one copy into pinned
     // memory -- each copy costs tens of microseconds of latency -- large ones
     // straight into the caller's arrays
     size_t o0 = total;
-    for (int i = 1; i < 12; ++i)
+    for (int i = 1; i < NP; ++i)
         if (parts[i].host) o0 = std::min(o0, parts[i].off);
     const size_t obytes = total - o0;
-    if (obytes <= (size_t)4 << 20) {
-        if (obytes > f->h_stage_bytes) {
-            (void)hipHostFree(f->h_stage);
-            f->h_stage = nullptr;
-            f->h_stage_bytes = 0;
-            HIPCHK(ctx, hipHostMalloc(&f->h_stage, std::max(obytes, (size_t)1 << 16)));
-            f->h_stage_bytes = std::max(obytes, (size_t)1 << 16);
+    auto bring_back = [&]() -> int {
+        if (obytes <= (size_t)4 << 20) {
+            if (obytes > f->h_stage_bytes) {
+                (void)hipHostFree(f->h_stage);
+                f->h_stage = nullptr;
+                f->h_stage_bytes = 0;
+                HIPCHK(ctx, hipHostMalloc(&f->h_stage, std::max(obytes, (size_t)1 << 16)));
+                f->h_stage_bytes = std::max(obytes, (size_t)1 << 16);
+            }
+            HIPCHK(ctx, hipMemcpyAsync(f->h_stage, sb + o0, obytes, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+            for (int i = 1; i < NP; ++i)
+                if (parts[i].host) std::memcpy(parts[i].host, (char *)f->h_stage + (parts[i].off - o0), parts[i].bytes);
+        } else {
+            for (int i = 1; i < NP; ++i)
+                if (parts[i].host)
+                    HIPCHK(ctx, hipMemcpyAsync(parts[i].host, dptr(i), parts[i].bytes, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         }
-        HIPCHK(ctx, hipMemcpyAsync(f->h_stage, sb + o0, obytes, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        for (int i = 1; i < 12; ++i)
-            if (parts[i].host) std::memcpy(parts[i].host, (char *)f->h_stage + (parts[i].off - o0), parts[i].bytes);
-    } else {
-        for (int i = 1; i < 12; ++i)
-            if (parts[i].host)
-                HIPCHK(ctx, hipMemcpyAsync(parts[i].host, dptr(i), parts[i].bytes, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        return FPF_OK;
+    };
+    rc = bring_back();
+    if (rc) return rc;
+    if (guarded && h_flag[0] > 0) {
+        // some decisions fell within the guard band: re-solve those scenarios on the
+        // exact kernel (results and aggregate in place), then bring everything back again
+        rc = fpf::fixup_batch_device(f, n_scen, (const double *)dptr(0), &d, (double *)dptr(13), (void *)ctx->stream,
+                                     layout);
+        if (rc) return rc;
+        rc = bring_back();
+        if (rc) return rc;
     }
     if (agg) std::memcpy(agg, h_agg, sizeof(h_agg));
     return (int)h_agg[4];   // non-converged count

@@ -350,7 +350,8 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     fpf_outputs none;
     std::memset(&none, 0, sizeof(none));
     const fpf_outputs &u = out ? *out : none;
-    if (u.vpolar || u.pqb || u.pql) return afail(a, FPF_ERR_UNSUPPORTED, "fpf_areas_solve: Vpolar / PQb / PQL not produced");
+    if (u.vpolar || u.pqb || u.pql || u.errmx || u.guard)
+        return afail(a, FPF_ERR_UNSUPPORTED, "fpf_areas_solve: Vpolar / PQb / PQL / errmx / guard not produced");
     if (n_scen == 0) {
         if (agg) fpf_aggregate_fold(nullptr, 0, agg);
         return 0;

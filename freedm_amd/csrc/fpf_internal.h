@@ -155,6 +155,10 @@ struct WaveDev {
     // factorised: per slot lng and code, per code Zl (temp_sym: z_aa - zm x 3, zm;
     // else the 9 entries row-major (l, a))
     int32_t wps, ncode;
+    // convergence guard (fpf_opts.no_guard = 0): a decision whose errmx lies within
+    // guard_k * sum_k |IL_k|_1 of eps is flagged for the exact re-solve
+    // (fpf_api.cpp: guard_factor); 0 = off
+    double guard_k;
     const double *slot_lng;     // [C][L]
     const int32_t *slot_code;   // [C][L] 0-based line code
     const double *code_z;       // [ncode][4 or 9] complex
@@ -180,7 +184,22 @@ struct OutDev {
     // 1 [B][field][row] (the wave kernels read / write it natively; the host
     // transposes around the generic and tiled kernels, fpf_layout.hip)
     int32_t smaj;
+    // per-scenario errmx of the last sweep and the guard flag (fpf_outputs; may be NULL)
+    double *errmx;
+    int8_t *guard;
+    // fast kernels with the guard on: scenarios whose convergence decision fell in the
+    // guard band, appended as they finish (flag_ids [B]); NULL = guard off.  flag_out
+    // (host API): the aggregating workgroup copies the final count there
+    unsigned *flag_count;
+    int32_t *flag_ids;
+    unsigned *flag_out;
 };
+
+// The exact re-solve of flagged scenarios (fpf_generic.hip: dpf_fixup_kernel):
+// scenario flag_ids[j] of the batch (B scenarios, layout smaj) for j < *flag_count,
+// outputs at their batch index, then the batch aggregate again if agg != NULL;
+// the count is reset to 0 for the next launch.
+constexpr int FIXUP_BLOCKS = 1;   // one workgroup: 4 x 21 scenarios per pass
 
 #ifndef __HIPCC_RTC__
 }  // namespace fpf
@@ -190,7 +209,11 @@ int ctx_device(const fpf_ctx *ctx);   // the HIP device of a context
 // fpf_solve_batch_device with the wave kernel's two extra per-scenario arrays
 // (OutDev::vsrc, OutDev::s_in; both device memory, may be NULL)
 int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
-                          void *stream, const double *d_vsrc, double *d_s_in, int layout);
+                          void *stream, const double *d_vsrc, double *d_s_in, int layout,
+                          unsigned *d_flag_out = nullptr);
+// the exact re-solve of the scenarios a deferred (d_flag_out) guarded solve flagged
+int fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
+                       void *stream, int layout);
 // fpf_solve_batch in an explicit batch layout (internal callers build their own
 // batches in FPF_LAYOUT_SCEN_FASTEST whatever the feeder's fpf_opts.layout)
 int solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf_outputs *out, fpf_aggregate *agg,
@@ -199,6 +222,9 @@ int solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf_outp
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st);
 hipError_t launch_tiled(const FeederDev &f, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+hipError_t launch_fixup(const FeederDev &f, int n_scen, const double *pq, double *scratch, size_t ld, const OutDev &o,
+                        hipStream_t st);
+size_t fixup_scratch_ld();
 hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss,
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
                             double *d_agg, double *partials, unsigned *ticket, hipStream_t st);

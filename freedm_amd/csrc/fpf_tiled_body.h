@@ -351,6 +351,8 @@ __device__ __forceinline__ void tiled_body(const FeederDev &f, int B, const doub
                 if (errmx < f.eps || it == f.mxitr - 1) {
                     if (o.iters) o.iters[s0 + qs] = it + 1;
                     if (o.status) o.status[s0 + qs] = errmx < f.eps ? 0 : 1;
+                    if (o.errmx) o.errmx[s0 + qs] = errmx;
+                    if (o.guard) o.guard[s0 + qs] = 0;   // exact kernel: no guard band
                 }
             }
         }

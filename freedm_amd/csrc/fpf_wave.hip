@@ -137,7 +137,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     double2 *const stg = (double2 *)(knode + C * L);
     double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
-    const int RS = (3 * XC + noff + 3) | 1;                          // double2 per region
+    const int RS = (3 * XC + noff + 4) | 1;                          // double2 per region (+ the guard record)
     double2 *const X = reg0 + sc * RS;
     double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
     // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
@@ -318,6 +318,20 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     // last scenario is done.
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     bool done = !live;
+    // the guard record V0S[3] = (sum_k |S_k|_1, closest |err2 - eps^2| of a decision
+    // in the coarse band, +inf: none) of the scenario, in LDS (fpf_api.cpp: guard_factor)
+    if (o.flag_count) {
+        double sabs = 0.0;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx x = ldx(stg, p * PSTR + sb[c]);
+                sabs += fabs(x.re) + fabs(x.im);
+            }
+        sabs = seg_incl<L>(sabs);
+        if (li == L - 1) V0S[3] = make_double2(sabs, INFINITY);
+    }
 #ifdef FPF_WAVE_STAGGER
     // diagnostic: start the second half of the workgroup's waves (each shares a
     // SIMD with one of the first half) later, so partners sit in different
@@ -424,6 +438,21 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         const unsigned long long cbits = __ballot(li == L - 1 && err2 < f.eps * f.eps);
         const bool conv = (cbits >> (seg * L + L - 1)) & 1;
         const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
+        if (o.flag_count) {
+            // ---- the convergence guard (fpf_opts.no_guard = 0): the decision above
+            // tests a scan-ordered Ib(0).  Where errmx lies within the rounding band
+            // of eps (fpf_api.cpp: guard_factor) the reference's sequential sum could
+            // decide the other way.  Decisions within 2^-9 of eps^2 (rare) keep their
+            // distance from eps^2 in the scenario's LDS record (no register stays
+            // live for it); the band itself is evaluated after the loop
+            const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
+            if (li == L - 1 && !done && dd <= 0x1p-9 * e2) {
+                double2 g = V0S[3];
+                g.y = fmin(g.y, dd);
+                V0S[3] = g;
+            }
+        }
+        if (fin && li == L - 1 && o.errmx) o.errmx[s] = sqrt(err2);
         // the loss terms are needed only in a scenario's last sweep
         const bool any_fin = __ballot(fin) != 0;
         WSTAMP(7 + 8 * it);
@@ -729,6 +758,37 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         }
     }
 
+    // ---- the guard band (fpf_api.cpp: guard_factor) for the scenarios with a decision
+    // in the coarse band: errmx within tau = guard_k sum_k |IL_k|_1 of eps, where
+    // sum_k |IL_k|_1 <= sqrt2 sum_k |S_k|_1 / min_k |V_k| over the nonzero V (the
+    // final V; 1.25 covers its drift from the deciding sweep's).  Flagged scenarios
+    // are re-solved on the exact kernel (dpf_fixup_kernel)
+    if (o.flag_count && live) {
+        const double2 g = V0S[3];
+        const bool cand = g.y < INFINITY;
+        if (__ballot(cand) != 0) {
+            double m2 = INFINITY;
+            for (int k = li; k < nn; k += L) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + (k - 1) * SROW + sc);
+                    const double d = fma(vv.re, vv.re, vv.im * vv.im);
+                    if (d > 0.0) m2 = fmin(m2, d);
+                }
+            }
+            m2 = seg_reduce_min<L>(m2);
+            const double tau = 1.25 * f.guard_k * 1.4142135623730951 * g.x / sqrt(m2);
+            const bool near = cand && g.y <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
+            if (li == L - 1 && near)
+                o.flag_ids[__hip_atomic_fetch_add(o.flag_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = s;
+            if (li == L - 1 && o.guard) o.guard[s] = near ? 1 : 0;
+        } else if (li == L - 1 && o.guard) {
+            o.guard[s] = 0;
+        }
+    } else if (live && li == L - 1 && o.guard) {
+        o.guard[s] = 0;   // (guard off)
+    }
+
     // ---- fused batch aggregate [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over,
     // n_under, n_scen] over converged scenarios: the workgroup's partial in
     // scenario order, published with agent-scope stores; one ticket per
@@ -839,6 +899,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             }
             if (threadIdx.x < 8) o.agg[threadIdx.x] = sh[threadIdx.x * NT];
             if (threadIdx.x == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // (every workgroup's flags were appended before its ticket)
+            if (threadIdx.x == 0 && o.flag_out)
+                *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -846,7 +909,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 3) | 1);
+    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4) | 1);
     const size_t stage = 16 * 3 * ((size_t)w.nl + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
     const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;

@@ -202,6 +202,20 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     __syncthreads();
     if (WABL(4)) return;
 
+    // the guard record: sum_k |S_k|_1 of the scenario (wtb[7], read after the loop;
+    // Sld is overwritten by V in the last sweep)
+    if (o.flag_count) {
+        double a = 0.0;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx x = ldx(stg, p * PS + sb[c]);
+                a += fabs(x.re) + fabs(x.im);
+            }
+        a = seg_incl<64>(a);
+        if (lane == 63) wtb[8 * wv + 7] = a;
+    }
     cx v[C][3];
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
@@ -212,6 +226,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     int it = 0;
     bool conv = false;
+    double dmin = INFINITY;  // closest |err2 - eps^2| of a decision in the guard's coarse band
+    double err2_last = 0.0;
     for (;; ++it) {
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
@@ -280,6 +296,14 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         }
         conv = __builtin_amdgcn_readfirstlane(err2 < f.eps * f.eps ? 1 : 0) != 0;
         const bool fin = conv || it == f.mxitr - 1;
+        if (fin) err2_last = err2;
+        // the convergence guard (fpf_wave.hip): err2 is the same in every lane of the
+        // workgroup; a decision within 2^-9 of eps^2 keeps its distance in a register
+        // (evaluated against the band after the loop)
+        if (o.flag_count) {
+            const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
+            if (dd <= 0x1p-9 * e2) dmin = fmin(dmin, dd);
+        }
 
         // ---- branch drops lng * (Ib . Zl) (:163-178); in the last sweep also
         // Re(drop . conj(Ib)) per phase for the VVC loss (fpf_wave.hip: the loss identity)
@@ -428,7 +452,9 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     // ---- Vmin/Vmax (V_abc_list.cpp:7-81, VoltVarCtrl.cpp:1201-1207)
     if (FULL && f.has_mask) {
         // general V_abc_list: per phase the first K_p nonzero |V| in node order,
-        // zero padded; one wave per phase, 64 nodes per step (ballot ranks)
+        // zero padded; one wave per phase, 64 nodes per step (ballot ranks); also
+        // min over every nonzero |V|^2 of the wave's phases (the guard band)
+        double mz = INFINITY;
         for (int p = wv; p < 3; p += W) {
             const int K = f.K[p];
             int cnt = 0;
@@ -441,6 +467,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
                 }
                 const bool nz = k < nn && m != 0.0;
+                if (nz) mz = fmin(mz, m * m);
                 const unsigned long long bal = __ballot(nz);
                 const int rank = cnt + __popcll(bal & ((1ull << lane) - 1ull));
                 if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
@@ -454,6 +481,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 vx[2 * p + 1] = mx;
             }
         }
+        mz = seg_reduce_min<64>(mz);
+        if (lane == 63) wtf[8 * wv + 5] = mz;   // (the forward totals are dead)
     } else {
         // no zeroed phases: every Lnum_p + 1 = Nn and V_abc_list keeps every row --
         // the plain extremes of |V| (|V|^2 compared, one sqrt each)
@@ -506,6 +535,29 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         if (o.iters) o.iters[s] = it + 1;
         if (o.status) o.status[s] = conv ? 0 : 1;
         if (o.loss) o.loss[s] = x;
+        if (o.errmx) o.errmx[s] = sqrt(err2_last);
+        if (o.flag_count) {
+            // the guard band (fpf_api.cpp: guard_factor) of a decision in the coarse
+            // band: errmx within tau = guard_k sum_k |IL_k|_1 of eps, with sum_k
+            // |IL_k|_1 <= sqrt2 sum_k |S_k|_1 / min_k |V_k| over the nonzero V (the
+            // final V; 1.25 covers its drift from the deciding sweep's); flagged
+            // scenarios are re-solved on the exact kernel (dpf_fixup_kernel)
+            bool near = false;
+            if (dmin < INFINITY) {
+                double sabs = 0.0, m2 = INFINITY;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    sabs += wtb[8 * w + 7];
+                    m2 = fmin(m2, (FULL && f.has_mask) ? wtf[8 * w + 5] : wtf[8 * w + 6]);
+                }
+                const double tau = 1.25 * f.guard_k * 1.4142135623730951 * sabs / sqrt(m2);
+                near = dmin <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
+            }
+            if (o.guard) o.guard[s] = near ? 1 : 0;
+            if (near) o.flag_ids[__hip_atomic_fetch_add(o.flag_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = s;
+        } else if (o.guard) {
+            o.guard[s] = 0;
+        }
         if (o.vmin) o.vmin[s] = mn;
         if (o.vmax) o.vmax[s] = mx;
 #pragma unroll
@@ -578,6 +630,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             }
             if (tid < 8) o.agg[tid] = sh[tid * NT];
             if (tid == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0 && o.flag_out)   // (every workgroup's flag was appended before its ticket)
+                *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

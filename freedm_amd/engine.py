@@ -90,7 +90,7 @@ def _host_batch(pq, nl: int, nn: int, smaj: bool, full: bool):
         raise ValueError(f"pq must be [B][6][{nl}]" if smaj else f"pq must be [6][{nl}][B]")
     B = pq.shape[0] if smaj else pq.shape[2]
     r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
-         "vmin": np.zeros(B), "vmax": np.zeros(B)}
+         "vmin": np.zeros(B), "vmax": np.zeros(B), "errmx": np.zeros(B), "guard": np.zeros(B, np.int8)}
     if full:
         sh6, sh3 = ((B, 6, nn), (B, 3, nn)) if smaj else ((6, nn, B), (3, nn, B))
         r.update(Vpolar=np.zeros(sh6), PQb=np.zeros(sh6), PQL=np.zeros(sh6), V_re=np.zeros(sh3), V_im=np.zeros(sh3))
@@ -154,7 +154,7 @@ class PowerFlow:
         pq, B, r = _host_batch(pq, self.nl, self.nn, self.opts.layout == 1, full)
         out = _lib.FpfOutputs(_ptr(r.get("Vpolar")), _ptr(r.get("PQb")), _ptr(r.get("PQL")), _ptr(r.get("V_re")),
                               _ptr(r.get("V_im")), _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]),
-                              _ptr(r["vmin"]), _ptr(r["vmax"]))
+                              _ptr(r["vmin"]), _ptr(r["vmax"]), _ptr(r["errmx"]), _ptr(r["guard"]))
         agg = _lib.FpfAggregate()
         rc = L.fpf_solve_batch(self.h, B, pq.ctypes.data_as(_lib._dp), C.byref(out), C.byref(agg))
         if rc < 0:
@@ -172,7 +172,8 @@ class PowerFlow:
         B = int(pq.shape[0] if self.opts.layout == 1 else pq.shape[2])
         g = out.get
         o = _lib.FpfOutputs(_ptr(g("vpolar")), _ptr(g("pqb")), _ptr(g("pql")), _ptr(g("v_re")), _ptr(g("v_im")),
-                            _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")))
+                            _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")),
+                            _ptr(g("errmx")), _ptr(g("guard")))
         st = None
         if stream is not None:
             st = stream if isinstance(stream, int) else int(stream.cuda_stream)
@@ -188,7 +189,8 @@ class PowerFlow:
         B = int(pq.shape[0] if self.opts.layout == 1 else pq.shape[2])
         g = out.get
         o = _lib.FpfOutputs(_ptr(g("vpolar")), _ptr(g("pqb")), _ptr(g("pql")), _ptr(g("v_re")), _ptr(g("v_im")),
-                            _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")))
+                            _ptr(g("iters")), _ptr(g("status")), _ptr(g("loss")), _ptr(g("vmin")), _ptr(g("vmax")),
+                            _ptr(g("errmx")), _ptr(g("guard")))
         st = C.c_void_p(None if stream is None else (stream if isinstance(stream, int) else int(stream.cuda_stream)))
         h, pq_p, o_ref = self.h, C.c_void_p(_ptr(pq)), C.byref(o)
         fs, fa = L.fpf_solve_batch_device, L.fpf_aggregate_device
@@ -371,7 +373,7 @@ class MultiPowerFlow:
         pq, B, r = _host_batch(pq, self.nl, self.nn, self.opts.layout == 1, full)
         out = _lib.FpfOutputs(_ptr(r.get("Vpolar")), _ptr(r.get("PQb")), _ptr(r.get("PQL")), _ptr(r.get("V_re")),
                               _ptr(r.get("V_im")), _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]),
-                              _ptr(r["vmin"]), _ptr(r["vmax"]))
+                              _ptr(r["vmin"]), _ptr(r["vmax"]), _ptr(r["errmx"]), _ptr(r["guard"]))
         agg = _lib.FpfAggregate()
         rc = L.fpf_multi_solve(self.h, B, pq.ctypes.data_as(_lib._dp), C.byref(out), C.byref(agg))
         if rc < 0:

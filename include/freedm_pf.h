@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define FPF_ABI_VERSION 1
+#define FPF_ABI_VERSION 2   /* 2: fpf_outputs.errmx / .guard, fpf_opts.no_guard */
 
 /* return codes */
 #define FPF_OK               0
@@ -100,7 +100,15 @@ typedef struct fpf_opts {
                           columns P1 Q1 P2 Q2 P3 Q3 of Dl (DPF_return7.cpp:46-50), one
                           scenario after another -- and outputs [B][col][row].  The
                           per-scenario scalars are [B] either way; B = 1 is the same. */
-    int    reserved[4];
+    int    no_guard;   /* 0 (default): fast-mode convergence guard.  The fast kernels sum
+                          Ib(0) in another order than the reference, so a scenario whose
+                          errmx lands within the rounding band of eps at some sweep could
+                          stop one sweep apart from it (DPF_return7.cpp:199-210).  Such
+                          scenarios are flagged in the kernel (band: 4 (Nb + 16) 2^-53
+                          sum_k |IL_k|_1, the scan's worst-case rounding difference) and
+                          re-solved on the exact kernel, whose decisions are the reference's
+                          order of operations.  1: no guard (diagnostics). */
+    int    reserved[3];
 } fpf_opts;
 
 #define FPF_LAYOUT_SCEN_FASTEST 0   /* [field][row][B]: a workgroup of consecutive scenarios reads rows */
@@ -136,6 +144,11 @@ typedef struct fpf_outputs {
     double      *loss;     /* [B] kW   (VoltVarCtrl.cpp:1152-1161)             */
     double      *vmin;     /* [B] p.u. (VoltVarCtrl.cpp:1201-1207)             */
     double      *vmax;     /* [B] p.u.                                         */
+    double      *errmx;    /* [B] errmx = max_p |Ib(0,p) - Ibo(p)| of the scenario's last sweep,
+                              the value tested against eps (DPF_return7.cpp:199-204)          */
+    signed char *guard;    /* [B] 1: a convergence decision of the fast kernel fell within the
+                              guard band and the scenario was re-solved on the exact kernel
+                              (its results are the exact kernel's); 0 otherwise               */
 } fpf_outputs;
 
 /* Batch aggregate (the hosting-study reduction).  Also the payload of the
@@ -188,7 +201,7 @@ int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double 
  * stream and feeder each) and builds an RCCL communicator over them
  * (ncclCommInitAll; xGMI inside an MI355X node).  fpf_multi_solve cuts the
  * batch into contiguous shards (fpf_multi_shard), solves every shard on its
- * device concurrently and combines the per-device batch aggregates with one
+ * device concurrently (pinned, double-buffered chunks: fpf_multi_schedule) and combines the per-device batch aggregates with one
  * RCCL all-reduce (sum of the 8 fields, min of vmin, max of vmax) -- the only
  * exchange: per-scenario results go straight back to the caller's host arrays
  * at their global index.  pq / out / agg as fpf_solve_batch (host memory, the
@@ -208,6 +221,14 @@ int         fpf_multi_get_feeder(fpf_multi *m, int device, fpf_feeder **out);
 /* The partition (no device needed): scenarios [lo, hi) of `rank` out of
  * n_total over n_gpus, contiguous, sizes differing by at most one. */
 int         fpf_multi_shard(int rank, int n_gpus, long n_total, long *lo, long *hi);
+/* The order fpf_multi_solve issues its work in (no device needed): every
+ * transfer goes through pinned staging in chunks of at most `chunk` scenarios,
+ * double-buffered per device; round r issues chunk r of every device (pack,
+ * H2D, solve, D2H; nothing waits) before it collects round r - 1 (wait,
+ * unpack), so the devices run concurrently from one host thread.  ops[4 i ..]
+ * = {kind (0 issue, 1 collect), device, lo, hi}; at most max_ops entries are
+ * written; returns the number of operations or FPF_ERR_ARG. */
+long        fpf_multi_schedule(int n_gpus, long n_scen, long chunk, long *ops, long max_ops);
 /* The combine the all-reduce performs, on the host (no device needed):
  * sums of fields 0 and 3..7, min of vmin, max of vmax; n = 0 gives the identity. */
 void        fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate *out);

@@ -28,7 +28,8 @@ class RefOut(C.Structure):
     _fields_ = [("vpolar", C.POINTER(C.c_double)), ("pqb", C.POINTER(C.c_double)),
                 ("pql", C.POINTER(C.c_double)), ("v", C.POINTER(C.c_double)),
                 ("ib", C.POINTER(C.c_double)), ("il", C.POINTER(C.c_double)),
-                ("iters", C.c_int), ("status", C.c_int), ("errmx", C.c_double)]
+                ("iters", C.c_int), ("status", C.c_int), ("errmx", C.c_double),
+                ("errmx_trace", C.POINTER(C.c_double))]
 
 
 def build(force: bool = False) -> str:
@@ -59,6 +60,11 @@ def lib():
                                     dp, dp, dp, dp, dp,
                                     C.POINTER(C.c_int), C.POINTER(C.c_byte),
                                     dp, dp, dp, C.c_int]
+        L.ref_dpf_batch_ex.argtypes = [dp, C.c_int, C.c_int, dp, C.c_int, C.c_int,
+                                       C.POINTER(RefOpts), C.c_int, dp,
+                                       dp, dp, dp, dp, dp,
+                                       C.POINTER(C.c_int), C.POINTER(C.c_byte),
+                                       dp, dp, dp, dp, C.c_int]
         _lib = L
     return _lib
 
@@ -104,12 +110,13 @@ def dpf_solve(Dl, Z, opts: RefOpts | None = None) -> dict:
     v = np.zeros((nn, 3), dtype=np.complex128, order="F")
     ib = np.zeros((max(nn - 1, 1), 3), dtype=np.complex128, order="F")
     il = np.zeros((nn, 3), dtype=np.complex128, order="F")
+    o = opts if opts is not None else default_opts()
+    trace = np.full(max(o.mxitr, 1), np.nan)
     out = RefOut(_dp(vp), _dp(pb), _dp(pl), v.ctypes.data_as(C.POINTER(C.c_double)),
                  ib.ctypes.data_as(C.POINTER(C.c_double)), il.ctypes.data_as(C.POINTER(C.c_double)),
-                 0, 0, 0.0)
-    o = opts if opts is not None else default_opts()
+                 0, 0, 0.0, _dp(trace))
     rc = L.ref_dpf_solve(_dp(dl), nl, ncols, _dp(zb), zshape[0], zshape[1], C.byref(o), C.byref(out))
-    res = {"status": rc, "iters": out.iters, "errmx": out.errmx}
+    res = {"status": rc, "iters": out.iters, "errmx": out.errmx, "errmx_trace": trace[:max(out.iters, 0)].copy()}
     if rc >= 0:
         res.update(Vpolar=np.ascontiguousarray(vp), PQb=np.ascontiguousarray(pb),
                    PQL=np.ascontiguousarray(pl), V=np.ascontiguousarray(v),
@@ -152,18 +159,18 @@ def dpf_batch(Dl, Z, pq, opts: RefOpts | None = None, nthreads: int = 1, want_fu
     nn = L.ref_count_nodes(_dp(dl), nl, ncols)
     out = {
         "iters": np.zeros(B, dtype=np.int32), "status": np.zeros(B, dtype=np.int8),
-        "loss": np.zeros(B), "vmin": np.zeros(B), "vmax": np.zeros(B),
+        "loss": np.zeros(B), "vmin": np.zeros(B), "vmax": np.zeros(B), "errmx": np.zeros(B),
     }
     if want_full:
         out.update(Vpolar=np.zeros((6, nn, B)), PQb=np.zeros((6, nn, B)), PQL=np.zeros((6, nn, B)),
                    V_re=np.zeros((3, nn, B)), V_im=np.zeros((3, nn, B)))
     o = opts if opts is not None else default_opts()
     g = out.get
-    rc = L.ref_dpf_batch(_dp(dl), nl, ncols, _dp(zb), zshape[0], zshape[1], C.byref(o), B, _dp(pq),
-                         _dp(g("Vpolar")), _dp(g("PQb")), _dp(g("PQL")), _dp(g("V_re")), _dp(g("V_im")),
-                         out["iters"].ctypes.data_as(C.POINTER(C.c_int)),
-                         out["status"].ctypes.data_as(C.POINTER(C.c_byte)),
-                         _dp(out["loss"]), _dp(out["vmin"]), _dp(out["vmax"]), nthreads)
+    rc = L.ref_dpf_batch_ex(_dp(dl), nl, ncols, _dp(zb), zshape[0], zshape[1], C.byref(o), B, _dp(pq),
+                            _dp(g("Vpolar")), _dp(g("PQb")), _dp(g("PQL")), _dp(g("V_re")), _dp(g("V_im")),
+                            out["iters"].ctypes.data_as(C.POINTER(C.c_int)),
+                            out["status"].ctypes.data_as(C.POINTER(C.c_byte)),
+                            _dp(out["loss"]), _dp(out["vmin"]), _dp(out["vmax"]), _dp(out["errmx"]), nthreads)
     out["rc"] = rc
     return out
 

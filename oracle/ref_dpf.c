@@ -292,6 +292,7 @@ static int solve_ws(const double *dl, int nl, const double *z, int z_rows,
             errmx = df[0];
             for (a = 1; a < 3; ++a) if (df[a] > errmx) errmx = df[a];
         }
+        if (out->errmx_trace) out->errmx_trace[i] = errmx;
         for (a = 0; a < 3; ++a) Ibo[a] = w->ib[a];
         iters = i + 1;
         if (errmx < eps) { status = REF_CONVERGED; break; }
@@ -454,7 +455,7 @@ typedef struct batch_job {
     int n_scen, s0, s1, nn;
     const int *lnum;
     const double *pq;
-    double *vpolar, *pqb, *pql, *v_re, *v_im, *loss, *vmin, *vmax;
+    double *vpolar, *pqb, *pql, *v_re, *v_im, *loss, *vmin, *vmax, *errmx;
     int *iters; signed char *status;
     int n_nonconv, rc;
 } batch_job;
@@ -490,6 +491,7 @@ static void *batch_worker(void *arg)
         if (out.status != REF_CONVERGED) jb->n_nonconv++;
         if (jb->iters) jb->iters[s] = out.iters;
         if (jb->status) jb->status[s] = (signed char)out.status;
+        if (jb->errmx) jb->errmx[s] = out.errmx;
         if (jb->loss || jb->vmin || jb->vmax) {
             double l, mn, mx;
             ref_vvc_reduce(vp, pb, pl, nn, jb->lnum, &l, &mn, &mx);
@@ -525,6 +527,19 @@ int ref_dpf_batch(const double *dl, int nl, int ncols,
                   double *loss, double *vmin, double *vmax,
                   int nthreads)
 {
+    return ref_dpf_batch_ex(dl, nl, ncols, z, z_rows, z_cols, o, n_scen, pq, vpolar, pqb, pql, v_re, v_im, iters,
+                            status, loss, vmin, vmax, NULL, nthreads);
+}
+
+int ref_dpf_batch_ex(const double *dl, int nl, int ncols,
+                     const double *z, int z_rows, int z_cols,
+                     const ref_opts *o, int n_scen, const double *pq,
+                     double *vpolar, double *pqb, double *pql,
+                     double *v_re, double *v_im,
+                     int *iters, signed char *status,
+                     double *loss, double *vmin, double *vmax, double *errmx,
+                     int nthreads)
+{
     int rc, nn, t, lnum[3], total = 0;
     ref_opts od;
     batch_job *jobs;
@@ -546,6 +561,7 @@ int ref_dpf_batch(const double *dl, int nl, int ncols,
         jb->s1 = (int)((long long)n_scen * (t + 1) / nthreads);
         jb->vpolar = vpolar; jb->pqb = pqb; jb->pql = pql; jb->v_re = v_re; jb->v_im = v_im;
         jb->iters = iters; jb->status = status; jb->loss = loss; jb->vmin = vmin; jb->vmax = vmax;
+        jb->errmx = errmx;
         if (nthreads == 1) batch_worker(jb);
         else pthread_create(&th[t], NULL, batch_worker, jb);
     }

@@ -53,6 +53,7 @@ typedef struct ref_out {
     int     iters;   /* sweeps executed (i+1 at the converging sweep, mxitr otherwise) */
     int     status;  /* REF_* */
     double  errmx;   /* errmx of the last sweep                                        */
+    double *errmx_trace;  /* [mxitr] errmx of every sweep executed (may be NULL)        */
 } ref_out;
 
 void ref_opts_default(ref_opts *o);
@@ -107,6 +108,16 @@ int ref_vvc_gradient(const double *dl, int nl, int ncols, const double *z, int z
 int ref_vvc_main(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols, const ref_opts *o,
                  double beta0, double alpha, int m_max, int ld, double *g, double *load_nodes, int *n_loads,
                  double *loss_fwd, double *loss_rev, double *dl_out, double *res);
+
+/* ref_dpf_batch with the per-scenario errmx of the last sweep (errmx may be NULL) */
+int ref_dpf_batch_ex(const double *dl, int nl, int ncols,
+                     const double *z, int z_rows, int z_cols,
+                     const ref_opts *o, int n_scen, const double *pq,
+                     double *vpolar, double *pqb, double *pql,
+                     double *v_re, double *v_im,
+                     int *iters, signed char *status,
+                     double *loss, double *vmin, double *vmax, double *errmx,
+                     int nthreads);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,144 @@
+"""The fast kernels' convergence guard (fpf_opts.no_guard = 0).
+
+DPF_return7 stops at the first sweep with errmx < eps (Broker/src/vvc/
+DPF_return7.cpp:199-210).  The wave and wave-block kernels sum Ib(0) as a
+prefix scan, the reference (and the oracle, oracle/ref_dpf.c) as a sequential
+backward sweep; where errmx lands within that rounding difference of eps the
+two could stop one sweep apart.  The kernels flag every decision within the
+band 4 (Nb + 24) 2^-53 sum_k |IL_k|_1 of eps and the library re-solves those
+scenarios on the exact kernel (dpf_fixup_kernel), whose operations are the
+oracle's -- so the sweep counts are the oracle's by construction.
+
+The inputs are built to sit on the threshold: for each base scenario, a load
+scale and then one load entry are bisected to adjacent doubles around the
+point where the oracle's sweep count changes (tests/near_eps.py), leaving the
+deciding errmx within ~1e-14 (123-bus) to ~1e-12 (2048-bus; the oracle's own
+rounding steps) relative of eps -- both sides of every boundary.  Bars:
+identical iteration counts and status on every such scenario, V within 1e-10,
+every scenario inside the band flagged (guard = 1) and its results the exact
+kernel's; and on an ordinary batch nothing flagged and errmx equal to the
+oracle's within the band.
+"""
+import numpy as np
+import pytest
+
+from freedm_amd import feeder as F
+
+from near_eps import near_eps_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _vrel(r, c):
+    a = r["V_re"] + 1j * r["V_im"]
+    b = c["V_re"] + 1j * c["V_im"]
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))
+
+
+def _near_eps(n, n_pairs=8):
+    from oracle import oracle as O
+    f = F.synthetic_feeder(n, n)
+    base = F.scenario_loads(f, np.arange(40))
+    a, ma = near_eps_batch(O, f, base, n_pairs, 0.05, 1.0)     # light loads: 2..4 sweeps
+    b, mb = near_eps_batch(O, f, base, n_pairs, 1.0, 3.0)      # heavier: 5..7 sweeps
+    return f, np.ascontiguousarray(np.concatenate([a, b], axis=2)), np.concatenate([ma, mb])
+
+
+@pytest.mark.parametrize("n", [123, 2048])
+@pytest.mark.parametrize("layout", [0, 1])
+def test_near_eps_iterations_identical(n, layout):
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f, pq, margins = _near_eps(n)
+    assert margins.max() < 1e-11 and (margins < 1e-13).any(), margins
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    pf = PowerFlow(f, layout=layout)
+    assert pf.kernel == "wave"
+    x = pq if layout == 0 else np.ascontiguousarray(pq.transpose(2, 0, 1))
+    r = pf.solve(x)
+    if layout == 1:
+        r = {k: (np.ascontiguousarray(np.moveaxis(v, 0, -1)) if isinstance(v, np.ndarray) and v.ndim == 3 else v)
+             for k, v in r.items()}
+    assert (r["iters"] == c["iters"]).all(), (r["iters"], c["iters"])
+    assert (r["status"] == c["status"]).all()
+    assert _vrel(r, c) <= 1e-10
+    # every decision inside the band was flagged and re-solved on the exact kernel:
+    # its iterations, errmx and V are the oracle's to the bit
+    assert (r["guard"] == 1).all(), r["guard"]
+    np.testing.assert_allclose(r["errmx"], c["errmx"], rtol=4e-16)   # hypot: ocml vs glibc, an ulp
+    np.testing.assert_array_equal(r["V_re"], c["V_re"])
+    np.testing.assert_array_equal(r["V_im"], c["V_im"])
+    # the aggregate was recomputed over the corrected results
+    ag = r["aggregate"]
+    conv = r["status"] == 0
+    assert ag["n_conv"] == conv.sum() and ag["n_scen"] == pq.shape[2]
+    assert ag["loss_sum"] == pytest.approx(float(r["loss"][conv].sum()), rel=1e-12)
+    assert ag["vmin"] == r["vmin"][conv].min() and ag["vmax"] == r["vmax"][conv].max()
+
+
+@pytest.mark.parametrize("n", [123, 2048])
+def test_near_eps_device_paths(n):
+    """The device API (the fixup kernel enqueued after every fast solve, with and
+    without a fused aggregate) and the one-process multi-GPU entry give the host
+    API's results on the near-threshold batch."""
+    import torch
+    from freedm_amd import MultiPowerFlow, PowerFlow
+    f, pq, _ = _near_eps(n, 4)
+    pf = PowerFlow(f)
+    h = pf.solve(pq)
+    B, nn = pq.shape[2], pf.nn
+    dev = torch.device("cuda:0")
+    for with_agg in (False, True):
+        out = {"v_re": torch.zeros((3, nn, B), dtype=torch.float64, device=dev),
+               "v_im": torch.zeros((3, nn, B), dtype=torch.float64, device=dev),
+               "iters": torch.zeros(B, dtype=torch.int32, device=dev),
+               "status": torch.zeros(B, dtype=torch.int8, device=dev),
+               "loss": torch.zeros(B, dtype=torch.float64, device=dev),
+               "errmx": torch.zeros(B, dtype=torch.float64, device=dev),
+               "guard": torch.zeros(B, dtype=torch.int8, device=dev)}
+        agg = torch.zeros(8, dtype=torch.float64, device=dev) if with_agg else None
+        pf.solve_device(torch.from_numpy(pq).to(dev), out, agg=agg)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out["iters"].cpu().numpy(), h["iters"])
+        np.testing.assert_array_equal(out["guard"].cpu().numpy(), h["guard"])
+        np.testing.assert_array_equal(out["errmx"].cpu().numpy(), h["errmx"])
+        np.testing.assert_array_equal(out["v_re"].cpu().numpy(), h["V_re"])
+        np.testing.assert_array_equal(out["loss"].cpu().numpy(), h["loss"])
+        if with_agg:
+            a = agg.cpu().numpy()
+            assert a[3] == h["aggregate"]["n_conv"] and a[7] == B
+            assert a[0] == pytest.approx(h["aggregate"]["loss_sum"], rel=1e-12)
+    m = MultiPowerFlow(f, n_gpus=1)
+    r = m.solve(pq)
+    for k in ("iters", "status", "errmx", "guard", "V_re", "V_im", "loss"):
+        np.testing.assert_array_equal(r[k], h[k], err_msg=k)
+    m.close()
+
+
+@pytest.mark.parametrize("n,B", [(123, 4096), (2048, 256)])
+def test_guard_quiet_on_ordinary_batch(n, B):
+    """On an ordinary batch no decision is anywhere near eps: nothing is flagged
+    (the fast path runs alone) and errmx equals the oracle's within the band."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(n, n)
+    pq = F.scenario_loads(f, np.arange(B))
+    r = PowerFlow(f).solve(pq, full=False)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8, want_full=False)
+    assert (r["iters"] == c["iters"]).all()
+    assert not r["guard"].any()
+    np.testing.assert_allclose(r["errmx"], c["errmx"], rtol=1e-8)
+
+
+def test_guard_off_reports_fast_decisions():
+    """no_guard = 1 (diagnostics): the fast kernel's own decisions, nothing
+    re-solved -- errmx still agrees with the oracle's to the band's width."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f, pq, _ = _near_eps(123, 4)
+    r = PowerFlow(f, no_guard=1).solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert not r["guard"].any()
+    np.testing.assert_allclose(r["errmx"], c["errmx"], rtol=1e-9)
+    mism = int((r["iters"] != c["iters"]).sum())
+    print(f"near-eps batch without the guard: {mism} of {pq.shape[2]} sweep counts differ from the oracle")
