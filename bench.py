@@ -108,42 +108,46 @@ def _time_oracle(O, feeder, pq, threads: int, seconds: float):
     return n_conv / dt, passes, dt
 
 
-def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: bool = True):
+def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: bool = True, legs: int = 3):
     """The CPU oracle (oracle/ref_dpf.c, a scalar port of DPF_return7 + the VVC
-    reductions) on this host: once on every usable CPU (value, cores) and once
-    on a single core.  Bounded sample: `seconds` of the all-core leg plus
-    3 x seconds/6 of the single-core leg over one chunk of the config-2 batch."""
+    reductions) on this host: on every usable CPU (value, cores) and on one CPU,
+    each as the median of `legs` legs of seconds / legs over the same chunk of the
+    config-2 batch.  The single-CPU legs run with the process pinned to one CPU
+    of its affinity set (os.sched_setaffinity), so the lone thread is not moved
+    between cores; the per-core rate is the better of that and the all-CPU rate
+    divided by its threads, and the full-host estimate scales it by the host's
+    physical cores (not measured: the box's cgroup grants only `cores` CPUs)."""
     from oracle import oracle as O
     from freedm_amd import scenario_loads
     threads, cpu_info = usable_cpus()
     pq = scenario_loads(feeder, np.arange(chunk), seed=SCEN_SEED)
-    v_all, passes, dt = _time_oracle(O, feeder, pq, threads, seconds)
-    pq1 = np.ascontiguousarray(pq[:, :, :min(4096, chunk)])
-    # single core: best of three legs (a lone thread's rate on a shared host varies
-    # with what the other cores run; the best leg is the least disturbed)
-    legs = [_time_oracle(O, feeder, pq1, 1, max(1.0, seconds / 6)) for _ in range(3)]
-    v_one, passes1, dt1 = max(legs, key=lambda r: r[0])
+    leg_s = max(1.0, seconds / legs)
+    all_legs = [_time_oracle(O, feeder, pq, threads, leg_s) for _ in range(legs)]
+    v_all = float(np.median([r[0] for r in all_legs]))
+    passes, dt = sum(r[1] for r in all_legs), sum(r[2] for r in all_legs)
+    aff = sorted(os.sched_getaffinity(0))
+    try:
+        os.sched_setaffinity(0, {aff[len(aff) // 2]})
+        one_legs = [_time_oracle(O, feeder, pq, 1, leg_s) for _ in range(legs)]
+    finally:
+        os.sched_setaffinity(0, set(aff))
+    v_one = float(np.median([r[0] for r in one_legs]))
+    passes1, dt1 = sum(r[1] for r in one_legs), sum(r[2] for r in one_legs)
+    per_core = max(v_one, v_all / threads)
     phys, logical = _host_cores()
     out_c1 = None
     if config1:
-        # BASELINE config 1 end to end: one sequential vvc_main round of the reference
-        # (gradient + step-size search, 2m+1 DPF calls) on the demo feeder, one core
-        from freedm_amd.feeder import demo_feeder
-        d = demo_feeder()
-        O.vvc_main(d.Dl, d.Z)
-        t_round = []
-        for _ in range(5):
-            t0 = time.perf_counter()
-            r = O.vvc_main(d.Dl, d.Z)
-            t_round.append(time.perf_counter() - t0)
-        out_c1 = {"ms": min(t_round) * 1e3, "dpf_calls": int(r["calls"]), "stop_fwd": int(r["stop_fwd"]),
-                  "note": "oracle/ref_vvc.c vvc_main (VoltVarCtrl.cpp:1141-1762), best of 5, one core"}
+        out_c1 = config1_cpu()
     out = {"value": v_all, "unit": "converged scenarios/s", "cores": threads, "kind": "port",
-           "sample": f"{passes} passes x {chunk} scenarios of the batch ({feeder.name}, seed {SCEN_SEED}), "
-                     f"oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s; single core: "
-                     f"best of 3 legs of {passes1} passes x {pq1.shape[2]} scenarios, {dt1:.1f} s",
-           "single_core": {"value": v_one, "unit": "converged scenarios/s", "cores": 1},
+           "sample": f"median of {legs} legs, {passes} passes x {chunk} scenarios of the batch ({feeder.name}, seed "
+                     f"{SCEN_SEED}), oracle/ref_dpf.c ({threads} pthreads, -O3, no FMA), {dt:.1f} s; single core: "
+                     f"median of {legs} legs pinned to CPU {aff[len(aff) // 2]}, {passes1} passes x {chunk} "
+                     f"scenarios, {dt1:.1f} s",
+           "legs": [r[0] for r in all_legs],
+           "single_core": {"value": v_one, "unit": "converged scenarios/s", "cores": 1,
+                           "legs": [r[0] for r in one_legs]},
            "parallel_efficiency": v_all / (v_one * threads),
+           "per_core_rate": per_core,
            "cpu_model": _cpu_model(), "host_physical_cores": phys, "host_logical_cpus": logical,
            }
     if out_c1:
@@ -151,8 +155,35 @@ def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: boo
     out.update(cpu_info)
     if phys:
         # not measured: what the whole host would give if the port scaled linearly
-        # over every physical core (the box's cgroup grants only `cores` CPUs)
-        out["full_host_linear_estimate"] = v_one * phys
+        # over every physical core at the better-measured per-core rate
+        out["full_host_linear_estimate"] = per_core * phys
+    return out
+
+
+def config1_feeders():
+    """BASELINE config 1's feeders: the reference's own 9-row demo feeder
+    (load_system_data.cpp), Broker/Dl_new.mat (IEEE 34-node, with the supplied Z)
+    and the synthetic 123-bus feeder."""
+    from freedm_amd import demo_feeder, dl_new_feeder, synthetic_feeder
+    return [("demo", demo_feeder()), ("dl_new", dl_new_feeder()), ("123bus", synthetic_feeder(123, 123))]
+
+
+def config1_cpu(reps: int = 5):
+    """One sequential vvc_main round of the reference (gradient + step-size
+    search, 2m+1 DPF calls; oracle/ref_vvc.c, VoltVarCtrl.cpp:1141-1762) per
+    config-1 feeder, one core, best of `reps`."""
+    from oracle import oracle as O
+    out = {}
+    for name, f in config1_feeders():
+        O.vvc_main(f.Dl, f.Z)
+        t_round = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = O.vvc_main(f.Dl, f.Z)
+            t_round.append(time.perf_counter() - t0)
+        out[name] = {"ms": min(t_round) * 1e3, "dpf_calls": int(r["calls"]), "stop_fwd": int(r["stop_fwd"]),
+                     "reversed": int(r["reversed"])}
+    out["note"] = "oracle/ref_vvc.c vvc_main (VoltVarCtrl.cpp:1141-1762), best of %d, one core" % reps
     return out
 
 
@@ -489,19 +520,23 @@ def main():
                                      "note": "torch copy_ of 1 GiB, read+write bytes; roofline.frac stays "
                                              "against the 8 TB/s spec"}
         if world == 1 and args.config == 2 and not args.no_c4 and not args.nodes and not args.scenarios:
-            # BASELINE config 1: one whole VVC round (fpf_vvc_round: gradient on the
-            # host after a device solve, all m_max+1 step sizes as one batch, the
-            # reversal) on the demo feeder; host-synchronous, best of 20
-            from freedm_amd import demo_feeder
-            d1 = demo_feeder()
-            pf1 = PowerFlow(d1, device=local)
-            for _ in range(3):
-                r1 = pf1.vvc_round(d1.Dl)
-            tt = []
-            for _ in range(20):
-                t0 = time.perf_counter()
-                r1 = pf1.vvc_round(d1.Dl)
-                tt.append(time.perf_counter() - t0)
+            # BASELINE config 1: one whole VVC round (fpf_vvc_round: the gradient
+            # after a device solve, all m_max+1 step sizes as one batch, the
+            # reversal) per config-1 feeder (demo, Dl_new.mat, 123-bus);
+            # host-synchronous, best of 20 (5 for the 123-bus feeder)
+            c1 = {}
+            for name1, d1 in config1_feeders():
+                pf1 = PowerFlow(d1, device=local)
+                for _ in range(2):
+                    r1 = pf1.vvc_round(d1.Dl)
+                tt = []
+                for _ in range(5 if d1.nl > 100 else 20):
+                    t0 = time.perf_counter()
+                    r1 = pf1.vvc_round(d1.Dl)
+                    tt.append(time.perf_counter() - t0)
+                c1[name1] = {"gpu_ms": min(tt) * 1e3, "stop_fwd": int(r1["stop_fwd"]), "sent": int(r1["sent"]),
+                             "reversed": int(r1["reversed"]), "kernel": pf1.kernel, "nl": int(d1.nl)}
+                pf1.close()
             # the host-buffer entry (fpf_solve_batch: PCIe copies in and out included;
             # per-scenario scalars out, no V), one config-2 batch
             pq_h = d_pqs[0].cpu().numpy()
@@ -535,10 +570,9 @@ def main():
                                     "note": "fpf_areas_solve, host buffers, boundary exchange to 1e-12 p.u.; "
                                             "tests/test_areas.py checks V against the monolithic solve to 1e-10"}
             ap.close()
-            res["config1_vvc_round"] = {"gpu_ms": min(tt) * 1e3, "stop_fwd": r1["stop_fwd"], "sent": r1["sent"],
-                                        "candidates": 101, "kernel": pf1.kernel,
-                                        "note": "fpf_vvc_round on the 9-row demo feeder, host-synchronous"}
-            pf1.close()
+            c1["note"] = ("fpf_vvc_round (gradient + 101 step sizes in one batch + reversal), host-synchronous, "
+                          "per config-1 feeder")
+            res["config1_vvc_round"] = c1
         if world == 1 and args.config == 3 and not args.no_cpu_baseline and not args.nodes:
             # the 2048-bus feeder on the host: a bounded sample of 1024 scenarios
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds, chunk=1024, config1=False)
@@ -548,8 +582,11 @@ def main():
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
             if "config1_vvc_round" in res and "config1_vvc_main" in cb:
-                res["config1_vvc_round"]["cpu_ms"] = cb["config1_vvc_main"]["ms"]
-                res["config1_vvc_round"]["speedup"] = cb["config1_vvc_main"]["ms"] / res["config1_vvc_round"]["gpu_ms"]
+                for name1, c in res["config1_vvc_round"].items():
+                    if isinstance(c, dict) and name1 in cb["config1_vvc_main"]:
+                        c["cpu_ms"] = cb["config1_vvc_main"][name1]["ms"]
+                        c["cpu_dpf_calls"] = cb["config1_vvc_main"][name1]["dpf_calls"]
+                        c["speedup"] = c["cpu_ms"] / c["gpu_ms"]
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = value / cb["value"]
             res["speedup_vs_cpu_single_core"] = value / cb["single_core"]["value"]

@@ -91,6 +91,9 @@ struct fpf_feeder {
     int32_t *d_flag_ids = nullptr;
     int flag_cap = 0;
     double *d_fix_scratch = nullptr;
+    // the guard's local mode inside the wave kernel (solves without an aggregate):
+    // the exact op lists as a device-side FeederDev
+    FeederDev *d_fixdev = nullptr;
 };
 
 // The guard band of the fast kernels' convergence test (fpf_opts.no_guard).
@@ -1383,6 +1386,8 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             e = hipMalloc(&f->d_flag_count, sizeof(unsigned));
             if (e == hipSuccess) e = hipMemset(f->d_flag_count, 0, sizeof(unsigned));
             if (e == hipSuccess) e = hipMalloc(&f->d_fix_scratch, sizeof(double) * per * ld);
+            if (e == hipSuccess) e = hipMalloc(&f->d_fixdev, sizeof(FeederDev));
+            if (e == hipSuccess) e = hipMemcpy(f->d_fixdev, &d, sizeof(FeederDev), hipMemcpyHostToDevice);
             if (e != hipSuccess) {
                 fpf_feeder_destroy(f);
                 return fail(ctx, FPF_ERR_HIP, std::string("guard buffers: ") + hipGetErrorString(e));
@@ -1456,6 +1461,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_flag_count);
     (void)hipFree(f->d_flag_ids);
     (void)hipFree(f->d_fix_scratch);
+    (void)hipFree(f->d_fixdev);
     if (f->agg_event) (void)hipEventDestroy(f->agg_event);
     if (f->rtc) rtc_release(f->rtc_kernel);
     if (f->rtc_ib) rtc_release(f->rtc_kernel_ib);
@@ -1669,15 +1675,23 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
         o.flag_count = f->d_flag_count;
         o.flag_ids = f->d_flag_ids;
         o.flag_out = agg_done ? d_flag_out : nullptr;
+        if (!agg_done && !d_agg && !f->wdev.wps &&
+            (size_t)96 * (f->dev.nl + f->dev.nn) <= wave_lds_bytes(wave_dev_for(f, n_scen))) {
+            // no aggregate to recompute: every wave-kernel workgroup re-solves the
+            // scenarios it flagged itself, in its LDS (no second launch, nothing
+            // global on the common path)
+            o.fix_dev = f->d_fixdev;
+        }
     }
     if (kern == FPF_KERNEL_WAVE) {
         WaveDev w = f->wdev.wps ? f->wdev : wave_dev_for(f, n_scen);
         if (!guarded) w.guard_k = 0.0;
         e = w.wps ? launch_wblk(w, n_scen, d_pq, o, st) : launch_wave(w, n_scen, d_pq, o, st);
-        // the exact re-solve of flagged scenarios: enqueued after every fast solve
-        // (it exits at once when none was flagged), unless the host API defers it
-        // until it has read the count (d_flag_out)
-        if (e == hipSuccess && guarded && !(d_flag_out && agg_done))
+        // with an aggregate, the exact re-solve of flagged scenarios (and the
+        // aggregate again) is a launch of its own after the fast solve (it exits at
+        // once when none was flagged), unless the host API defers it until it has
+        // read the count (d_flag_out)
+        if (e == hipSuccess && guarded && !o.fix_dev && !(d_flag_out && agg_done))
             e = launch_fixup(f->dev, n_scen, d_pq, f->d_fix_scratch, fixup_scratch_ld(), o, st);
     } else if (kern == FPF_KERNEL_TILED) {
         if (f->rtc && o.pqb && !f->rtc_ib) {

@@ -193,6 +193,12 @@ struct OutDev {
     unsigned *flag_count;
     int32_t *flag_ids;
     unsigned *flag_out;
+    // the guard's local mode (wave kernel, a solve without an aggregate): each
+    // workgroup re-solves the scenarios it flagged itself on the exact body
+    // (fpf_generic_body.h: g3_fixup_local) with fix_dev's op lists, its state in
+    // the workgroup's LDS; fix_dev = NULL: the flags go to the batch's list and a
+    // dpf_fixup_kernel launch re-solves them
+    const struct FeederDev *fix_dev;
 };
 
 // The exact re-solve of flagged scenarios (fpf_generic.hip: dpf_fixup_kernel):

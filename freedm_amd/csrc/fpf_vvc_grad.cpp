@@ -13,10 +13,11 @@
 // It is a few hundred buses solved once per 9 s round with long double
 // accumulators (the F and J sums), so it runs on the host in x87 extended
 // precision exactly like the reference's build; the DPF solves around it run
-// on the GPU.  inv() is LAPACK in the reference; here an LU with partial
-// pivoting (agreement to rounding: tests/test_vvc_gradient.py).
+// on the GPU.  inv() is LAPACK in the reference; here one LU solve with partial
+// pivoting (agreement to rounding: tests/test_vvc_round.py).
 #include "../../include/freedm_pf.h"
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstring>
@@ -46,9 +47,12 @@ struct PhaseNet {
     cplx y(int a, int b) const { return Y[(size_t)a + (size_t)b * (lnum + 1)]; }
 };
 
-// LU with partial pivoting, then A^-1 column by column (A n x n column-major)
-bool invert(std::vector<double> a, int n, std::vector<double> &inv) {
-    std::vector<int> piv(n);
+// Solve A x = b by LU with partial pivoting (A n x n column-major, b -> x).
+// lambda = -inv(J^T) Fx needs one solve, not the inverse the reference forms
+// (LAPACK getri, then a product): n^3 / 3 operations instead of n^3, the same
+// result to rounding (1e-10 against the oracle's inverse, tests/test_vvc_round.py).
+// The elimination runs column by column (contiguous in column-major storage).
+bool lu_solve(std::vector<double> a, int n, std::vector<double> &x) {
     auto A = [&](int r, int c) -> double & { return a[(size_t)r + (size_t)c * n]; };
     for (int k = 0; k < n; ++k) {
         int p = k;
@@ -58,29 +62,28 @@ bool invert(std::vector<double> a, int n, std::vector<double> &inv) {
                 best = std::fabs(A(i, k));
                 p = i;
             }
-        piv[k] = p;
         if (best == 0) return false;
-        if (p != k)
+        if (p != k) {
             for (int j = 0; j < n; ++j) std::swap(A(k, j), A(p, j));
-        for (int i = k + 1; i < n; ++i) {
-            const double l = A(i, k) / A(k, k);
-            A(i, k) = l;
-            for (int j = k + 1; j < n; ++j) A(i, j) -= l * A(k, j);
+            std::swap(x[k], x[p]);
         }
+        const double piv = A(k, k);
+        double *ck = &A(0, k);
+        for (int i = k + 1; i < n; ++i) ck[i] /= piv;
+        for (int j = k + 1; j < n; ++j) {
+            const double akj = A(k, j);
+            if (akj == 0) continue;
+            double *cj = &A(0, j);
+            for (int i = k + 1; i < n; ++i) cj[i] -= ck[i] * akj;
+        }
+        const double xk = x[k];
+        if (xk != 0)
+            for (int i = k + 1; i < n; ++i) x[i] -= ck[i] * xk;
     }
-    inv.assign((size_t)n * n, 0.0);
-    std::vector<double> x(n);
-    for (int j = 0; j < n; ++j) {
-        for (int i = 0; i < n; ++i) x[i] = i == j ? 1.0 : 0.0;
-        for (int k = 0; k < n; ++k)
-            if (piv[k] != k) std::swap(x[k], x[piv[k]]);
-        for (int i = 0; i < n; ++i)
-            for (int k = 0; k < i; ++k) x[i] -= A(i, k) * x[k];
-        for (int i = n - 1; i >= 0; --i) {
-            for (int k = i + 1; k < n; ++k) x[i] -= A(i, k) * x[k];
-            x[i] /= A(i, i);
-        }
-        for (int i = 0; i < n; ++i) inv[(size_t)i + (size_t)j * n] = x[i];
+    for (int i = n - 1; i >= 0; --i) {
+        double v = x[i];
+        for (int k = i + 1; k < n; ++k) v -= A(i, k) * x[k];
+        x[i] = v / A(i, i);
     }
     return true;
 }
@@ -170,20 +173,40 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
         std::vector<int> ka(n);
         ka[0] = (int)P.sbus[0].real();
         for (int i = 0; i < L; ++i) ka[i + 1] = (int)P.rbus[i].real();
+        // (form_Yabc's loops visit, per entry, the branches in order: the diagonal
+        // adds every branch touching ka[m], an off-diagonal subtracts first the
+        // branches s -> r, then those r -> s.  Assembled here branch by branch from
+        // the positions of each bus in ka -- the same additions per entry in the same
+        // order, O(L) instead of O(n^2 L))
         P.Y.assign((size_t)n * n, 0.0);
-        for (int m = 0; m < n; ++m)
-            for (int q = 0; q < n; ++q) {
-                cplx &e = P.Y[(size_t)m + (size_t)q * n];
-                if (m == q) {
-                    for (int i = 0; i < L; ++i)
-                        if ((int)P.sbus[i].real() == ka[m] || (int)P.rbus[i].real() == ka[m]) e = e + yy[i];
-                } else {
-                    for (int i = 0; i < L; ++i)
-                        if ((int)P.sbus[i].real() == ka[m] && (int)P.rbus[i].real() == ka[q]) e = e - yy[i];
-                    for (int i = 0; i < L; ++i)
-                        if ((int)P.rbus[i].real() == ka[m] && (int)P.sbus[i].real() == ka[q]) e = e - yy[i];
-                }
+        {
+            std::vector<std::vector<int>> at_node;
+            auto pos = [&](int node) -> const std::vector<int> & {
+                static const std::vector<int> none;
+                return node >= 0 && node < (int)at_node.size() ? at_node[node] : none;
+            };
+            int mx = 0;
+            for (int m = 0; m < n; ++m) mx = std::max(mx, ka[m]);
+            at_node.resize((size_t)mx + 1);
+            for (int m = 0; m < n; ++m)
+                if (ka[m] >= 0) at_node[ka[m]].push_back(m);
+            for (int i = 0; i < L; ++i) {
+                const int si = (int)P.sbus[i].real(), ri = (int)P.rbus[i].real();
+                // diagonal: once per m with ka[m] == si or ka[m] == ri
+                for (int m : pos(si)) P.Y[(size_t)m + (size_t)m * n] += yy[i];
+                if (ri != si)
+                    for (int m : pos(ri)) P.Y[(size_t)m + (size_t)m * n] += yy[i];
             }
+            // off-diagonal: all s -> r contributions of an entry precede its r -> s ones
+            for (int pass = 0; pass < 2; ++pass)
+                for (int i = 0; i < L; ++i) {
+                    const int si = (int)P.sbus[i].real(), ri = (int)P.rbus[i].real();
+                    const int a = pass == 0 ? si : ri, b = pass == 0 ? ri : si;
+                    for (int m : pos(a))
+                        for (int q : pos(b))
+                            if (m != q) P.Y[(size_t)m + (size_t)q * n] -= yy[i];
+                }
+        }
         // V_abc_list (V_abc_list.cpp): the first n rows with a nonzero |V| of this phase
         P.V.assign(n, 0.0);
         P.theta.assign(n, 0.0);
@@ -259,17 +282,12 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
                 }
             }
         }
-        std::vector<double> Ji;
-        if (!invert(Jt, nf, Ji)) {
+        std::vector<double> lam(Fx);
+        if (!lu_solve(Jt, nf, lam)) {
             *err = "singular Jacobian";
             return FPF_ERR_TOPOLOGY;
         }
-        std::vector<double> lam(nf, 0.0);
-        for (int a = 0; a < nf; ++a) {
-            double acc = 0;
-            for (int b = 0; b < nf; ++b) acc += (-Ji[(size_t)a + (size_t)b * nf]) * Fx[b];
-            lam[a] = acc;
-        }
+        for (double &v : lam) v = -v;
         // g_vq = -gu^T lambda, gu = [0; Gqq], Gqq(ia, ja) = -1 where V-list bus ia+1 is load ja
         n_loads[x] = std::min(lload[x], ld);
         double gx_min = INFINITY, gx_max = 0.0;
@@ -338,6 +356,23 @@ extern "C" int fpf_vvc_gradient(fpf_feeder *feeder, const double *ctrl_dl, int n
         stats[6] = vmax;
         stats[7] = iters;
     }
+    return FPF_OK;
+}
+
+extern "C" int fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+                                   const double *vpolar, int nn, double bkva, double bkv, double beta0, int ld,
+                                   double *g, double *load_nodes, int *n_loads, double *stats) {
+    (void)z_cols;
+    if (!ctrl_dl || !z || !vpolar || !g || !load_nodes || !n_loads || ld < 1 || ncols < 12 || nn < 2 ||
+        !(bkva > 0) || !(bkv > 0))
+        return FPF_ERR_ARG;
+    std::string err;
+    double st[4] = {0, 0, 0, 0};
+    const int gr = gradient(Table{ctrl_dl, nl}, ncols, z, z_rows, vpolar, nn, bkva, bkv, beta0, ld, g, load_nodes,
+                            n_loads, st, &err);
+    if (gr != FPF_OK) return gr;
+    if (stats)
+        for (int i = 0; i < 4; ++i) stats[i] = st[i];
     return FPF_OK;
 }
 

@@ -47,6 +47,7 @@
 #include "fpf_internal.h"
 #include "fpf_math.hpp"
 #include "fpf_wave_common.h"
+#include "fpf_generic_body.h"
 
 namespace fpf {
 
@@ -110,6 +111,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     if ((int)blockIdx.x >= f.stag_lo && (int)blockIdx.x < f.stag_hi)
         for (int i = 0; i < f.stag_n; ++i) __builtin_amdgcn_s_sleep(127);
     WSTAMP(0);
+    // the guard's local list (OutDev::fix_dev): scenarios this workgroup flagged
+    __shared__ int fix_n, fix_ids[SPB];
+    if (threadIdx.x == 0) fix_n = 0;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int seg = lane / L, li = lane % L;
     const int sc = wv * SPW + seg;                 // scenario within the workgroup
@@ -780,7 +784,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             const double tau = 1.25 * f.guard_k * 1.4142135623730951 * g.x / sqrt(m2);
             const bool near = cand && g.y <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
             if (li == L - 1 && near)
-                o.flag_ids[__hip_atomic_fetch_add(o.flag_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = s;
+                guard_flag(o, s, &fix_n, fix_ids);
             if (li == L - 1 && o.guard) o.guard[s] = near ? 1 : 0;
         } else if (li == L - 1 && o.guard) {
             o.guard[s] = 0;
@@ -902,6 +906,17 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // (every workgroup's flags were appended before its ticket)
             if (threadIdx.x == 0 && o.flag_out)
                 *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (o.fix_dev) {
+        // the guard's local mode (a solve without an aggregate): the scenarios this
+        // workgroup flagged are re-solved on the exact body by its first wave, state
+        // in the (now dead) LDS, after every store of the fast results has landed
+        __syncthreads();
+        if (fix_n > 0) {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (wv == 0) g3::g3_fixup_local(o.fix_dev, B, pq, (double *)lds, &o, fix_ids, fix_n);
         }
     }
 }

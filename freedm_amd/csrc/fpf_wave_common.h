@@ -127,6 +127,19 @@ __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn,
 }
 }  // namespace
 
+// ---- the convergence guard of the fast kernels (fpf_api.cpp: guard_factor)
+// Append scenario s to the batch's flag list (agent-scope stores: a later
+// kernel reads it) -- or, in the wave kernel's local mode (OutDev::fix_dev, a
+// solve without an aggregate), to its workgroup's own list in LDS.
+__device__ __forceinline__ void guard_flag(const OutDev &o, int s, int *local_n, int *local_ids) {
+    if (o.fix_dev) {
+        local_ids[atomicAdd(local_n, 1)] = s;
+        return;
+    }
+    const unsigned q = __hip_atomic_fetch_add(o.flag_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o.flag_ids + q, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // packed per-slot info (fpf_api.cpp: analyse_wave)
 __device__ __forceinline__ int si_mask(int x) { return x & 7; }
 __device__ __forceinline__ bool si_valid(int x) { return (x >> 3) & 1; }

@@ -554,7 +554,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 near = dmin <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
             }
             if (o.guard) o.guard[s] = near ? 1 : 0;
-            if (near) o.flag_ids[__hip_atomic_fetch_add(o.flag_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = s;
+            if (near) guard_flag(o, s, nullptr, nullptr);
         } else if (o.guard) {
             o.guard[s] = 0;
         }

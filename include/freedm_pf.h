@@ -326,6 +326,13 @@ int         fpf_vvc_gradient(fpf_feeder *feeder, const double *ctrl_dl, int nl, 
                              const double *z, int z_rows, int z_cols, double beta0, int ld,
                              double *g, double *load_nodes, int *n_loads, double *stats);
 
+/* The same gradient at a given DPF result (no device needed): vpolar is the
+ * solve's Vpolar (nn x 6, column-major, substation first); stats[4] (may be
+ * NULL) = gmin, gmax, gabs_min, c0.  Returns FPF_OK or FPF_ERR_*. */
+int         fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+                                const double *vpolar, int nn, double bkva, double bkv, double beta0, int ld,
+                                double *g, double *load_nodes, int *n_loads, double *stats);
+
 /* One whole VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762): the gradient,
  * the step-size search as one batch (fpf_vvc_line_search), and the reversed
  * search when the reference reverses.  loss_fwd / loss_rev [m_max + 1] (loss_rev

@@ -50,7 +50,8 @@ def test_near_eps_iterations_identical(n, layout):
     from freedm_amd import PowerFlow
     from oracle import oracle as O
     f, pq, margins = _near_eps(n)
-    assert margins.max() < 1e-11 and (margins < 1e-13).any(), margins
+    # (the 2048-bus oracle's errmx moves in steps of ~1e-13 relative at the threshold)
+    assert margins.max() < 1e-11 and (margins < (1e-13 if n < 1000 else 1e-12)).any(), margins
     c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
     pf = PowerFlow(f, layout=layout)
     assert pf.kernel == "wave"
@@ -132,13 +133,18 @@ def test_guard_quiet_on_ordinary_batch(n, B):
 
 def test_guard_off_reports_fast_decisions():
     """no_guard = 1 (diagnostics): the fast kernel's own decisions, nothing
-    re-solved -- errmx still agrees with the oracle's to the band's width."""
+    re-solved.  On this batch some of them go the other way (measured: 4 of 8
+    sweep counts differ from the oracle's, one sweep early or late) -- what the
+    guard exists for; errmx agrees with the oracle's wherever the sweep counts do."""
     from freedm_amd import PowerFlow
     from oracle import oracle as O
     f, pq, _ = _near_eps(123, 4)
     r = PowerFlow(f, no_guard=1).solve(pq)
     c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
     assert not r["guard"].any()
-    np.testing.assert_allclose(r["errmx"], c["errmx"], rtol=1e-9)
-    mism = int((r["iters"] != c["iters"]).sum())
-    print(f"near-eps batch without the guard: {mism} of {pq.shape[2]} sweep counts differ from the oracle")
+    same = r["iters"] == c["iters"]
+    np.testing.assert_allclose(r["errmx"][same], c["errmx"][same], rtol=1e-9)
+    # the decisions that went the other way did so by one sweep, either way
+    assert (np.abs(r["iters"][~same] - c["iters"][~same]) == 1).all()
+    print(f"near-eps batch without the guard: {int((~same).sum())} of {pq.shape[2]} sweep counts differ "
+          f"from the oracle")

@@ -119,3 +119,35 @@ def test_vvc_round_against_g7(name, exact):
     np.testing.assert_allclose(r["loss_fwd"][: stop + 1], g["loss_fwd"][: stop + 1], rtol=1e-8 if not exact else 1e-10)
     assert r["ploss_after"] == pytest.approx(sc["ploss_after"], rel=1e-8)
     np.testing.assert_allclose(vvc.s2_setpoints(r["Dl"]), g["S2"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("which", ["demo", "dlnew", "123bus"])
+def test_gradient_at_against_oracle_cpu(which):
+    """fpf_vvc_gradient_at (the host gradient at a given DPF result, no device):
+    the oracle's Vpolar in, the gradient and step size out -- within 1e-10 of
+    ref_vvc.c (which forms inv(J^T) as the reference does; the library solves
+    once), load nodes identical."""
+    import ctypes as C
+    from freedm_amd import _lib
+    from oracle import oracle as O
+    f = {"demo": F.demo_feeder, "dlnew": F.dl_new_feeder, "123bus": lambda: F.synthetic_feeder(123, 123)}[which]()
+    c = O.dpf_solve(f.Dl, f.Z)
+    o = O.vvc_gradient(f.Dl, f.Z, c["Vpolar"])
+    L = _lib.load()
+    dl = np.asfortranarray(f.Dl)
+    Z = np.asarray(f.Z, dtype=np.complex128)
+    zb = np.zeros(2 * Z.size)
+    zb[0::2], zb[1::2] = Z.real.ravel(order="F"), Z.imag.ravel(order="F")
+    vp = np.asfortranarray(c["Vpolar"])
+    ld = dl.shape[0]
+    g, nodes, st = np.zeros((3, ld)), np.zeros((3, ld)), np.zeros(4)
+    n = (C.c_int * 3)()
+    rc = L.fpf_vvc_gradient_at(dl.ctypes.data_as(_lib._dp), dl.shape[0], dl.shape[1], zb.ctypes.data_as(_lib._dp),
+                               Z.shape[0], Z.shape[1], vp.ctypes.data_as(_lib._dp), vp.shape[0], 1000.0, 12.47, 0.1, ld,
+                               g.ctypes.data_as(_lib._dp), nodes.ctypes.data_as(_lib._dp), n, st.ctypes.data_as(_lib._dp))
+    assert rc == 0
+    for x in range(3):
+        np.testing.assert_array_equal(nodes[x, :n[x]], o["load_nodes"][x])
+        np.testing.assert_allclose(g[x, :n[x]], o["g"][x], rtol=1e-10, atol=0)
+    for i, k in enumerate(("gmin", "gmax", "gabs_min", "c0")):
+        assert st[i] == pytest.approx(o[k], rel=1e-10), k
