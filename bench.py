@@ -557,20 +557,59 @@ def main():
             from freedm_amd.feeder import subtree_node_areas
             pq_a = pq_h if layout == 0 else np.ascontiguousarray(pq_h.transpose(1, 2, 0))   # areas: [6][Nl][B]
             ap = AreaPowerFlow(feeder, subtree_node_areas(feeder, [30, 60]), device=local)
-            ra = ap.solve(pq_a, tol=1e-12)
-            ta = []
-            for _ in range(3):
+            ra = ap.solve(pq_a, tol=1e-12, v_out=False)
+            ta, tv = [], []
+            for _ in range(5):   # scalars out, as the monolithic host-buffer solve above
                 t0 = time.perf_counter()
-                ra = ap.solve(pq_a, tol=1e-12)
+                ra = ap.solve(pq_a, tol=1e-12, v_out=False)
                 ta.append(time.perf_counter() - t0)
+            for _ in range(3):   # and with V back (24 MB)
+                t0 = time.perf_counter()
+                ap.solve(pq_a, tol=1e-12)
+                tv.append(time.perf_counter() - t0)
             res["config5_areas"] = {"areas": len(ap.area_nodes), "area_nodes": ap.area_nodes, "scenarios": int(B),
-                                    "ms_per_batch": min(ta) * 1e3, "outer_iterations": int(ra["iters"].max()),
+                                    "ms_per_batch": min(ta) * 1e3, "ms_per_batch_with_v": min(tv) * 1e3,
+                                    "outer_iterations": int(ra["iters"].max()),
                                     "converged": int((ra["status"] == 0).sum()),
                                     "monolithic_host_ms": min(th) * 1e3,
-                                    "note": "fpf_areas_solve, host buffers, boundary exchange to 1e-12 p.u.; "
-                                            "tests/test_areas.py checks V against the monolithic solve to 1e-10"}
+                                    "vs_monolithic": min(ta) / min(th),
+                                    "note": "fpf_areas_solve, host buffers (scalars out, as the monolithic figure; "
+                                            "with_v: V back too), boundary exchange to 1e-12 p.u., device-side stop "
+                                            "test; tests/test_areas.py checks V against the monolithic solve to 1e-10"}
             ap.close()
-            c1["note"] = ("fpf_vvc_round (gradient + 101 step sizes in one batch + reversal), host-synchronous, "
+            # the one-process multi-GPU entry a Broker would use (fpf_multi_*: one host
+            # thread drives every visible GPU, VoltVarCtrl.cpp:1141 runs on the Broker's
+            # single io_service thread): the config-4 hosting study (131 072 scenarios,
+            # host buffers, scalars out) over n = 1 and all visible devices.  Only when
+            # more than one GPU is visible to this process (FPF_BENCH_MULTI=1 forces it
+            # on one GPU to exercise the leg)
+            n_vis = torch.cuda.device_count()
+            if n_vis > 1 or os.environ.get("FPF_BENCH_MULTI") == "1":
+                from freedm_amd import MultiPowerFlow
+                Bm = CONFIGS[4][2]
+                pq_m = np.empty((Bm, 6, feeder.nl))
+                for a in range(0, Bm, 16384):
+                    pq_m[a:a + 16384] = hosting_loads(feeder, np.arange(a, a + 16384),
+                                                      seed=CONFIGS[4][3]).transpose(2, 0, 1)
+                mres = {}
+                for n_dev in sorted({1, n_vis}):
+                    mp = MultiPowerFlow(feeder, n_gpus=n_dev, layout=1)
+                    rm = mp.solve(pq_m, full=False)
+                    tm = []
+                    for _ in range(3):
+                        t0 = time.perf_counter()
+                        rm = mp.solve(pq_m, full=False)
+                        tm.append(time.perf_counter() - t0)
+                    mres[str(n_dev)] = {"ms": min(tm) * 1e3, "scen_per_s": Bm / min(tm),
+                                        "converged": int(rm["aggregate"]["n_conv"])}
+                    mp.close()
+                res["multi_gpu_inproc"] = {
+                    "workload": f"BASELINE config 4 study, {Bm} hosting scenarios, host buffers (843 MB in, scalars "
+                                "out), fpf_multi_solve", "devices": mres,
+                    "speedup_all_vs_1": mres[str(1)]["ms"] / mres[str(n_vis)]["ms"],
+                    "note": "PCIe-bound (host-resident inputs); never the bench value"}
+                del pq_m
+            c1["note"] =("fpf_vvc_round (gradient + 101 step sizes in one batch + reversal), host-synchronous, "
                           "per config-1 feeder")
             res["config1_vvc_round"] = c1
         if world == 1 and args.config == 3 and not args.no_cpu_baseline and not args.nodes:

@@ -37,15 +37,16 @@
 namespace fpf {
 hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, int nl, int B, double *dst,
                              hipStream_t st);
-hipError_t areas_add_row(double *work, int nl, int lrow, int B, const double *add, hipStream_t st);
+hipError_t areas_add_row(double *work, const double *base, int nl, int lrow, int B, const double *add,
+                         const int32_t *ctl, hipStream_t st);
 hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
-                             hipStream_t st);
+                             const int32_t *ctl, hipStream_t st);
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
                                hipStream_t st);
 hipError_t areas_fold_results(int B, const double *loss, const double *vmin, const double *vmax, const int8_t *status,
                               int first, double *o_loss, double *o_vmin, double *o_vmax, int8_t *o_status,
                               hipStream_t st);
-hipError_t areas_max(const double *x, int n, double *out, hipStream_t st);
+hipError_t areas_check(double *diff, int n, double tol, int single, int32_t *ctl, double *last, hipStream_t st);
 }  // namespace fpf
 
 using namespace fpf;
@@ -74,12 +75,23 @@ struct Area {
 struct fpf_areas {
     fpf_ctx *ctx = nullptr;
     int nl = 0, ncols = 0, nn = 0;
+    double lb_v = 0.96, ub_v = 1.05;   // the hosting counters of the aggregate (fpf_opts)
     std::vector<Area> area;      // index = area id, parents before children
     std::vector<int> order;      // solve order
-    int cap = 0;
-    double *d_pq = nullptr, *d_diff = nullptr, *d_max = nullptr;
+    int cap = 0, vcap = 0;
+    hipStream_t stream = nullptr;
+    double *d_pq = nullptr, *d_diff = nullptr;
+    // the whole-feeder results, one block so that one copy brings them back:
+    // [ctl: done, outer, 2 pad (int32)][last move][loss B][vmin B][vmax B][status B (int8)]
+    char *d_res = nullptr, *h_res = nullptr;   // h_res: pinned
+    double *d_vre = nullptr, *d_vim = nullptr;  // [3][Nn][B] in the feeder's numbering (when V is asked for)
     std::string err;
 };
+
+namespace {
+constexpr size_t RES_HEAD = 32;   // ctl (16 bytes) + the last boundary move (8) + pad
+size_t res_bytes(size_t B) { return RES_HEAD + 24 * B + ((B + 7) & ~(size_t)7); }
+}  // namespace
 
 namespace {
 int afail(fpf_areas *a, int code, const std::string &msg) {
@@ -122,7 +134,11 @@ extern "C" void fpf_areas_destroy(fpf_areas *a) {
     }
     (void)hipFree(a->d_pq);
     (void)hipFree(a->d_diff);
-    (void)hipFree(a->d_max);
+    (void)hipFree(a->d_res);
+    (void)hipHostFree(a->h_res);
+    (void)hipFree(a->d_vre);
+    (void)hipFree(a->d_vim);
+    if (a->stream) (void)hipStreamDestroy(a->stream);
     delete a;
 }
 
@@ -278,6 +294,12 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
     fpf_opts o;
     if (opts) o = *opts;
     else fpf_opts_default(&o);
+    a->lb_v = o.lb_v;
+    a->ub_v = o.ub_v;
+    if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
+        fpf_areas_destroy(a);
+        return FPF_ERR_HIP;
+    }
     o.kernel = FPF_KERNEL_WAVE;
     o.exact = 0;
     o.layout = FPF_LAYOUT_SCEN_FASTEST;   // fpf_areas_solve's arrays are [field][row][B] (include/freedm_pf.h)
@@ -310,32 +332,45 @@ extern "C" int fpf_areas_info(const fpf_areas *a, int *n_areas, int *area_nodes,
     return FPF_OK;
 }
 
-static int areas_reserve(fpf_areas *a, int B) {
-    if (B <= a->cap) return FPF_OK;
-    for (Area &A : a->area) free_area_buffers(A);
-    (void)hipFree(a->d_pq);
-    (void)hipFree(a->d_diff);
-    (void)hipFree(a->d_max);
-    a->d_pq = a->d_diff = a->d_max = nullptr;
-    a->cap = 0;
+static int areas_reserve(fpf_areas *a, int B, bool want_v) {
     const size_t b = (size_t)B;
-    AHIP(a, hipMalloc(&a->d_pq, sizeof(double) * 6 * a->nl * b));
-    AHIP(a, hipMalloc(&a->d_diff, sizeof(double) * b));
-    AHIP(a, hipMalloc(&a->d_max, sizeof(double)));
-    for (Area &A : a->area) {
-        AHIP(a, hipMalloc(&A.d_base, sizeof(double) * 6 * A.nl * b));
-        AHIP(a, hipMalloc(&A.d_work, sizeof(double) * 6 * A.nl * b));
-        AHIP(a, hipMalloc(&A.d_vsrc, sizeof(double) * 6 * b));
-        AHIP(a, hipMalloc(&A.d_sin, sizeof(double) * 6 * b));
-        AHIP(a, hipMalloc(&A.d_vre, sizeof(double) * 3 * A.nn * b));
-        AHIP(a, hipMalloc(&A.d_vim, sizeof(double) * 3 * A.nn * b));
-        AHIP(a, hipMalloc(&A.d_loss, sizeof(double) * b));
-        AHIP(a, hipMalloc(&A.d_vmin, sizeof(double) * b));
-        AHIP(a, hipMalloc(&A.d_vmax, sizeof(double) * b));
-        AHIP(a, hipMalloc(&A.d_iters, sizeof(int32_t) * b));
-        AHIP(a, hipMalloc(&A.d_status, sizeof(int8_t) * b));
+    if (B > a->cap) {
+        for (Area &A : a->area) free_area_buffers(A);
+        (void)hipFree(a->d_pq);
+        (void)hipFree(a->d_diff);
+        (void)hipFree(a->d_res);
+        (void)hipHostFree(a->h_res);
+        a->d_pq = a->d_diff = nullptr;
+        a->d_res = a->h_res = nullptr;
+        a->cap = 0;
+        AHIP(a, hipMalloc(&a->d_pq, sizeof(double) * 6 * a->nl * b));
+        AHIP(a, hipMalloc(&a->d_diff, sizeof(double) * b));
+        AHIP(a, hipMalloc(&a->d_res, res_bytes(b)));
+        AHIP(a, hipHostMalloc((void **)&a->h_res, res_bytes(b), hipHostMallocDefault));
+        for (Area &A : a->area) {
+            AHIP(a, hipMalloc(&A.d_base, sizeof(double) * 6 * A.nl * b));
+            AHIP(a, hipMalloc(&A.d_work, sizeof(double) * 6 * A.nl * b));
+            AHIP(a, hipMalloc(&A.d_vsrc, sizeof(double) * 6 * b));
+            AHIP(a, hipMalloc(&A.d_sin, sizeof(double) * 6 * b));
+            AHIP(a, hipMalloc(&A.d_vre, sizeof(double) * 3 * A.nn * b));
+            AHIP(a, hipMalloc(&A.d_vim, sizeof(double) * 3 * A.nn * b));
+            AHIP(a, hipMalloc(&A.d_loss, sizeof(double) * b));
+            AHIP(a, hipMalloc(&A.d_vmin, sizeof(double) * b));
+            AHIP(a, hipMalloc(&A.d_vmax, sizeof(double) * b));
+            AHIP(a, hipMalloc(&A.d_iters, sizeof(int32_t) * b));
+            AHIP(a, hipMalloc(&A.d_status, sizeof(int8_t) * b));
+        }
+        a->cap = B;
     }
-    a->cap = B;
+    if (want_v && B > a->vcap) {
+        (void)hipFree(a->d_vre);
+        (void)hipFree(a->d_vim);
+        a->d_vre = a->d_vim = nullptr;
+        a->vcap = 0;
+        AHIP(a, hipMalloc(&a->d_vre, sizeof(double) * 3 * a->nn * b));
+        AHIP(a, hipMalloc(&a->d_vim, sizeof(double) * 3 * a->nn * b));
+        a->vcap = B;
+    }
     return FPF_OK;
 }
 
@@ -343,6 +378,14 @@ static int areas_reserve(fpf_areas *a, int B) {
 // in the feeder's node numbering, iters = outer iterations, status (worst
 // area; FPF_NONCONVERGED also when the outer loop did not reach tol), loss
 // (sum over areas), vmin / vmax (over areas).  vpolar / pqb / pql must be NULL.
+//
+// Schedule: every launch on the object's stream, no host round trip inside the
+// outer loop.  The convergence test is a device flag (check_kernel: ctl[0]);
+// every kernel of an iteration enqueued after it is set does nothing.  The host
+// enqueues iterations in chunks and looks at the flag of chunk c (an 8-byte
+// copy into pinned memory) only after chunk c + 1 is enqueued, so the GPU never
+// waits for the host; at most two chunks of no-op launches follow convergence.
+// The scalar results and the flag come back in one copy.
 extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, double tol, int max_outer,
                                const fpf_outputs *out, fpf_aggregate *agg) {
     if (!a || n_scen < 0 || (n_scen > 0 && !pq) || !(tol > 0) || max_outer < 1)
@@ -358,28 +401,37 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     }
     const int B = n_scen;
     const size_t b = (size_t)B;
+    const bool want_v = u.v_re || u.v_im;
     AHIP(a, hipSetDevice(ctx_device(a->ctx)));
-    int rc = areas_reserve(a, B);
+    int rc = areas_reserve(a, B, want_v);
     if (rc) return rc;
-    hipStream_t st = nullptr;
-    AHIP(a, hipMemcpy(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice));
+    hipStream_t st = a->stream;
+    int32_t *ctl = (int32_t *)a->d_res;
+    double *last = (double *)(a->d_res + 16);
+    double *r_loss = (double *)(a->d_res + RES_HEAD), *r_vmin = r_loss + b, *r_vmax = r_vmin + b;
+    int8_t *r_status = (int8_t *)(r_vmax + b);
+    AHIP(a, hipMemcpyAsync(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice, st));
+    AHIP(a, hipMemsetAsync(a->d_res, 0, RES_HEAD, st));
+    AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b, st));
     for (Area &A : a->area) {
         AHIP(a, areas_gather_rows(a->d_pq, a->nl, A.d_rows, A.nl, B, A.d_base, st));
+        // the working loads: the area's own (the rows a child hangs off are
+        // rewritten every iteration)
+        AHIP(a, hipMemcpyAsync(A.d_work, A.d_base, sizeof(double) * 6 * A.nl * b, hipMemcpyDeviceToDevice, st));
         AHIP(a, hipMemsetAsync(A.d_sin, 0, sizeof(double) * 6 * b, st));
         AHIP(a, hipMemsetAsync(A.d_vsrc, 0, sizeof(double) * 6 * b, st));
     }
-    int outer = 0;
-    bool conv = false;
-    double last = INFINITY;
-    for (outer = 1; outer <= max_outer && !conv; ++outer) {
-        AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b, st));
+    const int single = a->area.size() == 1 ? 1 : 0;
+    auto enqueue_iteration = [&]() -> int {
         for (int ar : a->order) {
             Area &A = a->area[ar];
-            AHIP(a, hipMemcpyAsync(A.d_work, A.d_base, sizeof(double) * 6 * A.nl * b, hipMemcpyDeviceToDevice, st));
-            for (const auto &k : A.kids) AHIP(a, areas_add_row(A.d_work, A.nl, k.first, B, a->area[k.second].d_sin, st));
+            // the boundary rows = their own load + the child's source power of the
+            // previous iteration (every other row of d_work is the base, copied once)
+            for (const auto &k : A.kids)
+                AHIP(a, areas_add_row(A.d_work, A.d_base, A.nl, k.first, B, a->area[k.second].d_sin, ctl, st));
             if (A.parent >= 0) {
                 const Area &P = a->area[A.parent];
-                AHIP(a, areas_gather_vsrc(P.d_vre, P.d_vim, P.nn, A.lb, B, A.d_vsrc, a->d_diff, st));
+                AHIP(a, areas_gather_vsrc(P.d_vre, P.d_vim, P.nn, A.lb, B, A.d_vsrc, a->d_diff, ctl, st));
             }
             fpf_outputs o;
             std::memset(&o, 0, sizeof(o));
@@ -390,76 +442,90 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
             o.loss = A.d_loss;
             o.vmin = A.d_vmin;
             o.vmax = A.d_vmax;
-            rc = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)st, A.parent >= 0 ? A.d_vsrc : nullptr,
-                                       A.d_sin, FPF_LAYOUT_SCEN_FASTEST);
-            if (rc < 0) return afail(a, rc, std::string("area solve: ") + fpf_last_error(a->ctx));
+            const int r = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)st,
+                                                A.parent >= 0 ? A.d_vsrc : nullptr, A.d_sin, FPF_LAYOUT_SCEN_FASTEST,
+                                                nullptr, ctl);
+            if (r < 0) return afail(a, r, std::string("area solve: ") + fpf_last_error(a->ctx));
         }
-        // the boundary voltages' largest move this iteration (the first always moves)
-        double mx = 0.0;
-        AHIP(a, areas_max(a->d_diff, B, a->d_max, st));
-        AHIP(a, hipMemcpy(&mx, a->d_max, sizeof(double), hipMemcpyDeviceToHost));
-        last = mx;
-        conv = outer > 1 && mx <= tol;
-        if (a->area.size() == 1) conv = true;
+        AHIP(a, areas_check(a->d_diff, B, tol, single, ctl, last, st));
+        return FPF_OK;
+    };
+    // chunks of K iterations; the flag of chunk c is read after chunk c + 1 is enqueued
+    const int K = 2;
+    int32_t *h_ctl[2] = {(int32_t *)a->h_res, (int32_t *)a->h_res + 2};   // two 8-byte slots in the pinned head
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    AHIP(a, hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    AHIP(a, hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    int enq = 0, chunk = 0;
+    bool stop = false;
+    while (!stop && enq < max_outer) {
+        for (int i = 0; i < K && enq < max_outer; ++i, ++enq) {
+            rc = enqueue_iteration();
+            if (rc) break;
+        }
+        if (rc) break;
+        AHIP(a, hipMemcpyAsync(h_ctl[chunk & 1], ctl, 8, hipMemcpyDeviceToHost, st));
+        AHIP(a, hipEventRecord(ev[chunk & 1], st));
+        if (chunk > 0) {
+            AHIP(a, hipEventSynchronize(ev[(chunk - 1) & 1]));
+            stop = h_ctl[(chunk - 1) & 1][0] != 0;
+        }
+        ++chunk;
     }
-    --outer;
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
     // results in the feeder's numbering; whole-feeder loss / extremes / status
-    double *d_vre = nullptr, *d_vim = nullptr, *d_loss = nullptr, *d_vmin = nullptr, *d_vmax = nullptr;
-    int8_t *d_status = nullptr;
-    AHIP(a, hipMalloc(&d_loss, sizeof(double) * b));
-    AHIP(a, hipMalloc(&d_vmin, sizeof(double) * b));
-    AHIP(a, hipMalloc(&d_vmax, sizeof(double) * b));
-    AHIP(a, hipMalloc(&d_status, b));
-    if (u.v_re || u.v_im) {
-        AHIP(a, hipMalloc(&d_vre, sizeof(double) * 3 * a->nn * b));
-        AHIP(a, hipMalloc(&d_vim, sizeof(double) * 3 * a->nn * b));
-    }
     bool first = true;
     for (int ar : a->order) {
         Area &A = a->area[ar];
-        AHIP(a, areas_fold_results(B, A.d_loss, A.d_vmin, A.d_vmax, A.d_status, first ? 1 : 0, d_loss, d_vmin, d_vmax,
-                                   d_status, st));
+        AHIP(a, areas_fold_results(B, A.d_loss, A.d_vmin, A.d_vmax, A.d_status, first ? 1 : 0, r_loss, r_vmin, r_vmax,
+                                   r_status, st));
         first = false;
-        if (d_vre) {
+        if (want_v) {
             // the root area's local node 0 is the substation (monolithic node 0)
             const int k0 = A.parent < 0 ? 0 : 1;
-            AHIP(a, areas_scatter_nodes(A.d_vre, A.nn, k0, A.d_mono, a->nn, B, d_vre, st));
-            AHIP(a, areas_scatter_nodes(A.d_vim, A.nn, k0, A.d_mono, a->nn, B, d_vim, st));
+            AHIP(a, areas_scatter_nodes(A.d_vre, A.nn, k0, A.d_mono, a->nn, B, a->d_vre, st));
+            AHIP(a, areas_scatter_nodes(A.d_vim, A.nn, k0, A.d_mono, a->nn, B, a->d_vim, st));
         }
     }
-    std::vector<int8_t> h_status(b);
-    AHIP(a, hipMemcpy(h_status.data(), d_status, b, hipMemcpyDeviceToHost));
-    if (!conv)
-        for (auto &x : h_status) x = FPF_NONCONVERGED;
-    std::vector<double> h_loss(b), h_vmin(b), h_vmax(b);
-    AHIP(a, hipMemcpy(h_loss.data(), d_loss, sizeof(double) * b, hipMemcpyDeviceToHost));
-    AHIP(a, hipMemcpy(h_vmin.data(), d_vmin, sizeof(double) * b, hipMemcpyDeviceToHost));
-    AHIP(a, hipMemcpy(h_vmax.data(), d_vmax, sizeof(double) * b, hipMemcpyDeviceToHost));
-    if (u.v_re) AHIP(a, hipMemcpy(u.v_re, d_vre, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost));
-    if (u.v_im) AHIP(a, hipMemcpy(u.v_im, d_vim, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost));
-    (void)hipFree(d_vre);
-    (void)hipFree(d_vim);
-    (void)hipFree(d_loss);
-    (void)hipFree(d_vmin);
-    (void)hipFree(d_vmax);
-    (void)hipFree(d_status);
+    AHIP(a, hipMemcpyAsync(a->h_res, a->d_res, res_bytes(b), hipMemcpyDeviceToHost, st));
+    if (u.v_re) AHIP(a, hipMemcpyAsync(u.v_re, a->d_vre, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost, st));
+    if (u.v_im) AHIP(a, hipMemcpyAsync(u.v_im, a->d_vim, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost, st));
+    AHIP(a, hipStreamSynchronize(st));
+    const int32_t *h_c = (const int32_t *)a->h_res;
+    const bool conv = h_c[0] != 0;
+    const int outer = h_c[1];
+    double h_last;
+    std::memcpy(&h_last, a->h_res + 16, 8);
+    const double *h_loss = (const double *)(a->h_res + RES_HEAD), *h_vmin = h_loss + b, *h_vmax = h_vmin + b;
+    const int8_t *h_status = (const int8_t *)(h_vmax + b);
+    auto status_of = [&](int s) -> int8_t { return conv ? h_status[s] : (int8_t)FPF_NONCONVERGED; };
     if (u.iters)
         for (int s = 0; s < B; ++s) u.iters[s] = outer;
-    if (u.status) std::memcpy(u.status, h_status.data(), b);
-    if (u.loss) std::memcpy(u.loss, h_loss.data(), sizeof(double) * b);
-    if (u.vmin) std::memcpy(u.vmin, h_vmin.data(), sizeof(double) * b);
-    if (u.vmax) std::memcpy(u.vmax, h_vmax.data(), sizeof(double) * b);
+    if (u.status)
+        for (int s = 0; s < B; ++s) u.status[s] = status_of(s);
+    if (u.loss) std::memcpy(u.loss, h_loss, sizeof(double) * b);
+    if (u.vmin) std::memcpy(u.vmin, h_vmin, sizeof(double) * b);
+    if (u.vmax) std::memcpy(u.vmax, h_vmax, sizeof(double) * b);
+    // the aggregate as every fpf_aggregate producer forms it (converged scenarios;
+    // n_over / n_under by the hosting bounds)
     int n_nonconv = 0;
     fpf_aggregate g;
     std::memset(&g, 0, sizeof(g));
     g.vmin = INFINITY;
     g.vmax = -INFINITY;
     for (int s = 0; s < B; ++s) {
-        if (h_status[s] == FPF_CONVERGED) {
+        if (status_of(s) == FPF_CONVERGED) {
             g.loss_sum += h_loss[s];
             g.vmin = std::min(g.vmin, h_vmin[s]);
             g.vmax = std::max(g.vmax, h_vmax[s]);
             g.n_conv += 1;
+            if (h_vmax[s] > a->ub_v) g.n_over += 1;
+            if (h_vmin[s] < a->lb_v) g.n_under += 1;
         } else {
             g.n_nonconv += 1;
             ++n_nonconv;
@@ -467,6 +533,6 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     }
     g.n_scen = B;
     if (agg) *agg = g;
-    a->err = "outer iterations " + std::to_string(outer) + ", last boundary move " + std::to_string(last);
+    a->err = "outer iterations " + std::to_string(outer) + ", last boundary move " + std::to_string(h_last);
     return n_nonconv;
 }

@@ -20,19 +20,25 @@ __global__ void gather_rows_kernel(const double *__restrict__ src, int nl_src, c
     dst[(size_t)fr * B + s] = m < 0 ? 0.0 : src[((size_t)f * nl_src + m) * B + s];
 }
 
-// work[f][lrow][s] += add[f][s]  for the 6 load fields (P1 Q1 P2 Q2 P3 Q3)
-__global__ void add_row_kernel(double *__restrict__ work, int nl, int lrow, int B, const double *__restrict__ add) {
+// The kernels of one outer iteration do nothing once the loop has converged
+// (ctl[0] != 0: iterations enqueued before the host looked are no-ops).
+
+// work[f][lrow][s] = base[f][lrow][s] + add[f][s]  for the 6 load fields (P1 Q1 P2 Q2 P3 Q3)
+__global__ void add_row_kernel(double *__restrict__ work, const double *__restrict__ base, int nl, int lrow, int B,
+                               const double *__restrict__ add, const int32_t *__restrict__ ctl) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     const int f = blockIdx.y;
-    if (s >= B) return;
-    work[((size_t)f * nl + lrow) * B + s] += add[(size_t)f * B + s];
+    if (s >= B || ctl[0]) return;
+    const size_t i = ((size_t)f * nl + lrow) * B + s;
+    work[i] = base[i] + add[(size_t)f * B + s];
 }
 
 // vsrc[2p][s], vsrc[2p+1][s] = V(p, node lb) of the parent area; diff[s] = max(diff[s], |change|)
 __global__ void gather_vsrc_kernel(const double *__restrict__ v_re, const double *__restrict__ v_im, int nn, int lb,
-                                   int B, double *__restrict__ vsrc, double *__restrict__ diff) {
+                                   int B, double *__restrict__ vsrc, double *__restrict__ diff,
+                                   const int32_t *__restrict__ ctl) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B) return;
+    if (s >= B || ctl[0]) return;
     double d = diff[s];
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
@@ -74,17 +80,30 @@ __global__ void fold_results_kernel(int B, const double *__restrict__ loss, cons
     }
 }
 
-__global__ void max_kernel(const double *__restrict__ x, int n, double *__restrict__ out) {
+// the end of one outer iteration: the boundary voltages' largest move (the
+// first iteration always moves; a single area needs one), then the device-side
+// stop -- ctl[0] done, ctl[1] outer iterations run; last = the move
+__global__ void check_kernel(double *__restrict__ x, int n, double tol, int single, int32_t *__restrict__ ctl,
+                             double *__restrict__ last) {
+    if (ctl[0]) return;   // (uniform)
     __shared__ double sh[256];
     double m = 0.0;
-    for (int i = threadIdx.x; i < n; i += 256) m = fmax(m, x[i]);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        m = fmax(m, x[i]);
+        x[i] = 0.0;   // (the next iteration's diff starts from 0)
+    }
     sh[threadIdx.x] = m;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + w]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = sh[0];
+    if (threadIdx.x == 0) {
+        const int outer = ctl[1] + 1;
+        ctl[1] = outer;
+        *last = sh[0];
+        if (single || (outer > 1 && sh[0] <= tol)) ctl[0] = 1;
+    }
 }
 
 inline dim3 grid(int B, int y) { return dim3((unsigned)((B + 255) / 256), (unsigned)y); }
@@ -95,13 +114,14 @@ hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, 
     hipLaunchKernelGGL(gather_rows_kernel, grid(B, 6 * nl), dim3(256), 0, st, src, nl_src, row, nl, B, dst);
     return hipGetLastError();
 }
-hipError_t areas_add_row(double *work, int nl, int lrow, int B, const double *add, hipStream_t st) {
-    hipLaunchKernelGGL(add_row_kernel, grid(B, 6), dim3(256), 0, st, work, nl, lrow, B, add);
+hipError_t areas_add_row(double *work, const double *base, int nl, int lrow, int B, const double *add,
+                         const int32_t *ctl, hipStream_t st) {
+    hipLaunchKernelGGL(add_row_kernel, grid(B, 6), dim3(256), 0, st, work, base, nl, lrow, B, add, ctl);
     return hipGetLastError();
 }
 hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(gather_vsrc_kernel, grid(B, 1), dim3(256), 0, st, v_re, v_im, nn, lb, B, vsrc, diff);
+                             const int32_t *ctl, hipStream_t st) {
+    hipLaunchKernelGGL(gather_vsrc_kernel, grid(B, 1), dim3(256), 0, st, v_re, v_im, nn, lb, B, vsrc, diff, ctl);
     return hipGetLastError();
 }
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
@@ -117,8 +137,8 @@ hipError_t areas_fold_results(int B, const double *loss, const double *vmin, con
                        o_vmin, o_vmax, o_status);
     return hipGetLastError();
 }
-hipError_t areas_max(const double *x, int n, double *out, hipStream_t st) {
-    hipLaunchKernelGGL(max_kernel, dim3(1), dim3(256), 0, st, x, n, out);
+hipError_t areas_check(double *diff, int n, double tol, int single, int32_t *ctl, double *last, hipStream_t st) {
+    hipLaunchKernelGGL(check_kernel, dim3(1), dim3(256), 0, st, diff, n, tol, single, ctl, last);
     return hipGetLastError();
 }
 

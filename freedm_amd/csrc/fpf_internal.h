@@ -199,6 +199,10 @@ struct OutDev {
     // the workgroup's LDS; fix_dev = NULL: the flags go to the batch's list and a
     // dpf_fixup_kernel launch re-solves them
     const struct FeederDev *fix_dev;
+    // the multi-area solve's device-side stop (fpf_areas.cpp): *skip != 0 -> the
+    // launch does nothing (the outer loop has converged; later iterations were
+    // enqueued before the host looked).  NULL: always solve.  Wave kernels only.
+    const int32_t *skip;
 };
 
 // The exact re-solve of flagged scenarios (fpf_generic.hip: dpf_fixup_kernel):
@@ -216,7 +220,7 @@ int ctx_device(const fpf_ctx *ctx);   // the HIP device of a context
 // (OutDev::vsrc, OutDev::s_in; both device memory, may be NULL)
 int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                           void *stream, const double *d_vsrc, double *d_s_in, int layout,
-                          unsigned *d_flag_out = nullptr);
+                          unsigned *d_flag_out = nullptr, const int32_t *d_skip = nullptr);
 // the exact re-solve of the scenarios a deferred (d_flag_out) guarded solve flagged
 int fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                        void *stream, int layout);

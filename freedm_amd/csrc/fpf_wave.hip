@@ -108,6 +108,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     constexpr int NT = WPB * 64;
     extern __shared__ double2 lds[];
     if (DBG(4096)) return;
+    if (o.skip && *o.skip) return;   // (the multi-area solve's device-side stop)
     if ((int)blockIdx.x >= f.stag_lo && (int)blockIdx.x < f.stag_hi)
         for (int i = 0; i < f.stag_n; ++i) __builtin_amdgcn_s_sleep(127);
     WSTAMP(0);
@@ -482,7 +483,6 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     const cx d = DBG(65536) ? mk(f.eps * (a + 1), f.V0[0] * 1e-3) : ldx(tl, (a * C + c) * L + li);
                     const cx b = ib[c][a];
                     g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
-                    if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
                 }
             }
 #else
@@ -504,7 +504,6 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     const cx d = tq[a];
                     const cx b = ib[c][a];
                     g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
-                    if (any_fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
                 }
                 if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
 #pragma unroll
@@ -529,11 +528,19 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     else { const double2 t = ld_global2(f.slot_temp, ti); tm[l * 3 + a] = mk(t.x, t.y); }
                 }
                 g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
-                if (any_fin) lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
             }
 #ifdef FPF_WAVE_SB
             __builtin_amdgcn_sched_barrier(0);
 #endif
+        }
+        // (a wave-uniform branch of its own: inside the slot loops the compiler turned
+        // the accumulation into selects executed every sweep)
+        if (any_fin) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
         }
         WSTAMP(8 + 8 * it);
 #pragma unroll
@@ -912,11 +919,16 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         // the guard's local mode (a solve without an aggregate): the scenarios this
         // workgroup flagged are re-solved on the exact body by its first wave, state
         // in the (now dead) LDS, after every store of the fast results has landed
+        // (the exact body gets an LDS copy of the output pointers: taking the kernel
+        // argument's address would put the whole OutDev in scratch memory and turn
+        // every o.* read of the sweep loop into a scratch load)
+        __shared__ OutDev osh;
         __syncthreads();
         if (fix_n > 0) {
             __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == 0) osh = o;
             __syncthreads();
-            if (wv == 0) g3::g3_fixup_local(o.fix_dev, B, pq, (double *)lds, &o, fix_ids, fix_n);
+            if (wv == 0) g3::g3_fixup_local(o.fix_dev, B, pq, (double *)lds, &osh, fix_ids, fix_n);
         }
     }
 }

@@ -100,6 +100,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                                                              OutDev o) {
     constexpr int L = 64 * W, NT = 64 * W;
     extern __shared__ double2 lds[];
+    if (o.skip && *o.skip) return;   // (the multi-area solve's device-side stop)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int s = xcd_tile(blockIdx.x, gridDim.x);   // this workgroup's scenario
     const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
@@ -322,7 +323,6 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     const cx b = ib[c][a];
                     g[c][a] = mk(lg[c] * fma(d.re, b.re, fma(-d.im, b.im, ms.re)),
                                  lg[c] * fma(d.re, b.im, fma(d.im, b.re, ms.im)));
-                    if (fin) lp[a] = fma(g[c][a].re, b.re, fma(g[c][a].im, b.im, lp[a]));
                 }
             }
         } else {
@@ -335,9 +335,18 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 for (int a = 0; a < 3; ++a) {
                     const cx t = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
                     g[c][a] = mk(lg[c] * t.re, lg[c] * t.im);
-                    if (fin) lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
                 }
             }
+        }
+
+        // (a uniform branch of its own: inside the slot loops the compiler turned the
+        // accumulation into selects executed every sweep)
+        if (fin) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
         }
 
         // ---- forward sweep (:163-195): V = V0 - A, A = Ginc + off(block)

@@ -425,16 +425,20 @@ class AreaPowerFlow:
         except Exception:
             pass
 
-    def solve(self, pq: np.ndarray, tol: float = 1e-12, max_outer: int = 100) -> dict:
+    def solve(self, pq: np.ndarray, tol: float = 1e-12, max_outer: int = 100, v_out: bool = True) -> dict:
+        """v_out=False: per-scenario scalars only (no V copied back)."""
         L = _lib.load()
         pq = np.ascontiguousarray(pq, dtype=np.float64)
         if pq.ndim != 3 or pq.shape[:2] != (6, self.nl):
             raise ValueError(f"pq must be [6][{self.nl}][B]")
         B, nn = pq.shape[2], self.nn
         r = {"iters": np.zeros(B, np.int32), "status": np.zeros(B, np.int8), "loss": np.zeros(B),
-             "vmin": np.zeros(B), "vmax": np.zeros(B), "V_re": np.zeros((3, nn, B)), "V_im": np.zeros((3, nn, B))}
-        out = _lib.FpfOutputs(None, None, None, _ptr(r["V_re"]), _ptr(r["V_im"]), _ptr(r["iters"]), _ptr(r["status"]),
-                              _ptr(r["loss"]), _ptr(r["vmin"]), _ptr(r["vmax"]))
+             "vmin": np.zeros(B), "vmax": np.zeros(B)}
+        if v_out:
+            r["V_re"] = np.zeros((3, nn, B))
+            r["V_im"] = np.zeros((3, nn, B))
+        out = _lib.FpfOutputs(None, None, None, _ptr(r["V_re"]) if v_out else None, _ptr(r["V_im"]) if v_out else None,
+                              _ptr(r["iters"]), _ptr(r["status"]), _ptr(r["loss"]), _ptr(r["vmin"]), _ptr(r["vmax"]))
         agg = _lib.FpfAggregate()
         rc = L.fpf_areas_solve(self.h, B, pq.ctypes.data_as(_lib._dp), float(tol), int(max_outer), C.byref(out),
                                C.byref(agg))

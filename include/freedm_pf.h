@@ -190,8 +190,13 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
  * Launches that produce an aggregate (d_agg != NULL here, fpf_aggregate_device,
  * fpf_solve_batch) share the feeder's partials and arrival ticket; the library
  * serialises them across streams with an event per feeder (each waits for the
- * previous one), so they may be enqueued on different streams. Solves without
- * an aggregate on one feeder run concurrently.
+ * previous one), so they may be enqueued on different streams.  Other solves on
+ * one feeder may overlap across streams only when they run the wave kernels
+ * (fast mode, feeders of at most 2048 branches), every per-scenario output they
+ * use is the caller's (NULL outputs fall back to buffers of the feeder) and they
+ * produce no aggregate; the generic and tiled kernels' scratch and layout
+ * buffers and the guard's flag list belong to the feeder, so any other mix must
+ * share one stream (or be serialised by the caller).
  * Returns FPF_OK or an error (the non-converged count is in d_agg / status). */
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);

@@ -8,8 +8,9 @@
 // fpf_broker.h (no Armadillo), which tests/test_integration.py compiles as C++98
 // and runs on the GPU; this file only moves arma::mat memory in and out and
 // needs the Broker's Armadillo to build (not present in this repository's image).
-#include "fun_return.h"
+#include "fun_return_hip.h"   // fun_return.h + the DPF_batch declaration
 
+#include <iostream>
 #include <vector>
 
 #include "fpf_broker.h"
@@ -17,6 +18,11 @@
 namespace {
 fpf_broker::Engine &engine() {
     static fpf_broker::Engine e(0, 1);   // device 0, exact mode: the reference's roundings
+    static bool init = false;
+    if (!init) {
+        e.set_log(&std::cout);           // DPF_return7.cpp:38,206 print on every call
+        init = true;
+    }
     return e;
 }
 

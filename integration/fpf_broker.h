@@ -27,6 +27,7 @@
 #include <freedm_pf.h>
 
 #include <cstring>
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -47,7 +48,8 @@ class Engine {
 public:
     /* exact = 1: the reference's roundings (bit-identical V / PQb / PQL);
        0: fast mode (1e-10 on V, same iteration counts) */
-    explicit Engine(int device = 0, int exact = 1) : ctx_(0), feeder_(0), nl_(0), ncols_(0), z_rows_(0), z_cols_(0) {
+    explicit Engine(int device = 0, int exact = 1)
+        : ctx_(0), feeder_(0), nl_(0), ncols_(0), z_rows_(0), z_cols_(0), log_(0) {
         if (fpf_ctx_create(device, &ctx_) != FPF_OK) throw std::runtime_error("libfreedm_pf: no HIP device");
         fpf_opts_default(&opts_);
         opts_.exact = exact;
@@ -82,6 +84,12 @@ public:
     }
 
     const fpf_feeder_info &info() const { return info_; }
+
+    /* The reference's console lines (DPF_return7.cpp:38 "Run DPF on <Nn> Nodes
+       System" and :206 " DPF converged!") per solved scenario, in the order K
+       sequential calls would print them (0: silent, the default here;
+       Broker/src/vvc/DPF_hip.cpp sets std::cout, as the reference prints). */
+    void set_log(std::ostream *os) { log_ = os; }
     const char *last_error() const { return fpf_last_error(ctx_); }
 
     /* DPF_return7(Dl, Z): one scenario; throws std::logic_error where the
@@ -128,8 +136,12 @@ public:
         const int rc = fpf_solve_batch(f, K, &pq[0], &o, 0);
         if (rc < 0) throw std::runtime_error(std::string("libfreedm_pf: ") + fpf_last_error(ctx_));
         for (int s = 0; s < K; ++s) {
+            if (log_) *log_ << "Run DPF on " << nn << " Nodes System" << std::endl;
+            /* (a non-converged solve prints nothing more: the reference's :210 test
+               i >= mxitr is never true inside its loop, and :242 throws) */
             if (throw_nonconv && status[s] != FPF_CONVERGED)
                 throw std::logic_error("DPF_return7: no convergence");   /* DPF_return7.cpp:100-101,242 */
+            if (log_ && status[s] == FPF_CONVERGED) *log_ << " DPF converged!" << std::endl;
             Vpq &r = out[s];
             r.nn = nn;
             r.vpolar.resize((size_t)6 * nn);
@@ -161,6 +173,7 @@ private:
     fpf_feeder_info info_;
     std::vector<double> topo_, z_;
     int nl_, ncols_, z_rows_, z_cols_;
+    std::ostream *log_;
 };
 
 }  // namespace fpf_broker

@@ -2,7 +2,7 @@
 // DPF_hip.cpp does, from plain files, so tests/test_integration.py can compile
 // it as C++98 and check it on the GPU against the oracle.
 //
-//   glue_check in.bin out.bin
+//   glue_check in.bin out.bin [log.txt]
 // in.bin : int32 nl, ncols, z_rows, z_cols, K, exact; Dl (nl x ncols col-major f64);
 //          Z (z_rows x z_cols complex, interleaved re/im, col-major); then K load
 //          sets, each the 6 Dl columns 6..11 (nl x 6 col-major f64)
@@ -10,8 +10,10 @@
 //          f64 loss, vmin, vmax, vpolar[nn*6], pqb[nn*6], pql[nn*6] (col-major);
 //          then int32 single_ok (DPF_return7 of scenario 0 equals batch[0]) and
 //          int32 threw (DPF_return7 threw std::logic_error on a non-converged scenario, -1: none)
+// log.txt: the reference's console lines of the K single DPF_return7 calls
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <stdexcept>
 #include <vector>
 
@@ -20,7 +22,7 @@
 static bool rd(FILE *f, void *p, size_t n) { return std::fread(p, 1, n, f) == n; }
 
 int main(int argc, char **argv) {
-    if (argc != 3) return 2;
+    if (argc != 3 && argc != 4) return 2;
     FILE *in = std::fopen(argv[1], "rb");
     if (!in) return 2;
     int hdr[6];
@@ -40,6 +42,11 @@ int main(int argc, char **argv) {
     fpf_broker::Engine eng(0, exact);
     std::vector<fpf_broker::Vpq> r = eng.dpf_batch(ptrs, nl, ncols, &z[0], zr, zc, false);
     int single_ok = 0, threw = -1;
+    std::ofstream log;
+    if (argc == 4) {
+        log.open(argv[3]);
+        eng.set_log(&log);
+    }
     for (int s = 0; s < K; ++s) {
         try {
             fpf_broker::Vpq one = eng.dpf_return7(ptrs[s], nl, ncols, &z[0], zr, zc);

@@ -60,3 +60,34 @@ def test_areas_equal_monolithic(case):
     ag = r["aggregate"]
     assert ag["n_conv"] == pq.shape[2] and ag["loss_sum"] == pytest.approx(r["loss"].sum(), rel=1e-12)
     ap.close()
+
+
+@pytest.mark.gpu
+def test_areas_schedule_and_aggregate():
+    """The device-side stop (fpf_areas.cpp): scalars without V equal those with V
+    bit for bit, the outer-iteration count does not depend on how many no-op
+    iterations were enqueued after convergence (max_outer 100 vs the exact count),
+    a max_outer below it reports every scenario non-converged after exactly
+    max_outer iterations, and the aggregate counts the hosting bounds like every
+    other producer."""
+    from freedm_amd import AreaPowerFlow
+    f = F.synthetic_feeder(123, 123)
+    pq = F.scenario_loads(f, np.arange(256))
+    ap = AreaPowerFlow(f, F.subtree_node_areas(f, [30, 60]))
+    r = ap.solve(pq, tol=1e-12, max_outer=100)
+    n = int(r["iters"][0])
+    assert (r["status"] == 0).all() and n >= 3
+    s = ap.solve(pq, tol=1e-12, max_outer=100, v_out=False)
+    assert "V_re" not in s
+    for k in ("iters", "status", "loss", "vmin", "vmax"):
+        np.testing.assert_array_equal(s[k], r[k])
+    e = ap.solve(pq, tol=1e-12, max_outer=n)   # no chunk beyond the last needed iteration
+    for k in ("iters", "status", "loss", "vmin", "vmax", "V_re", "V_im"):
+        np.testing.assert_array_equal(e[k], r[k])
+    short = ap.solve(pq, tol=1e-12, max_outer=n - 1)
+    assert (short["iters"] == n - 1).all() and (short["status"] != 0).all()
+    assert short["aggregate"]["n_nonconv"] == pq.shape[2]
+    ag = r["aggregate"]
+    assert ag["n_under"] == int((r["vmin"] < 0.96).sum()) and ag["n_over"] == int((r["vmax"] > 1.05).sum())
+    assert ag["n_under"] + ag["n_over"] > 0 or (r["vmin"] >= 0.96).all()
+    ap.close()

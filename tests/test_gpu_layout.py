@@ -75,3 +75,33 @@ def test_multi_scenario_major(n):
     s = PowerFlow(f, layout=1).solve(pq)
     for k in ("iters", "status", "loss", "vmin", "vmax", "V_re", "V_im", "PQb"):
         np.testing.assert_array_equal(r[k], s[k], err_msg=k)
+
+
+def test_scenario_major_past_the_grid_y_limit():
+    """A scenario-major batch on the exact kernels is transposed in and out
+    (fpf_layout.hip); the transpose's grid y dimension (row tiles of 32) caps
+    one launch at 65535 x 32 = 2 097 120 scenarios, so a longer batch goes in
+    several launches.  2.2 M scenarios of the demo feeder (device buffers):
+    the scenario-major results equal the scenario-fastest ones bit for bit."""
+    import torch
+    from freedm_amd import PowerFlow
+    f = F.demo_feeder()
+    dev = torch.device("cuda:0")
+    B = 2_200_000
+    base = torch.from_numpy(F.scenario_loads(f, np.arange(1024))).to(dev)          # [6][Nl][1024]
+    ids = torch.arange(B, device=dev)
+    x0 = (base[:, :, ids % 1024] * (0.9 + 0.2 * ((ids * 2654435761) % 1000).double() / 1000.0)).contiguous()
+    res = []
+    for layout, x in ((0, x0), (1, x0.permute(2, 0, 1).contiguous())):
+        pf = PowerFlow(f, exact=1, kernel="generic", layout=layout)
+        sh = (3, pf.nn, B) if layout == 0 else (B, 3, pf.nn)
+        out = {"v_re": torch.empty(sh, dtype=torch.float64, device=dev),
+               "iters": torch.empty(B, dtype=torch.int32, device=dev)}
+        pf.solve_device(x, out)
+        torch.cuda.synchronize()
+        v = out["v_re"] if layout == 0 else out["v_re"].permute(1, 2, 0)
+        res.append((out["iters"].cpu(), v.cpu()))
+        pf.close()
+        del x, out, v
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])

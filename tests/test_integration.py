@@ -76,12 +76,21 @@ def test_glue_against_oracle(tmp_path):
     pq[:, :, 7] *= 60.0                                  # diverges: the reference throws
     loads = [pq[:, :, s] for s in range(pq.shape[2])]
     _write_input(tmp_path / "in.bin", f, loads, exact=1)
-    subprocess.run([BIN, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], check=True, timeout=120)
+    subprocess.run([BIN, str(tmp_path / "in.bin"), str(tmp_path / "out.bin"), str(tmp_path / "log.txt")],
+                   check=True, timeout=120)
     res, single_ok, threw = _read_output(tmp_path / "out.bin")
     c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=4)
     assert single_ok
     nonconv = np.nonzero(c["status"] != 0)[0]
     assert threw == (int(nonconv[0]) if nonconv.size else -1)
+    # the reference's console lines of the K single calls (DPF_return7.cpp:38,206): a
+    # "Run DPF" line each, " DPF converged!" after the converged ones only
+    want = []
+    for s in range(len(loads)):
+        want.append(f"Run DPF on {f.n_nodes} Nodes System")
+        if c["status"][s] == 0:
+            want.append(" DPF converged!")
+    assert (tmp_path / "log.txt").read_text().splitlines() == want
     for s, r in enumerate(res):
         assert r["iters"] == c["iters"][s] and r["conv"] == (c["status"][s] == 0)
         np.testing.assert_array_equal(r["PQb"], c["PQb"][:, :, s].T)
