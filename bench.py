@@ -108,7 +108,8 @@ def _time_oracle(O, feeder, pq, threads: int, seconds: float):
     return n_conv / dt, passes, dt
 
 
-def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: bool = True, legs: int = 3):
+def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: bool = True, legs: int = 3,
+                 gpu_solve=None, n_check: int = 256):
     """The CPU oracle (oracle/ref_dpf.c, a scalar port of DPF_return7 + the VVC
     reductions) on this host: on every usable CPU (value, cores) and on one CPU,
     each as the median of `legs` legs of seconds / legs over the same chunk of the
@@ -157,7 +158,29 @@ def cpu_baseline(feeder, seconds: float = 10.0, chunk: int = 32768, config1: boo
         # not measured: what the whole host would give if the port scaled linearly
         # over every physical core at the better-measured per-core rate
         out["full_host_linear_estimate"] = per_core * phys
+    if gpu_solve is not None:
+        # the benched kernel against this oracle on the first n_check scenarios of the
+        # sample (the parity bar: V within 1e-10 relative, identical sweep counts)
+        sub = np.ascontiguousarray(pq[:, :, :n_check])
+        c = O.dpf_batch(feeder.Dl, feeder.Z, sub, nthreads=threads)
+        gv = gpu_solve(sub)
+        a = gv["V_re"] + 1j * gv["V_im"]
+        b = c["V_re"] + 1j * c["V_im"]
+        out["parity_sample"] = {"scenarios": int(sub.shape[2]),
+                                "max_v_rel_err": float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300))),
+                                "iters_identical": bool((gv["iters"] == c["iters"]).all()),
+                                "mean_sweeps": float(c["iters"].mean()),
+                                "note": "the benched kernel vs oracle/ref_dpf.c on the first scenarios of the "
+                                        "CPU-baseline sample (same feeder and scenario generator)"}
     return out
+
+
+def _gpu_solve_scen_fastest(pf, pq):
+    """pf.solve on a [6][Nl][B] host batch, results [..][B] whatever pf's layout."""
+    if pf.opts.layout == 1:
+        r = pf.solve(np.ascontiguousarray(pq.transpose(2, 0, 1)), full=True)
+        return {"V_re": np.moveaxis(r["V_re"], 0, -1), "V_im": np.moveaxis(r["V_im"], 0, -1), "iters": r["iters"]}
+    return pf.solve(pq, full=True)
 
 
 def config1_feeders():
@@ -614,12 +637,13 @@ def main():
             res["config1_vvc_round"] = c1
         if world == 1 and args.config == 3 and not args.no_cpu_baseline and not args.nodes:
             # the 2048-bus feeder on the host: a bounded sample of 1024 scenarios
-            cb = cpu_baseline(feeder, seconds=args.cpu_seconds, chunk=1024, config1=False)
+            cb = cpu_baseline(feeder, seconds=args.cpu_seconds, chunk=1024, config1=False,
+                              gpu_solve=lambda x: _gpu_solve_scen_fastest(pf, x))
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = value / cb["value"]
             res["speedup_vs_cpu_single_core"] = value / cb["single_core"]["value"]
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
-            cb = cpu_baseline(feeder, seconds=args.cpu_seconds)
+            cb = cpu_baseline(feeder, seconds=args.cpu_seconds, gpu_solve=lambda x: _gpu_solve_scen_fastest(pf, x))
             if "config1_vvc_round" in res and "config1_vvc_main" in cb:
                 for name1, c in res["config1_vvc_round"].items():
                     if isinstance(c, dict) and name1 in cb["config1_vvc_main"]:

@@ -17,12 +17,17 @@
 // pivoting (agreement to rounding: tests/test_vvc_round.py).
 #include "../../include/freedm_pf.h"
 
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include "fpf_gradb.h"
+#include "fpf_internal.h"
 
 #pragma clang fp contract(off)
 
@@ -43,6 +48,8 @@ struct PhaseNet {
     std::vector<cplx> sbus, rbus, zself; // rows of brnches for this phase (VoltVarCtrl.cpp:408-433)
     std::vector<cplx> Y;                // (lnum+1)^2, column-major (form_Yabc.cpp:118-220)
     std::vector<double> V, theta, node; // V_abc_list (lnum+1 each)
+    std::vector<int> vrow;              // the Vpolar row of each V_abc_list entry (-1: none, V = 0)
+    int scan_end = 0;                   // V_abc_list scanned Vpolar rows [0, scan_end)
     std::vector<int> s, r;              // renamed branch ends (rename_brn.cpp)
     cplx y(int a, int b) const { return Y[(size_t)a + (size_t)b * (lnum + 1)]; }
 };
@@ -88,22 +95,36 @@ bool lu_solve(std::vector<double> a, int n, std::vector<double> &x) {
     return true;
 }
 
-// The gradient at the DPF result vpolar (nn x 6) of table t.
-int gradient(const Table &t, int ncols, const double *z, int z_rows, const double *vpolar, int nn, double bkva,
-             double bkv, double beta0, int ld, double *g, double *load_nodes, int *n_loads, double *stats,
-             std::string *err) {
+}  // namespace
+
+// Everything of the gradient but the numbers that depend on the voltages'
+// values: the load lists, the per-phase branch lists and Y, the V_abc_list rows
+// (from vpolar's nonzero pattern) and the renamed branch ends; P.V / P.theta are
+// filled from vpolar as well (the host path).
+struct GradPlan {
+    int cnt_nodes = 0, lload[3] = {0, 0, 0};
+    std::vector<double> node_f, loads[3];
+    PhaseNet ph[3];
+};
+
+namespace {
+int build_plan(const Table &t, int ncols, const double *z, int z_rows, const double *vpolar, int nn, double bkva,
+               double bkv, GradPlan &plan, std::string *err) {
     const int nl = t.nl;
     if (ncols < 12) return FPF_ERR_ARG;
     // ---- Node_f and Load_a/b/c (VoltVarCtrl.cpp:354-398): (int) tests, and the scan
     // stops at the first full counter
     int cnt_nodes = 1;
-    int lload[3] = {0, 0, 0};
+    int *const lload = plan.lload;
     for (int i = 0; i < nl; ++i) {
         if ((int)t(i, 0) != 0) ++cnt_nodes;
         for (int x = 0; x < 3; ++x)
             if ((int)t(i, 6 + 2 * x) != 0) ++lload[x];
     }
-    std::vector<double> node_f(cnt_nodes, 0.0), loads[3];
+    plan.cnt_nodes = cnt_nodes;
+    std::vector<double> &node_f = plan.node_f;
+    std::vector<double> *const loads = plan.loads;
+    node_f.assign(cnt_nodes, 0.0);
     for (int x = 0; x < 3; ++x) loads[x].assign(lload[x], 0.0);
     {
         int jn = 1, jl[3] = {0, 0, 0};
@@ -137,7 +158,7 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
         }
         br.push_back(b);
     }
-    PhaseNet ph[3];
+    PhaseNet *const ph = plan.ph;
     for (int x = 0; x < 3; ++x)
         for (const Br &b : br)
             if (std::abs(b.z[x]) > 0) ++ph[x].lnum;
@@ -159,7 +180,6 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
                     ++fill[x];
                 }
     }
-    double gmin = INFINITY, gmax = -INFINITY;
     for (int x = 0; x < 3; ++x) {
         PhaseNet &P = ph[x];
         const int L = P.lnum, n = L + 1;
@@ -211,14 +231,20 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
         P.V.assign(n, 0.0);
         P.theta.assign(n, 0.0);
         P.node.assign(n, 0.0);
-        for (int i = 0, j = 0; i < nn && j < n; ++i) {
-            const double mag = vpolar[i + (size_t)(2 * x) * nn];
-            if (mag != 0) {
-                P.V[j] = mag;
-                P.theta[j] = vpolar[i + (size_t)(2 * x + 1) * nn];
-                P.node[j] = i < cnt_nodes ? node_f[i] : 0.0;
-                ++j;
+        P.vrow.assign(n, -1);
+        {
+            int i = 0;
+            for (int j = 0; i < nn && j < n; ++i) {
+                const double mag = vpolar[i + (size_t)(2 * x) * nn];
+                if (mag != 0) {
+                    P.V[j] = mag;
+                    P.theta[j] = vpolar[i + (size_t)(2 * x + 1) * nn];
+                    P.node[j] = i < cnt_nodes ? node_f[i] : 0.0;
+                    P.vrow[j] = i;
+                    ++j;
+                }
             }
+            P.scan_end = i;
         }
         // rename_brn: each end to its position in the V list (the last match wins)
         P.s.assign(L, 0);
@@ -232,6 +258,19 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
             P.s[i] = (int)s_new;
             P.r[i] = (int)r_new;
         }
+    }
+    return FPF_OK;
+}
+
+// The numbers at the plan's voltages (P.V, P.theta): Fx, J, lambda, g (host).
+int numeric(GradPlan &plan, double bkva, double beta0, int ld, double *g, double *load_nodes, int *n_loads,
+            double *stats, std::string *err) {
+    const int *const lload = plan.lload;
+    const std::vector<double> *const loads = plan.loads;
+    double gmin = INFINITY, gmax = -INFINITY;
+    for (int x = 0; x < 3; ++x) {
+        PhaseNet &P = plan.ph[x];
+        const int L = P.lnum, n = L + 1;
         // Fx = [dF/dtheta; dF/dV] over the n-1 non-reference buses
         const int m1 = n - 1, nf = 2 * m1;
         std::vector<double> Fx(nf, 0.0);
@@ -310,6 +349,16 @@ int gradient(const Table &t, int ncols, const double *z, int z_rows, const doubl
         stats[3] = beta0 / (bkva / 3) / gmin;     // cvq (:1323)
     }
     return FPF_OK;
+}
+
+// The gradient at the DPF result vpolar (nn x 6) of table t.
+int gradient(const Table &t, int ncols, const double *z, int z_rows, const double *vpolar, int nn, double bkva,
+             double bkv, double beta0, int ld, double *g, double *load_nodes, int *n_loads, double *stats,
+             std::string *err) {
+    GradPlan plan;
+    const int rc = build_plan(t, ncols, z, z_rows, vpolar, nn, bkva, bkv, plan, err);
+    if (rc != FPF_OK) return rc;
+    return numeric(plan, bkva, beta0, ld, g, load_nodes, n_loads, stats, err);
 }
 
 }  // namespace
@@ -433,4 +482,261 @@ extern "C" int fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, 
         std::memcpy(res, v, sizeof(v));
     }
     return nonconv ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// The batched gradient (VoltVarCtrl.cpp:1141-1325 for B scenarios of one control
+// table): base solves, V lists, Fx, J^T, the LU solves (fpf_vvc_gradb.hip: partial
+// pivoting, the host lu_solve's steps) and g all on the device;
+// the plan (load lists, branch lists, Y, V_abc_list rows, renamed branch ends)
+// on the host once per batch, from the first converged scenario.
+
+namespace {
+template <class T>
+struct DevArr {   // a device copy of a host vector
+    T *p = nullptr;
+    ~DevArr() { (void)hipFree(p); }
+    hipError_t up(const std::vector<T> &v) {
+        hipError_t e = hipMalloc(&p, sizeof(T) * std::max<size_t>(v.size(), 1));
+        if (e == hipSuccess && !v.empty()) e = hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice);
+        return e;
+    }
+};
+struct PhaseBufs {
+    DevArr<int32_t> vrow, bs, br, inc_ptr, inc_br, y_ptr, y_col, ld_ptr, ld_ia;
+    DevArr<int8_t> vmask, inc_role;
+    DevArr<double> yre_sr, y_re, y_im, ydiag_re, ydiag_im;
+};
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() { (void)hipFree(p); }
+};
+}  // namespace
+
+extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols, const double *z,
+                                      int z_rows, int z_cols, int n_scen, const double *pq, double beta0, int ld,
+                                      double *g, double *load_nodes, int *n_loads, double *stats,
+                                      signed char *gstatus) {
+    (void)z_cols;
+    if (!feeder || !ctrl_dl || !z || n_scen < 0 || (n_scen > 0 && (!pq || !g || !stats || !gstatus)) || !load_nodes ||
+        !n_loads || ld < 1 || ncols < 12)
+        return FPF_ERR_ARG;
+    fpf_feeder_info in;
+    if (fpf_feeder_get_info(feeder, &in) != FPF_OK || in.nl != nl) return FPF_ERR_ARG;
+    if (n_scen == 0) return 0;
+    const int B = n_scen, nn = in.nn;
+    const size_t b = (size_t)B;
+    // every scenario must give the (int) load tests of ctrl_dl (VoltVarCtrl.cpp:354-398):
+    // the load lists, and with them node_f, are the plan's
+    for (int x = 0; x < 3; ++x)
+        for (int i = 0; i < nl; ++i) {
+            const bool c = (int)ctrl_dl[(size_t)(6 + 2 * x) * nl + i] != 0;
+            const double *row = pq + ((size_t)(2 * x) * nl + i) * b;
+            for (int s = 0; s < B; ++s)
+                if (((int)row[s] != 0) != c) return FPF_ERR_ARG;
+        }
+    const double bkva = fpf_feeder_bkva(feeder), bkv = fpf_feeder_bkv(feeder);
+    hipStream_t st = nullptr;
+#define GCHK(expr)                                      \
+    do {                                                \
+        if ((expr) != hipSuccess) return FPF_ERR_HIP;   \
+    } while (0)
+    // ---- the base solves (VoltVarCtrl.cpp:1141), scenario fastest
+    DevBuf d_pq, d_vp, d_it, d_stt, d_loss, d_vmin, d_vmax, d_gst;
+    GCHK(hipMalloc(&d_pq.p, sizeof(double) * 6 * nl * b));
+    GCHK(hipMalloc(&d_vp.p, sizeof(double) * 6 * nn * b));
+    GCHK(hipMalloc(&d_it.p, sizeof(int32_t) * b));
+    GCHK(hipMalloc(&d_stt.p, b));
+    GCHK(hipMalloc(&d_loss.p, sizeof(double) * b));
+    GCHK(hipMalloc(&d_vmin.p, sizeof(double) * b));
+    GCHK(hipMalloc(&d_vmax.p, sizeof(double) * b));
+    GCHK(hipMalloc(&d_gst.p, b));
+    GCHK(hipMemcpy(d_pq.p, pq, sizeof(double) * 6 * nl * b, hipMemcpyHostToDevice));
+    fpf_outputs o;
+    std::memset(&o, 0, sizeof(o));
+    o.vpolar = (double *)d_vp.p;
+    o.iters = (int *)d_it.p;
+    o.status = (signed char *)d_stt.p;
+    o.loss = (double *)d_loss.p;
+    o.vmin = (double *)d_vmin.p;
+    o.vmax = (double *)d_vmax.p;
+    int rc = fpf::solve_batch_device_ex(feeder, B, (const double *)d_pq.p, &o, nullptr, (void *)st, nullptr, nullptr,
+                                        FPF_LAYOUT_SCEN_FASTEST);
+    if (rc < 0) return rc;
+    std::vector<int8_t> h_st(b);
+    std::vector<int32_t> h_it(b);
+    std::vector<double> h_loss(b), h_vmin(b), h_vmax(b);
+    GCHK(hipMemcpy(h_st.data(), d_stt.p, b, hipMemcpyDeviceToHost));
+    GCHK(hipMemcpy(h_it.data(), d_it.p, sizeof(int32_t) * b, hipMemcpyDeviceToHost));
+    GCHK(hipMemcpy(h_loss.data(), d_loss.p, sizeof(double) * b, hipMemcpyDeviceToHost));
+    GCHK(hipMemcpy(h_vmin.data(), d_vmin.p, sizeof(double) * b, hipMemcpyDeviceToHost));
+    GCHK(hipMemcpy(h_vmax.data(), d_vmax.p, sizeof(double) * b, hipMemcpyDeviceToHost));
+    int s0 = -1;
+    for (int s = 0; s < B && s0 < 0; ++s)
+        if (h_st[s] == FPF_CONVERGED) s0 = s;
+    std::vector<int8_t> h_gst(b);
+    for (int s = 0; s < B; ++s) h_gst[s] = h_st[s] == FPF_CONVERGED ? fpf::FPF_GRAD_OK : fpf::FPF_GRAD_NONCONV;
+    for (int s = 0; s < B; ++s) {
+        stats[(size_t)s * 8 + 4] = h_loss[s];   // Ploss_orig (:1152-1161)
+        stats[(size_t)s * 8 + 5] = h_vmin[s];   // Vmin_orig / Vmax_orig (:1201-1207)
+        stats[(size_t)s * 8 + 6] = h_vmax[s];
+        stats[(size_t)s * 8 + 7] = h_it[s];
+    }
+    std::memset(g, 0, sizeof(double) * b * 3 * ld);
+    if (s0 < 0) {
+        for (int s = 0; s < B; ++s) gstatus[s] = h_gst[s];
+        return B;
+    }
+    // ---- the plan, from the first converged scenario's Vpolar (nn x 6 column-major)
+    std::vector<double> vp0((size_t)6 * nn);
+    GCHK(hipMemcpy2D(vp0.data(), sizeof(double), (const double *)d_vp.p + s0, sizeof(double) * b, sizeof(double),
+                     (size_t)6 * nn, hipMemcpyDeviceToHost));
+    GradPlan plan;
+    std::string err;
+    rc = build_plan(Table{ctrl_dl, nl}, ncols, z, z_rows, vp0.data(), nn, bkva, bkv, plan, &err);
+    if (rc != FPF_OK) return rc;
+    GCHK(hipMemcpy(d_gst.p, h_gst.data(), b, hipMemcpyHostToDevice));
+    DevBuf d_g;
+    GCHK(hipMalloc(&d_g.p, sizeof(double) * b * 3 * ld));
+    GCHK(hipMemset(d_g.p, 0, sizeof(double) * b * 3 * ld));
+    for (int x = 0; x < 3; ++x) {
+        const PhaseNet &P = plan.ph[x];
+        const int L = P.lnum, n = L + 1, m1 = n - 1, nf = 2 * m1;
+        // the plan's arrays for the device
+        std::vector<int8_t> vmask((size_t)std::max(P.scan_end, 1), 0);
+        for (int j = 0; j < n; ++j)
+            if (P.vrow[j] >= 0) vmask[P.vrow[j]] = 1;
+        // (a branch end rename_brn did not find keeps its bus number, which can lie
+        // outside the V list: the reference would index past its vectors; refused here)
+        for (int j = 0; j < L; ++j)
+            if (P.s[j] < 0 || P.s[j] >= n || P.r[j] < 0 || P.r[j] >= n) return FPF_ERR_TOPOLOGY;
+        std::vector<double> yre_sr(L);
+        for (int j = 0; j < L; ++j) yre_sr[j] = P.y(P.s[j], P.r[j]).real();
+        std::vector<int32_t> inc_ptr(1, 0), inc_br;
+        std::vector<int8_t> inc_role;
+        for (int i = 0; i < m1; ++i) {
+            for (int j = 0; j < L; ++j) {
+                if (P.s[j] == i + 1) { inc_br.push_back(j); inc_role.push_back(0); }
+                if (P.r[j] == i + 1) { inc_br.push_back(j); inc_role.push_back(1); }
+            }
+            inc_ptr.push_back((int32_t)inc_br.size());
+        }
+        std::vector<int32_t> y_ptr(1, 0), y_col;
+        std::vector<double> y_re, y_im, yd_re(n), yd_im(n);
+        for (int a = 0; a < n; ++a) {
+            for (int m = 0; m < n; ++m) {
+                const cplx y = P.y(a, m);
+                if (m == a || (y.real() == 0 && y.imag() == 0)) continue;
+                y_col.push_back(m);
+                y_re.push_back(y.real());
+                y_im.push_back(y.imag());
+            }
+            y_ptr.push_back((int32_t)y_col.size());
+            yd_re[a] = P.y(a, a).real();
+            yd_im[a] = P.y(a, a).imag();
+        }
+        const int nld = std::min(plan.lload[x], ld);
+        n_loads[x] = nld;
+        std::vector<int32_t> ld_ptr(1, 0), ld_ia;
+        for (int j = 0; j < nld; ++j) {
+            load_nodes[(size_t)x * ld + j] = plan.loads[x][j];
+            for (int ia = 0; ia < L; ++ia)
+                if (P.node[ia + 1] == plan.loads[x][j]) ld_ia.push_back(ia);
+            ld_ptr.push_back((int32_t)ld_ia.size());
+        }
+        PhaseBufs pb;
+        GCHK(pb.vrow.up(P.vrow));
+        GCHK(pb.vmask.up(vmask));
+        GCHK(pb.bs.up(P.s));
+        GCHK(pb.br.up(P.r));
+        GCHK(pb.yre_sr.up(yre_sr));
+        GCHK(pb.inc_ptr.up(inc_ptr));
+        GCHK(pb.inc_br.up(inc_br));
+        GCHK(pb.inc_role.up(inc_role));
+        GCHK(pb.y_ptr.up(y_ptr));
+        GCHK(pb.y_col.up(y_col));
+        GCHK(pb.y_re.up(y_re));
+        GCHK(pb.y_im.up(y_im));
+        GCHK(pb.ydiag_re.up(yd_re));
+        GCHK(pb.ydiag_im.up(yd_im));
+        GCHK(pb.ld_ptr.up(ld_ptr));
+        GCHK(pb.ld_ia.up(ld_ia));
+        fpf::GradPhaseDev D;
+        D.x = x;
+        D.L = L;
+        D.n = n;
+        D.nn = nn;
+        D.scan_end = P.scan_end;
+        D.n_loads = nld;
+        D.vrow = pb.vrow.p;
+        D.vmask = pb.vmask.p;
+        D.bs = pb.bs.p;
+        D.br = pb.br.p;
+        D.yre_sr = pb.yre_sr.p;
+        D.inc_ptr = pb.inc_ptr.p;
+        D.inc_br = pb.inc_br.p;
+        D.inc_role = pb.inc_role.p;
+        D.y_ptr = pb.y_ptr.p;
+        D.y_col = pb.y_col.p;
+        D.y_re = pb.y_re.p;
+        D.y_im = pb.y_im.p;
+        D.ydiag_re = pb.ydiag_re.p;
+        D.ydiag_im = pb.ydiag_im.p;
+        D.ld_ptr = pb.ld_ptr.p;
+        D.ld_ia = pb.ld_ia.p;
+        // the dense J^T of a chunk of scenarios at a time (nf^2 doubles each, within ~2 GB)
+        const size_t per = (size_t)nf * nf * sizeof(double);
+        const int chunk = (int)std::max<size_t>(1, std::min<size_t>(b, ((size_t)2 << 30) / per));
+        DevBuf d_A, d_rhs, d_sing;
+        GCHK(hipMalloc(&d_A.p, per * chunk));
+        GCHK(hipMalloc(&d_rhs.p, sizeof(double) * nf * chunk));
+        GCHK(hipMalloc(&d_sing.p, chunk));
+        std::vector<int8_t> sing(chunk);
+        for (int c0 = 0; c0 < B; c0 += chunk) {
+            const int nb = std::min(chunk, B - c0);
+            double *A = (double *)d_A.p, *rhs = (double *)d_rhs.p;
+            GCHK(fpf::launch_gradb_setup(D, B, c0, nb, (const double *)d_vp.p, A, rhs, (int8_t *)d_gst.p, st));
+            // lambda = -inv(J^T) Fx: one LU with partial pivoting and one solve per matrix
+            GCHK(fpf::launch_gradb_lu(nf, nb, A, rhs, (int8_t *)d_sing.p, st));
+            GCHK(fpf::launch_gradb_g(D, c0, nb, rhs, ld, (double *)d_g.p, st));
+            GCHK(hipMemcpy(sing.data(), d_sing.p, nb, hipMemcpyDeviceToHost));
+            for (int k = 0; k < nb; ++k)
+                if (sing[k] != 0 && h_gst[c0 + k] == fpf::FPF_GRAD_OK) h_gst[c0 + k] = fpf::FPF_GRAD_SINGULAR;
+        }
+    }
+    // per-scenario results: the device's pattern flags merged with the host's
+    std::vector<int8_t> d_flags(b);
+    GCHK(hipMemcpy(d_flags.data(), d_gst.p, b, hipMemcpyDeviceToHost));
+    GCHK(hipMemcpy(g, d_g.p, sizeof(double) * b * 3 * ld, hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int s = 0; s < B; ++s) {
+        int8_t gs = h_gst[s];
+        if (gs == fpf::FPF_GRAD_OK && d_flags[s] != fpf::FPF_GRAD_OK) gs = d_flags[s];
+        gstatus[s] = gs;
+        double *st8 = stats + (size_t)s * 8;
+        if (gs != fpf::FPF_GRAD_OK) {
+            ++bad;
+            std::memset(g + (size_t)s * 3 * ld, 0, sizeof(double) * 3 * ld);
+            st8[0] = st8[1] = st8[2] = st8[3] = 0.0;
+            continue;
+        }
+        // gmin / gmax / gabs_min / c0 (:1319-1323) as the host path forms them
+        double gmin = INFINITY, gmax = -INFINITY;
+        for (int x = 0; x < 3; ++x) {
+            double gx_min = INFINITY, gx_max = 0.0;
+            for (int j = 0; j < n_loads[x]; ++j) {
+                const double a = g[((size_t)s * 3 + x) * ld + j];
+                gx_min = std::min(gx_min, std::fabs(a));
+                gx_max = std::max(gx_max, std::fabs(a));
+            }
+            gmin = std::min(gmin, gx_min);
+            gmax = std::max(gmax, gx_max);
+        }
+        st8[0] = gmin;
+        st8[1] = gmax;
+        st8[2] = gmin;
+        st8[3] = beta0 / (bkva / 3) / gmin;
+    }
+    return bad;
+#undef GCHK
 }

@@ -52,6 +52,12 @@ namespace fpf {
 #else
 #define WABL(bit) 0
 #endif
+// diagnostic build without the convergence guard's code (FPF_WBLK_NO_GUARD_CODE)
+#ifdef FPF_WBLK_NO_GUARD_CODE
+constexpr bool GUARD_CODE = false;
+#else
+constexpr bool GUARD_CODE = true;
+#endif
 
 namespace {
 constexpr int WB_C = 4;   // slots per lane
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 
     // the guard record: sum_k |S_k|_1 of the scenario (wtb[7], read after the loop;
     // Sld is overwritten by V in the last sweep)
-    if (o.flag_count) {
+    if (GUARD_CODE && o.flag_count) {
         double a = 0.0;
 #pragma unroll
         for (int c = 0; c < C; ++c)
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         // the convergence guard (fpf_wave.hip): err2 is the same in every lane of the
         // workgroup; a decision within 2^-9 of eps^2 keeps its distance in a register
         // (evaluated against the band after the loop)
-        if (o.flag_count) {
+        if (GUARD_CODE && o.flag_count) {
             const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
             if (dd <= 0x1p-9 * e2) dmin = fmin(dmin, dd);
         }
@@ -545,7 +551,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         if (o.status) o.status[s] = conv ? 0 : 1;
         if (o.loss) o.loss[s] = x;
         if (o.errmx) o.errmx[s] = sqrt(err2_last);
-        if (o.flag_count) {
+        if (GUARD_CODE && o.flag_count) {
             // the guard band (fpf_api.cpp: guard_factor) of a decision in the coarse
             // band: errmx within tau = guard_k sum_k |IL_k|_1 of eps, with sum_k
             // |IL_k|_1 <= sqrt2 sum_k |S_k|_1 / min_k |V_k| over the nonzero V (the

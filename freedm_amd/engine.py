@@ -283,6 +283,31 @@ class PowerFlow:
                 "gmin": st[0], "gmax": st[1], "gabs_min": st[2], "c0": st[3], "ploss_orig": st[4],
                 "vmin_orig": st[5], "vmax_orig": st[6], "iters": int(st[7])}
 
+    def vvc_gradient_batch(self, ctrl_dl: np.ndarray, pq: np.ndarray, beta0: float = 0.1) -> dict:
+        """fpf_vvc_gradient_batch: the gradient of every scenario of pq ([6][Nl][B],
+        the load columns 6..11 of ctrl_dl per scenario) as one device batch."""
+        L = _lib.load()
+        ctrl = np.asfortranarray(ctrl_dl, dtype=np.float64)
+        pq = np.ascontiguousarray(pq, dtype=np.float64)
+        if pq.ndim != 3 or pq.shape[:2] != (6, ctrl.shape[0]):
+            raise ValueError(f"pq must be [6][{ctrl.shape[0]}][B]")
+        B = pq.shape[2]
+        zbuf, zs = self._zbuf()
+        ld = ctrl.shape[0]
+        g, nodes, st = np.zeros((B, 3, ld)), np.zeros((3, ld)), np.zeros((B, 8))
+        gs = np.zeros(B, np.int8)
+        n = (C.c_int * 3)()
+        rc = L.fpf_vvc_gradient_batch(self.h, ctrl.ctypes.data_as(_lib._dp), ctrl.shape[0], ctrl.shape[1],
+                                      zbuf.ctypes.data_as(_lib._dp), zs[0], zs[1], B, pq.ctypes.data_as(_lib._dp),
+                                      float(beta0), ld, g.ctypes.data_as(_lib._dp), nodes.ctypes.data_as(_lib._dp), n,
+                                      st.ctypes.data_as(_lib._dp), gs.ctypes.data_as(C.POINTER(C.c_int8)))
+        if rc < 0:
+            raise DPFError(rc, self.ctx.err())
+        return {"g": [[g[s, x, :n[x]].copy() for x in range(3)] for s in range(B)],
+                "load_nodes": [nodes[x, :n[x]].copy() for x in range(3)], "gstatus": gs, "n_bad": rc,
+                "gmin": st[:, 0], "gmax": st[:, 1], "gabs_min": st[:, 2], "c0": st[:, 3], "ploss_orig": st[:, 4],
+                "vmin_orig": st[:, 5], "vmax_orig": st[:, 6], "iters": st[:, 7].astype(int)}
+
     def vvc_round(self, ctrl_dl: np.ndarray, beta0: float = 0.1, alpha: float = 1.1, m_max: int = 100) -> dict:
         """fpf_vvc_round: one VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762) --
         gradient, batched step-size search, reversal -- and the control after it."""

@@ -338,6 +338,26 @@ int         fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, const 
                                 const double *vpolar, int nn, double bkva, double bkv, double beta0, int ld,
                                 double *g, double *load_nodes, int *n_loads, double *stats);
 
+/* The gradient of n_scen scenarios of one control table as one batch (the
+ * gradient stage of VoltVarCtrl.cpp:1141-1325 per scenario, for a VVC Monte
+ * Carlo over load scenarios): scenario s is ctrl_dl with its load columns 6..11
+ * replaced by pq[.][.][s] (host, [6][Nl][n_scen], scenario fastest).  The base
+ * solves, the V lists, Fx, J (long double sums as double-double), the LU solves
+ * (rocSOLVER batched getrf/getrs, partial pivoting) and g run on the device; Y,
+ * the branch lists and the load lists are shared.  Every scenario's (int) load
+ * tests (columns 6, 8, 10) must equal ctrl_dl's (else FPF_ERR_ARG): they fix the
+ * load lists.  g [n_scen][3][ld]; load_nodes [3][ld] and n_loads [3] (shared);
+ * stats [n_scen][8] = gmin, gmax, gabs_min, c0, Ploss_orig, Vmin_orig,
+ * Vmax_orig, sweeps; gstatus [n_scen]: 0 ok, 1 the base solve did not converge
+ * (the reference throws), 2 singular J, 3 V_abc_list rows differ from the first
+ * converged scenario's (g and stats[0..3] are 0 unless 0).  Returns the number
+ * of scenarios with gstatus != 0, or FPF_ERR_* (FPF_ERR_UNSUPPORTED: no
+ * librocsolver). */
+int         fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
+                                   const double *z, int z_rows, int z_cols, int n_scen, const double *pq,
+                                   double beta0, int ld, double *g, double *load_nodes, int *n_loads,
+                                   double *stats, signed char *gstatus);
+
 /* One whole VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762): the gradient,
  * the step-size search as one batch (fpf_vvc_line_search), and the reversed
  * search when the reference reverses.  loss_fwd / loss_rev [m_max + 1] (loss_rev

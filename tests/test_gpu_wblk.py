@@ -227,3 +227,33 @@ def test_wblk_areas_equal_monolithic():
     vc = c["V_re"] + 1j * c["V_im"]
     assert float(np.max(np.abs(v - vc) / np.abs(vc))) <= 1e-10
     np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-8)
+
+
+def test_wblk_heavy_2048_bus():
+    """The benched 2048-bus feeder (config 3) under heavier loads than the bench's:
+    scale 1.7 .. 3.3 of the calibrated scenarios (SURVEY 8(d)'s Vmin ~ 0.92 and
+    below: 6 .. 12 sweeps, Vmin 0.93 .. 0.81), both batch layouts, against the
+    oracle: iteration counts and status identical, V within 1e-10 relative
+    (the max error is printed: the margin of the prefix-sum voltages)."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(2048, 2048)
+    B = 48
+    pq = F.scenario_loads(f, np.arange(B)) * np.geomspace(1.7, 3.3, B)[None, None, :]
+    pq = np.ascontiguousarray(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (c["status"] == 0).all() and c["iters"].min() <= 7 and c["iters"].max() >= 11
+    assert c["vmin"].min() < 0.85
+    for layout in (0, 1):
+        pf = PowerFlow(f, layout=layout)
+        assert pf.kernel == "wave" and pf.info["tile"] == 1
+        x = pq if layout == 0 else np.ascontiguousarray(pq.transpose(2, 0, 1))
+        r = pf.solve(x, full=False)
+        vr, vi = (r["V_re"], r["V_im"]) if layout == 0 else (np.moveaxis(r["V_re"], 0, -1), np.moveaxis(r["V_im"], 0, -1))
+        assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+        e = _vrel(vr, vi, c["V_re"], c["V_im"])
+        print(f"layout {layout}: max V rel err {e:.3e}, sweeps {c['iters'].min()}..{c['iters'].max()}")
+        assert e <= 1e-10
+        np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
+        np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-8)
+        pf.close()

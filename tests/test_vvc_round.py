@@ -151,3 +151,40 @@ def test_gradient_at_against_oracle_cpu(which):
         np.testing.assert_allclose(g[x, :n[x]], o["g"][x], rtol=1e-10, atol=0)
     for i, k in enumerate(("gmin", "gmax", "gabs_min", "c0")):
         assert st[i] == pytest.approx(o[k], rel=1e-10), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["demo", "dlnew", "123bus"])
+def test_gradient_batch_against_oracle(which):
+    """fpf_vvc_gradient_batch (batched): B = 64 load scenarios
+    of the control table, every scenario's gradient against ref_vvc.c at the
+    oracle's own solve of that scenario -- g within 1e-10, the load lists and
+    the step size c0 as the oracle's; one scenario with a different (int) load
+    pattern is refused."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = {"demo": F.demo_feeder, "dlnew": F.dl_new_feeder, "123bus": lambda: F.synthetic_feeder(123, 123)}[which]()
+    pf = PowerFlow(f, exact=1)
+    B = 64
+    # load scenarios that keep the control's (int) load tests (the load lists are shared):
+    # entries whose test would flip keep the control's value
+    base = np.ascontiguousarray(f.Dl[:, 6:12].T)[:, :, None]
+    pq = base * np.random.default_rng(7).uniform(0.6, 1.4, size=(6, f.nl, B))
+    flip = (pq.astype(np.int64) != 0) != (base.astype(np.int64) != 0)
+    pq = np.where(flip, base, pq)
+    r = pf.vvc_gradient_batch(f.Dl, pq)
+    assert r["n_bad"] == 0 and (r["gstatus"] == 0).all()
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    for s in range(B):
+        D = f.Dl.copy()
+        D[:, 6:12] = pq[:, :, s].T
+        o = O.vvc_gradient(D, f.Z, c["Vpolar"][:, :, s].T)   # [6][nn][B] -> nn x 6
+        for x in range(3):
+            np.testing.assert_array_equal(r["load_nodes"][x], o["load_nodes"][x])
+            np.testing.assert_allclose(r["g"][s][x], o["g"][x], rtol=1e-10, atol=0, err_msg=f"scenario {s}")
+        assert r["c0"][s] == pytest.approx(o["c0"], rel=1e-10)
+        assert r["iters"][s] == c["iters"][s]
+    bad = pq.copy()
+    bad[0, np.nonzero(base[0, :, 0].astype(np.int64) != 0)[0][0], 5] = 0.0   # scenario 5 loses a phase-a load
+    with pytest.raises(Exception):
+        pf.vvc_gradient_batch(f.Dl, bad)
