@@ -81,3 +81,50 @@ def test_multi_create_failure_reason():
     rc = L.fpf_multi_create(4096, dl.ctypes.data_as(_lib._dp), 1, 12, z.ctypes.data_as(_lib._dp), 0, 0, None, C.byref(h))
     assert rc < 0 and not h.value
     assert b"4096 devices requested" in L.fpf_multi_last_error(None)
+
+
+@pytest.mark.parametrize("n_gpus,n_scen,chunk", [(8, 1_000_000, 65536), (3, 100_001, 7000), (2, 5, 65536), (1, 0, 16)])
+def test_multi_schedule_issues_all_before_collecting(n_gpus, n_scen, chunk):
+    """fpf_multi_solve's order (fpf_multi_schedule, no device needed): every
+    scenario is issued once and collected once, on its shard's device; round r
+    of every device is issued before round r - 1 of any device is collected
+    (one host thread keeps all devices busy); a staging slot is reissued only
+    after its previous chunk was collected (double buffering)."""
+    import ctypes as C
+    from freedm_amd import _lib
+    L = _lib.load()
+    n_ops = L.fpf_multi_schedule(n_gpus, n_scen, chunk, None, 0)
+    assert n_ops >= 0
+    buf = (C.c_long * (4 * max(n_ops, 1)))()
+    assert L.fpf_multi_schedule(n_gpus, n_scen, chunk, buf, n_ops) == n_ops
+    ops = np.array(buf[:4 * n_ops], dtype=np.int64).reshape(-1, 4)   # kind, device, lo, hi
+    lo = np.zeros(n_gpus, np.int64)
+    hi = np.zeros(n_gpus, np.int64)
+    for d in range(n_gpus):
+        a, b = C.c_long(), C.c_long()
+        L.fpf_multi_shard(d, n_gpus, n_scen, C.byref(a), C.byref(b))
+        lo[d], hi[d] = a.value, b.value
+    for kind in (0, 1):
+        seen = np.zeros(n_scen, np.int32)
+        for k, d, a, b in ops[ops[:, 0] == kind]:
+            assert lo[d] <= a < b <= hi[d] and b - a <= chunk
+            seen[a:b] += 1
+        assert (seen == 1).all()
+    # position of each (kind, device, chunk start) in the order
+    pos = {(int(k), int(d), int(a)): i for i, (k, d, a, b) in enumerate(ops)}
+    rounds = {}
+    for (k, d, a), i in pos.items():
+        rounds[(k, d, a)] = (a - lo[d]) // chunk
+    for (k, d, a), i in pos.items():
+        if k != 1:
+            continue
+        r = rounds[(k, d, a)]
+        assert pos[(0, d, a)] < i   # a chunk is collected after it was issued
+        for d2 in range(n_gpus):    # ... and after round r + 1 of every device was issued
+            a2 = lo[d2] + (r + 1) * chunk
+            if a2 < hi[d2]:
+                assert pos[(0, d2, int(a2))] < i
+        # its slot (r & 1) is issued again (round r + 2) only after this collect
+        a3 = lo[d] + (r + 2) * chunk
+        if a3 < hi[d]:
+            assert pos[(0, d, int(a3))] > i
