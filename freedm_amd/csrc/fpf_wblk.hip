@@ -61,6 +61,7 @@ constexpr bool GUARD_CODE = true;
 
 namespace {
 constexpr int WB_C = 4;   // slots per lane
+constexpr int WB_BD = 6;  // block-chain depth resolved from registers (deeper: the LDS loop)
 
 // the wavefront totals [W][8] (6 used: re/im per phase) summed over the waves
 // before wave wv (pre) and over all waves (tot): lane j < W reads wave j's
@@ -194,6 +195,17 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             if (o.vsrc) v0 = make_double2(o.vsrc[(size_t)(2 * tid) * B + s], o.vsrc[(size_t)(2 * tid + 1) * B + s]);
             V0S[tid] = v0;
         }
+    }
+    // this thread's block chain (thread b < nblk resolves block b): the (tap,
+    // first - 1) index pairs, packed two per register, so that all of a chain's X
+    // reads issue together every sweep instead of one dependent pair per level
+    const bool chain_regs = bdepth <= WB_BD && nblk <= NT && XC < 65536;
+    int bp[WB_BD];
+#pragma unroll
+    for (int j = 0; j < WB_BD; ++j) {
+        const bool ok = chain_regs && j < bdepth && tid < nblk;
+        bp[j] = ok ? f.blk_pairs[(2 * j) * nblk + tid] | (f.blk_pairs[(2 * j + 1) * nblk + tid] << 16)
+                   : (XC - 1) | ((XC - 1) << 16);
     }
     int si[C], sb[C], bk[C], cz[C];
     double lg[C];
@@ -388,6 +400,24 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         if (!WABL(8)) __syncthreads();
         // block offsets, one thread per block, stored as V0 - off(b): off(b) = sum over
         // b's block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
+        if (chain_regs) {
+            if (tid < nblk) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+#pragma unroll
+                for (int j = 0; j < WB_BD; ++j) {
+                    if (j < bdepth) {   // uniform; levels past a chain's depth read the zero entry
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
+                    }
+                    // (two levels' twelve reads in flight at a time: the registers of
+                    // all of them at once would spill)
+                    if (j & 1) __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
+            }
+        } else
         for (int b = tid; b < nblk; b += NT) {
             cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
             for (int j = 0; j < bdepth; ++j) {
