@@ -278,6 +278,7 @@ int numeric(GradPlan &plan, double bkva, double beta0, int ld, double *g, double
             long double Rt = 0, Rv = 0;
             for (int j = 0; j < L; ++j) {
                 const int s = P.s[j], r = P.r[j];
+                if (s != i + 1 && r != i + 1) continue;   // (no term: no sin / cos to evaluate)
                 const double d = (P.theta[s] - P.theta[r]) * kPi / 180;
                 if (s == i + 1) {
                     Rt = Rt - 2 * (-P.y(s, r).real()) * P.V[s] * P.V[r] * (-std::sin(d));
@@ -296,15 +297,19 @@ int numeric(GradPlan &plan, double bkva, double beta0, int ld, double *g, double
         auto put = [&](int row, int col, double v) { Jt[(size_t)col + (size_t)row * nf] = v; };
         for (int a = 1; a < n; ++a) {
             long double Rs = 0, Rc = 0;   // sum over m != a of V_m (G sin - B cos), V_m (G cos + B sin)
+            // (a zero admittance contributes +-0 to these sums and +-0 entries to J: both
+            // skipped -- J starts zero, and a signed zero leaves a nonzero sum unchanged;
+            // Y of a radial feeder has a few nonzeros per row, so this is O(L), not O(L^2))
             for (int m = 0; m < n; ++m) {
-                if (m == a) continue;
-                const double d = (P.theta[a] - P.theta[m]) * kPi / 180;
                 const cplx yam = P.y(a, m);
+                if (m == a || (yam.real() == 0 && yam.imag() == 0)) continue;
+                const double d = (P.theta[a] - P.theta[m]) * kPi / 180;
                 Rs = Rs + P.V[m] * (yam.real() * std::sin(d) - yam.imag() * std::cos(d));
                 Rc = Rc + P.V[m] * (yam.real() * std::cos(d) + yam.imag() * std::sin(d));
             }
             for (int b = 1; b < n; ++b) {
                 const cplx yab = P.y(a, b);
+                if (a != b && yab.real() == 0 && yab.imag() == 0) continue;
                 if (a != b) {
                     const double d = (P.theta[a] - P.theta[b]) * kPi / 180;
                     const double sn = yab.real() * std::sin(d) - yab.imag() * std::cos(d);
