@@ -238,6 +238,20 @@ def _pmc_traffic(workload: str, kernel: str | None = None, key: str = "hbm_bytes
         return None
 
 
+def _instruction_efficiency(workload: str, kernel: str, flops_per_launch: float) -> dict:
+    """Useful fp64 flops per launch (the flop model above) / the issued VALU lane
+    capacity of the launch, 2 flops (an FMA) x 64 lanes per wave64 VALU
+    instruction, from the committed SQ_INSTS_VALU pass of this workload
+    (profiles/pmc_traffic.json "valu_insts_per_launch", tools/gpu_pmc_sq.sh): how
+    much of what the kernel issues on the VALU is the path's arithmetic (the rest:
+    DPP moves, address and loop arithmetic, the rounds of the scans)."""
+    v = _pmc_traffic(workload, kernel, key="valu_insts_per_launch")
+    if not v:
+        return {}
+    return {"valu_insts_per_launch": v, "instruction_efficiency": flops_per_launch / (128.0 * v),
+            "valu_source": _pmc_traffic(workload, kernel, key="valu_tag")}
+
+
 def _loads_on_device(torch, dev, loads, feeder, ids, seed, chunk=8192, layout=0):
     """[6][Nl][len(ids)] scenario loads of the global ids, generated on the host
     in chunks, scenario-fastest on the device."""
@@ -468,7 +482,9 @@ def main():
                          "bytes_alg_per_scenario": bytes_launch / B, "kernel_ms": avg_kern_s * 1e3,
                          "fp64": {"achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": fp64_tflops / FP64_PEAK_TFLOPS,
-                                  "mean_sweeps": k_sum / (B * args.steps)}},
+                                  "mean_sweeps": k_sum / (B * args.steps),
+                                  **_instruction_efficiency(f"{n_nodes}-bus x {B}", kname,
+                                                            flops / args.steps)}},
             "aggregate": {"loss_sum_kw": float(tot[0]), "vmin": float(tot[1]), "vmax": float(tot[2]),
                           "n_conv": int(tot[3]), "n_nonconv": int(tot[4]), "n_over": int(tot[5]),
                           "n_under": int(tot[6]), "n_scen": int(tot[7])},
@@ -494,7 +510,10 @@ def main():
                 "kernel_ms": ms4, "bytes_alg_per_scenario": bpa,
                 "converged_scenarios_per_s": conv4 / (ms4 / 1e3),
                 "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][lay4],
-                "mean_sweeps": float(o4["iters"].double().mean().item())}
+                "mean_sweeps": float(o4["iters"].double().mean().item()),
+                **_instruction_efficiency(f"{n4}-bus x {b4}", "dpf_wave_kernel",
+                                          123.0 * pf4.info["nb"] * float(o4["iters"].double().sum().item())
+                                          + 60.0 * pf4.nn * b4)}
             del d4
             pf4.close()
             # BASELINE config 3 beside it: the 2048-bus feeder x 65 536 scenarios on

@@ -22,3 +22,19 @@ def test_configs():
     assert bench.CONFIGS[2][:3] == (123, 123, 4096)
     assert bench.CONFIGS[3][:3] == (2048, 2048, 65536)
     assert bench.CONFIGS[4][2] * 8 == 1 << 20                         # 2^20 scenarios over 8 GPUs
+
+
+def test_instruction_efficiency_lookup(tmp_path, monkeypatch):
+    """roofline.fp64.instruction_efficiency: useful flops / (128 x the committed
+    SQ_INSTS_VALU per launch); absent when no SQ pass was committed."""
+    import json
+    import bench
+    d = {"by_workload": {"123-bus x 4096": {"kernel": "dpf_wave_kernel", "valu_insts_per_launch": 1.0e6,
+                                            "valu_tag": "t"}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(d))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    e = bench._instruction_efficiency("123-bus x 4096", "dpf_wave_kernel", 64.0e6)
+    assert e["instruction_efficiency"] == 0.5 and e["valu_source"] == "t"
+    assert bench._instruction_efficiency("123-bus x 4096", "dpf_wblk_kernel", 1.0) == {}
+    assert bench._instruction_efficiency("2048-bus x 1", "dpf_wave_kernel", 1.0) == {}
