@@ -84,6 +84,18 @@ extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr) {
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
 
+// experiments (tools/gpu_ab_trees.sh): IBO_LDS keeps the substation current of the
+// previous sweep (the convergence test's Ibo) in the scenario's LDS region instead
+// of 12 VGPRs of every lane; SLD_PREF reads slot 0's loads of the next sweep during
+// the forward sweep's LDS round trips
+#ifndef FPF_WAVE_IBO_LDS
+#define FPF_WAVE_IBO_LDS 0
+#endif
+#ifndef FPF_WAVE_SLD_PREF
+#define FPF_WAVE_SLD_PREF 0
+#endif
+constexpr int REGION_EXTRA = FPF_WAVE_IBO_LDS ? 3 : 0;
+
 template <int SPW, int C>
 struct WaveGeom {
     static constexpr int L = 64 / SPW;                 // lanes per scenario
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     double2 *const stg = (double2 *)(knode + C * L);
     double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
-    const int RS = (3 * XC + noff + 4) | 1;                          // double2 per region (+ the guard record)
+    const int RS = (3 * XC + noff + 4 + REGION_EXTRA) | 1;           // double2 per region (+ the guard record)
     double2 *const X = reg0 + sc * RS;
     double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
     // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
@@ -299,6 +311,8 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         bp[j] = ok ? pairs[(2 * j) * nblk + li] | (pairs[(2 * j + 1) * nblk + li] << 16) : (XC - 1) | ((XC - 1) << 16);
     }
     if (li < 3) X[li * XC + XC - 1] = make_double2(0.0, 0.0);
+    double2 *const IBO = X + 3 * XC + noff + 4;   // (FPF_WAVE_IBO_LDS) Ibo per phase
+    if (FPF_WAVE_IBO_LDS && li < 3) IBO[li] = make_double2(0.0, 0.0);
     // per-scenario results for the workgroup aggregate: [sc][loss, vmin, vmax, status]
     __shared__ double res[SPB][4];
 
@@ -344,6 +358,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     if (WPB >= 8 && wv >= WPB / 2) __builtin_amdgcn_s_sleep(FPF_WAVE_STAGGER);
 #endif
     WSTAMP(2);
+    cx slp[3];   // (FPF_WAVE_SLD_PREF) slot 0's loads, read a sweep ahead
+#pragma unroll
+    for (int p = 0; p < 3; ++p) slp[p] = FPF_WAVE_SLD_PREF ? ldx(stg, p * PSTR + sb[0]) : mk(0, 0);
     for (int it = 0; __ballot(!done) != 0; ++it) {
         WSTAMP(4 + 8 * it);
         // ---- load currents (:106-130)
@@ -364,7 +381,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // flight at a time
             cx sl[3], sn[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) sl[p] = ldx(stg, p * PSTR + sb[0]);
+            for (int p = 0; p < 3; ++p) sl[p] = FPF_WAVE_SLD_PREF ? slp[p] : ldx(stg, p * PSTR + sb[0]);
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
@@ -435,9 +452,14 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         double err2 = 0.0;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-            const double dr = tot[p].re - ibo[p].re, di = tot[p].im - ibo[p].im;
+            const cx io = FPF_WAVE_IBO_LDS ? ldx(IBO, p) : ibo[p];
+            const double dr = tot[p].re - io.re, di = tot[p].im - io.im;
             err2 = fmax(err2, fma(dr, dr, di * di));
-            ibo[p] = tot[p];
+            if (!FPF_WAVE_IBO_LDS) ibo[p] = tot[p];
+        }
+        if (FPF_WAVE_IBO_LDS && li == L - 1) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) stx(IBO, p, tot[p]);
         }
         // decided in the segment's last lane, broadcast by ballot
         const unsigned long long cbits = __ballot(li == L - 1 && err2 < f.eps * f.eps);
@@ -568,6 +590,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             }
         }
         wfence();
+        if (FPF_WAVE_SLD_PREF) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) slp[p] = ldx(stg, p * PSTR + sb[0]);
+        }
         WSTAMP(9 + 8 * it);
         // block offsets, one lane per block (block 0, node 1's chain, has none),
         // stored as V0 - off so that V = (V0 - off) - Ginc is one subtraction per
@@ -655,6 +681,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                         }
                     }
                 }
+            }
+            if (FPF_WAVE_IBO_LDS) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) ibo[p] = ldx(IBO, p);   // (this sweep's Ib(0))
             }
             if (li == L - 1) {   // the lane holding Ib(0)
 #pragma unroll
@@ -936,7 +966,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4) | 1);
+    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4 + REGION_EXTRA) | 1);
     const size_t stage = 16 * 3 * ((size_t)w.nl + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
     const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
