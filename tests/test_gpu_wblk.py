@@ -244,12 +244,24 @@ def test_wblk_heavy_2048_bus():
     c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
     assert (c["status"] == 0).all() and c["iters"].min() <= 7 and c["iters"].max() >= 11
     assert c["vmin"].min() < 0.85
+    import torch
+    dev = torch.device("cuda:0")
     for layout in (0, 1):
         pf = PowerFlow(f, layout=layout)
         assert pf.kernel == "wave" and pf.info["tile"] == 1
         x = pq if layout == 0 else np.ascontiguousarray(pq.transpose(2, 0, 1))
-        r = pf.solve(x, full=False)
-        vr, vi = (r["V_re"], r["V_im"]) if layout == 0 else (np.moveaxis(r["V_re"], 0, -1), np.moveaxis(r["V_im"], 0, -1))
+        # the light outputs (V and the scalars: the benched variant), device buffers
+        sh = (3, pf.nn, B) if layout == 0 else (B, 3, pf.nn)
+        o = {"v_re": torch.empty(sh, dtype=torch.float64, device=dev),
+             "v_im": torch.empty(sh, dtype=torch.float64, device=dev),
+             "iters": torch.empty(B, dtype=torch.int32, device=dev),
+             "status": torch.empty(B, dtype=torch.int8, device=dev),
+             "loss": torch.empty(B, dtype=torch.float64, device=dev),
+             "vmin": torch.empty(B, dtype=torch.float64, device=dev)}
+        pf.solve_device(torch.from_numpy(x).to(dev), o)
+        torch.cuda.synchronize()
+        r = {k: v.cpu().numpy() for k, v in o.items()}
+        vr, vi = (r["v_re"], r["v_im"]) if layout == 0 else (np.moveaxis(r["v_re"], 0, -1), np.moveaxis(r["v_im"], 0, -1))
         assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
         e = _vrel(vr, vi, c["V_re"], c["V_im"])
         print(f"layout {layout}: max V rel err {e:.3e}, sweeps {c['iters'].min()}..{c['iters'].max()}")
