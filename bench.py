@@ -183,6 +183,51 @@ def _gpu_solve_scen_fastest(pf, pq):
     return pf.solve(pq, full=True)
 
 
+def multi_leg(n_vis: int) -> dict:
+    """The one-process multi-GPU entry a Broker would use (fpf_multi_*: one host
+    thread drives every visible GPU; VoltVarCtrl.cpp:1141 runs on the Broker's
+    single io_service thread): the config-4 hosting study (131 072 scenarios,
+    host buffers, scalars out) on 1 and on all n_vis visible devices."""
+    from freedm_amd import MultiPowerFlow, hosting_loads, synthetic_feeder
+    feeder = synthetic_feeder(CONFIGS[4][0], CONFIGS[4][1])
+    Bm = CONFIGS[4][2]
+    pq_m = np.empty((Bm, 6, feeder.nl))
+    for a in range(0, Bm, 16384):
+        pq_m[a:a + 16384] = hosting_loads(feeder, np.arange(a, a + 16384), seed=CONFIGS[4][3]).transpose(2, 0, 1)
+    mres = {}
+    for n_dev in sorted({1, n_vis}):
+        mp = MultiPowerFlow(feeder, n_gpus=n_dev, layout=1)
+        rm = mp.solve(pq_m, full=False)
+        tm = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            rm = mp.solve(pq_m, full=False)
+            tm.append(time.perf_counter() - t0)
+        mres[str(n_dev)] = {"ms": min(tm) * 1e3, "scen_per_s": Bm / min(tm),
+                            "converged": int(rm["aggregate"]["n_conv"]), "n_scen": int(rm["aggregate"]["n_scen"])}
+        mp.close()
+    return {"workload": f"BASELINE config 4 study, {Bm} hosting scenarios, host buffers (843 MB in, scalars out), "
+                        "fpf_multi_solve", "devices": mres,
+            "speedup_all_vs_1": mres["1"]["ms"] / mres[str(n_vis)]["ms"],
+            "note": "PCIe-bound (host-resident inputs); never the bench value"}
+
+
+def _multi_leg_child(n_vis: int, timeout_s: float = 240.0) -> dict:
+    """multi_leg() in a child process (python bench.py --multi-leg N) with a time
+    limit: fpf_multi over several GPUs runs only where a process sees them (the
+    driver's 8-GPU node), so a failure there is reported, not fatal to the line."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--multi-leg", str(n_vis)],
+                           capture_output=True, text=True, timeout=timeout_s)
+        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        if r.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        return {"error": f"child exit {r.returncode}", "stderr_tail": r.stderr[-600:]}
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout_s:.0f} s"}
+
+
 def config1_feeders():
     """BASELINE config 1's feeders: the reference's own 9-row demo feeder
     (load_system_data.cpp), Broker/Dl_new.mat (IEEE 34-node, with the supplied Z)
@@ -306,6 +351,9 @@ def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--multi-leg":   # (bench.py's own child, _multi_leg_child)
+        print(json.dumps(multi_leg(int(sys.argv[2]))), flush=True)
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -626,31 +674,9 @@ def main():
             # more than one GPU is visible to this process (FPF_BENCH_MULTI=1 forces it
             # on one GPU to exercise the leg)
             n_vis = torch.cuda.device_count()
-            if n_vis > 1 or os.environ.get("FPF_BENCH_MULTI") == "1":
-                from freedm_amd import MultiPowerFlow
-                Bm = CONFIGS[4][2]
-                pq_m = np.empty((Bm, 6, feeder.nl))
-                for a in range(0, Bm, 16384):
-                    pq_m[a:a + 16384] = hosting_loads(feeder, np.arange(a, a + 16384),
-                                                      seed=CONFIGS[4][3]).transpose(2, 0, 1)
-                mres = {}
-                for n_dev in sorted({1, n_vis}):
-                    mp = MultiPowerFlow(feeder, n_gpus=n_dev, layout=1)
-                    rm = mp.solve(pq_m, full=False)
-                    tm = []
-                    for _ in range(3):
-                        t0 = time.perf_counter()
-                        rm = mp.solve(pq_m, full=False)
-                        tm.append(time.perf_counter() - t0)
-                    mres[str(n_dev)] = {"ms": min(tm) * 1e3, "scen_per_s": Bm / min(tm),
-                                        "converged": int(rm["aggregate"]["n_conv"])}
-                    mp.close()
-                res["multi_gpu_inproc"] = {
-                    "workload": f"BASELINE config 4 study, {Bm} hosting scenarios, host buffers (843 MB in, scalars "
-                                "out), fpf_multi_solve", "devices": mres,
-                    "speedup_all_vs_1": mres[str(1)]["ms"] / mres[str(n_vis)]["ms"],
-                    "note": "PCIe-bound (host-resident inputs); never the bench value"}
-                del pq_m
+            if (n_vis > 1 and os.environ.get("FPF_BENCH_MULTI") != "0") or os.environ.get("FPF_BENCH_MULTI") == "1":
+                # in a child process with a time limit: the bench line does not depend on it
+                res["multi_gpu_inproc"] = _multi_leg_child(n_vis)
             c1["note"] =("fpf_vvc_round (gradient + 101 step sizes in one batch + reversal), host-synchronous, "
                           "per config-1 feeder")
             res["config1_vvc_round"] = c1

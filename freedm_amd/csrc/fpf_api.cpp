@@ -1595,7 +1595,7 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
 
 int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                                void *stream, const double *d_vsrc, double *d_s_in, int layout, unsigned *d_flag_out,
-                               const int32_t *d_skip) {
+                               const int32_t *d_skip, const double *d_vinit_re, const double *d_vinit_im) {
     if (!f || n_scen < 0 || (n_scen > 0 && !d_pq)) return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "bad arguments");
     fpf_ctx *ctx = f->ctx;
     if (n_scen == 0) return FPF_OK;
@@ -1612,6 +1612,10 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     o.vsrc = d_vsrc;
     o.s_in = d_s_in;
     o.skip = d_skip;
+    o.vinit_re = d_vinit_re;
+    o.vinit_im = d_vinit_im;
+    if ((d_vinit_re != nullptr) != (d_vinit_im != nullptr) || (d_vinit_re && o.smaj))
+        return fail(ctx, FPF_ERR_ARG, "warm start: both planes, scenario-fastest batches only");
     hipError_t e;
     bool agg_done = false;
     const int kern = kernel_for(f, n_scen);
@@ -1664,7 +1668,7 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
         agg_done = true;
         HIPCHK(ctx, agg_before(f, st));
     }
-    if ((d_vsrc || d_s_in || d_skip) && kern != FPF_KERNEL_WAVE)
+    if ((d_vsrc || d_s_in || d_skip || d_vinit_re) && kern != FPF_KERNEL_WAVE)
         return fail(ctx, FPF_ERR_UNSUPPORTED, "per-scenario source voltages need the wave kernel");
     // the convergence guard: the fast kernel flags, the exact fixup kernel re-solves
     // (areas with per-scenario sources have no exact counterpart: no guard there)

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -76,6 +77,7 @@ struct fpf_areas {
     fpf_ctx *ctx = nullptr;
     int nl = 0, ncols = 0, nn = 0;
     double lb_v = 0.96, ub_v = 1.05;   // the hosting counters of the aggregate (fpf_opts)
+    bool warm = true;                  // warm-started area solves (FPF_AREAS_WARM=0: flat V0 each time)
     std::vector<Area> area;      // index = area id, parents before children
     std::vector<int> order;      // solve order
     int cap = 0, vcap = 0;
@@ -296,6 +298,7 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
     else fpf_opts_default(&o);
     a->lb_v = o.lb_v;
     a->ub_v = o.ub_v;
+    if (const char *e = getenv("FPF_AREAS_WARM")) a->warm = atoi(e) != 0;   // (A/B, tests)
     if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
         fpf_areas_destroy(a);
         return FPF_ERR_HIP;
@@ -422,7 +425,10 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
         AHIP(a, hipMemsetAsync(A.d_vsrc, 0, sizeof(double) * 6 * b, st));
     }
     const int single = a->area.size() == 1 ? 1 : 0;
-    auto enqueue_iteration = [&]() -> int {
+    // from the second outer iteration on, every area solve starts from its own V of
+    // the previous one (a warm start: its sweeps then only follow the boundary's
+    // move, instead of ~10 sweeps from the flat V0 to the inner tolerance)
+    auto enqueue_iteration = [&](bool warm) -> int {
         for (int ar : a->order) {
             Area &A = a->area[ar];
             // the boundary rows = their own load + the child's source power of the
@@ -444,7 +450,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
             o.vmax = A.d_vmax;
             const int r = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)st,
                                                 A.parent >= 0 ? A.d_vsrc : nullptr, A.d_sin, FPF_LAYOUT_SCEN_FASTEST,
-                                                nullptr, ctl);
+                                                nullptr, ctl, warm ? A.d_vre : nullptr, warm ? A.d_vim : nullptr);
             if (r < 0) return afail(a, r, std::string("area solve: ") + fpf_last_error(a->ctx));
         }
         AHIP(a, areas_check(a->d_diff, B, tol, single, ctl, last, st));
@@ -460,7 +466,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     bool stop = false;
     while (!stop && enq < max_outer) {
         for (int i = 0; i < K && enq < max_outer; ++i, ++enq) {
-            rc = enqueue_iteration();
+            rc = enqueue_iteration(enq > 0 && a->warm);
             if (rc) break;
         }
         if (rc) break;

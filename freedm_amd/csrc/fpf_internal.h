@@ -203,6 +203,11 @@ struct OutDev {
     // launch does nothing (the outer loop has converged; later iterations were
     // enqueued before the host looked).  NULL: always solve.  Wave kernels only.
     const int32_t *skip;
+    // the multi-area solve's warm start (wave kernels, [field][row][B] batches only):
+    // the sweeps start from these voltages ([3][Nn][B] re / im, the previous outer
+    // iteration's V of the area) instead of the flat V0 of DPF_return7.cpp:92-96.
+    // NULL: the reference's flat start
+    const double *vinit_re, *vinit_im;
 };
 
 // The exact re-solve of flagged scenarios (fpf_generic.hip: dpf_fixup_kernel):
@@ -220,7 +225,8 @@ int ctx_device(const fpf_ctx *ctx);   // the HIP device of a context
 // (OutDev::vsrc, OutDev::s_in; both device memory, may be NULL)
 int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                           void *stream, const double *d_vsrc, double *d_s_in, int layout,
-                          unsigned *d_flag_out = nullptr, const int32_t *d_skip = nullptr);
+                          unsigned *d_flag_out = nullptr, const int32_t *d_skip = nullptr,
+                          const double *d_vinit_re = nullptr, const double *d_vinit_im = nullptr);
 // the exact re-solve of the scenarios a deferred (d_flag_out) guarded solve flagged
 int fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                        void *stream, int layout);

@@ -330,6 +330,17 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         for (int c = 0; c < C; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
+        if (o.vinit_re && live) {
+            // the multi-area solve's warm start: node k of each slot from the given V
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                if (si_valid(si[c])) {
+                    const int k = knode[c * L + li];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        v[c][p] = mk(o.vinit_re[((size_t)p * nn + k) * B + s], o.vinit_im[((size_t)p * nn + k) * B + s]);
+                }
+        }
     }
 
     // A scenario's results are recorded in its last sweep (converged, or the

@@ -242,6 +242,17 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 #pragma unroll
         for (int c = 0; c < C; ++c) v[c][p] = v0;   // V(0..Nl-1) = V0  (:92-96)
     }
+    if (o.vinit_re) {
+        // the multi-area solve's warm start: node k of each slot from the given V
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (si_valid(si[c])) {
+                const int k = f.slot_node[c * L + tid];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    v[c][p] = mk(o.vinit_re[((size_t)p * nn + k) * B + s], o.vinit_im[((size_t)p * nn + k) * B + s]);
+            }
+    }
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     int it = 0;
     bool conv = false;
