@@ -188,3 +188,14 @@ def test_gradient_batch_against_oracle(which):
     bad[0, np.nonzero(base[0, :, 0].astype(np.int64) != 0)[0][0], 5] = 0.0   # scenario 5 loses a phase-a load
     with pytest.raises(Exception):
         pf.vvc_gradient_batch(f.Dl, bad)
+    # a scenario whose base solve does not converge (the reference throws there):
+    # gstatus 1, its g zero, every other scenario's gradient unchanged
+    heavy = pq.copy()
+    heavy[:, :, 3] *= 80.0
+    c3 = O.dpf_batch(f.Dl, f.Z, heavy[:, :, 3:4], nthreads=1)
+    if c3["status"][0] != 0:
+        h = pf.vvc_gradient_batch(f.Dl, heavy)
+        assert h["n_bad"] == 1 and h["gstatus"][3] == 1 and (np.delete(h["gstatus"], 3) == 0).all()
+        assert all((h["g"][3][x] == 0).all() for x in range(3))
+        for x in range(3):
+            np.testing.assert_array_equal(h["g"][7][x], r["g"][7][x])
