@@ -67,6 +67,7 @@ struct fpf_feeder {
     // waves per workgroup of large batches
     void *d_wave = nullptr;
     WaveDev wdev{}, wdev_big{};
+    void *d_xch = nullptr, *d_xsync = nullptr;   // the paired wave-block kernel's exchange
     // the partials + ticket scratch is shared by every aggregating launch on
     // this feeder (fused wave/specialised aggregate, fpf_aggregate_device): a
     // launch on another stream than the previous one first waits for it
@@ -414,20 +415,132 @@ struct WaveHost {
     int temp_sym = 0;
     int wpb_big_batch = 0;
     int wps = 0;                     // wave-block kernel: wavefronts per scenario (0: per-wavefront kernel)
-    std::vector<int32_t> row, node, info, blk, mref, pairs;
+    int coop = 0, nb_c = 0, nf_c = 0, nb_split = 0, nf_split = 0;   // paired wave-block kernel (fpf_wcoop.hip)
+    std::vector<int32_t> row, node, info, blk, mref, pairs, info2;
     std::vector<double> temp;
     std::vector<double> lng, code_z;   // wave-block kernel: per slot lng, per code Zl (fpf_internal.h)
     std::vector<int32_t> code;
 };
 
+// The tables of the paired wave-block kernel (fpf_wcoop.hip, 2049..4096
+// branches): the positions [0, P) of the depth-first order on workgroup 0, [P, n)
+// on workgroup 1 (P = ceil(n / 2)), C slots per lane of 512; the gathered
+// positions numbered in position order so that each workgroup owns one range of
+// the backward and of the forward index space.
+static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps, int nblk, int maxd, int has_mask,
+                         const std::vector<int> &par, const std::vector<int> &at, const std::vector<int> &pos,
+                         const std::vector<int> &blk, const std::vector<int> &size, const std::vector<int> &bfirst) {
+    auto no = [&](const std::string &why) { w.ok = false; w.why = why; };
+    if (has_mask) return no("paired wave-block kernel: zeroed phases (the generic kernel runs them)");
+    const int L = 64 * wps, P = (n + 1) / 2;
+    if (P > C * L || n - P > C * L) return no("paired wave-block kernel: more than 2 x 2048 positions");
+    if (nblk > L || maxd > 6) return no("paired wave-block kernel: block chains beyond the register-resolved form");
+    std::vector<char> isb(n, 0), isf(n, 0);
+    for (int q = 0; q < n; ++q) isb[q + size[at[q]] - 1] = 1;
+    for (int b = 1; b < nblk; ++b) {
+        isf[pos[par[bfirst[b]]]] = 1;
+        isf[pos[bfirst[b]] - 1] = 1;
+    }
+    std::vector<int> cb(n, -1), cf(n, -1);
+    int nb = 0, nf = 0, nbs = 0, nfs = 0;
+    for (int q = 0; q < n; ++q) {
+        if (q == P) {
+            nbs = nb;
+            nfs = nf;
+        }
+        if (isb[q]) cb[q] = nb++;
+        if (isf[q]) cf[q] = nf++;
+    }
+    const int ncomp = std::max(nb, nf);
+    if (ncomp > 16000) return no("paired wave-block kernel: too many gathered positions");
+    int bdepth = 0;
+    std::vector<std::vector<std::pair<int, int>>> chainp(nblk);
+    for (int b = 1; b < nblk; ++b) {
+        for (int j = b; j != 0; j = blk[par[bfirst[j]]]) chainp[b].push_back({cf[pos[par[bfirst[j]]]], cf[pos[bfirst[j]] - 1]});
+        bdepth = std::max(bdepth, (int)chainp[b].size());
+    }
+    w.pairs.assign((size_t)std::max(bdepth, 1) * 2 * nblk, ncomp);
+    for (int b = 1; b < nblk; ++b)
+        for (size_t j = 0; j < chainp[b].size(); ++j) {
+            w.pairs[(2 * j) * nblk + b] = chainp[b][j].first;
+            w.pairs[(2 * j + 1) * nblk + b] = chainp[b][j].second;
+        }
+    const size_t S = (size_t)2 * C * L;
+    w.row.assign(S, -1);
+    w.node.assign(S, -1);
+    w.info.assign(S, (int32_t)((uint32_t)ncomp << 18));   // empty slot: gathers the zero entry, stores nothing
+    w.info2.assign(S, 0);
+    w.blk.assign(S, 0);
+    w.lng.assign(S, 0.0);
+    w.code.assign(S, 0);
+    bool zsym = !getenv("FPF_WAVE_NO_SYM");
+    for (int q = 0; q < n; ++q) {
+        const int k = at[q], g = q >= P, ql = q - g * P, i = (g * C + ql % C) * L + ql / C;
+        const NodeOp &nd = h.node[k];
+        w.row[i] = nd.row;
+        w.node[i] = k;
+        w.info[i] = (int32_t)(8u | ((uint32_t)(cb[q] + 1) << 4) | ((uint32_t)cb[q + size[k] - 1] << 18));
+        w.info2[i] = cf[q] + 1;
+        w.blk[i] = blk[k];
+        w.lng[i] = h.at(nd.row, 4);
+        w.code[i] = nd.code;
+        const cx *z = &h.zl[(size_t)nd.code * 9];
+        for (int j = 1; j < 9 && zsym; ++j)
+            if (j % 4 != 0) zsym = z[j].re == z[1].re && z[j].im == z[1].im;
+    }
+    const int ntz = zsym ? 4 : 9;
+    w.code_z.assign((size_t)h.ncode * ntz * 2, 0.0);
+    for (int cd = 0; cd < h.ncode; ++cd) {
+        const cx *z = &h.zl[(size_t)cd * 9];
+        for (int j = 0; j < ntz; ++j) {
+            const cx v = !zsym ? z[j] : (j < 3 ? csub(z[4 * j], z[1]) : z[1]);
+            w.code_z[((size_t)cd * ntz + j) * 2] = v.re;
+            w.code_z[((size_t)cd * ntz + j) * 2 + 1] = v.im;
+        }
+    }
+    w.temp_sym = zsym ? 1 : 0;
+    w.n = n;
+    w.spw = 1;
+    w.C = C;
+    w.nblk = nblk;
+    w.bdepth = bdepth;
+    w.ncomp = ncomp;
+    w.has_rel = 0;
+    w.has_mask = 0;
+    w.off_in_x = 0;
+    w.wps = wps;
+    w.coop = 2;
+    w.nb_c = nb;
+    w.nf_c = nf;
+    w.nb_split = nbs;
+    w.nf_split = nfs;
+    WaveDev probe{};
+    probe.wps = wps;
+    probe.coop = 2;
+    probe.nl = h.nl;
+    probe.nblk = nblk;
+    probe.ncomp = ncomp;
+    probe.temp_sym = w.temp_sym;
+    probe.ncode = h.ncode;
+    if (wcoop_lds_bytes(probe) > WAVE_LDS_BUDGET) return no("paired wave-block kernel: LDS budget exceeded");
+    w.wpb = w.wpb_big_batch = wps;
+    w.ok = true;
+}
+
 void analyse_wave(const HostFeeder &h, WaveHost &w) {
     auto no = [&](const std::string &why) { w.ok = false; w.why = why; };
     if (!h.wf) return no("not well formed: " + h.wf_why);
     const int nl = h.nl, nn = h.nn, n = nn - 1;
-    int spw = 0, C = 0, wps = 0;
+    int spw = 0, C = 0, wps = 0, coop = 0;
     if (!wave_geometry(n, &spw, &C)) {
-        // one scenario per workgroup of wps wavefronts (fpf_wblk.hip)
-        if (!wblk_geometry(n, &wps, &C)) return no("more than 2048 branches");
+        // one scenario per workgroup of wps wavefronts (fpf_wblk.hip); above 2048
+        // branches one scenario per pair of such workgroups (fpf_wcoop.hip)
+        if (!wblk_geometry(n, &wps, &C)) {
+            if (n > 2 * 2048 || getenv("FPF_NO_COOP")) return no("more than 4096 branches");
+            coop = 2;
+            wps = 8;
+            C = 4;
+        }
         spw = 1;
     }
     const int L = wps ? 64 * wps : 64 / spw;
@@ -578,6 +691,7 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
             if (comp[q] >= 0) comp[q] = renum[comp[q]];
         ncomp = top;   // holes allowed
     };
+    if (coop) return analyse_coop(h, w, n, C, wps, nblk, maxd, has_mask, par, at, pos, blk, size, bfirst);
     if (!wps) {   // (the bank colouring assumes one scenario within a wavefront)
         color_space(cb, nb_c, true);
         color_space(cf, nf_c, false);
@@ -1335,6 +1449,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         const size_t o_mref = push_blob(wb, wh.mref);
         const size_t o_tmp = push_blob(wb, wh.temp), o_pairs = push_blob(wb, wh.pairs);
         const size_t o_lng = push_blob(wb, wh.lng), o_code = push_blob(wb, wh.code), o_cz = push_blob(wb, wh.code_z);
+        const size_t o_info2 = push_blob(wb, wh.info2);
         e = hipMalloc(&f->d_wave, wb.size());
         if (e == hipSuccess) e = hipMemcpy(f->d_wave, wb.data(), wb.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
@@ -1375,7 +1490,28 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.slot_lng = (const double *)(wbase + o_lng);
         w.slot_code = (const int32_t *)(wbase + o_code);
         w.code_z = (const double *)(wbase + o_cz);
-        if ((w.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w)) > WAVE_LDS_BUDGET) {
+        if (wh.coop) {
+            // the paired kernel's exchange areas (one per scenario in flight) and
+            // their arrival counts / generations (zeroed before every launch)
+            w.coop = wh.coop;
+            w.nb_c = wh.nb_c;
+            w.nf_c = wh.nf_c;
+            w.nb_split = wh.nb_split;
+            w.nf_split = wh.nf_split;
+            w.slot_info2 = (const int32_t *)(wbase + o_info2);
+            w.coop_nslot = COOP_NSLOT;
+            w.coop_area = (48 + 6 * (wh.nb_c + wh.nf_c) + 15) & ~15;
+            e = hipMalloc(&f->d_xch, sizeof(double) * (size_t)w.coop_nslot * w.coop_area);
+            if (e == hipSuccess) e = hipMalloc(&f->d_xsync, sizeof(unsigned) * (2 * (size_t)w.coop_nslot + 16));
+            if (e == hipSuccess) e = hipMemset(f->d_xsync, 0, sizeof(unsigned) * (2 * (size_t)w.coop_nslot + 16));
+            if (e != hipSuccess) {
+                fpf_feeder_destroy(f);
+                return fail(ctx, FPF_ERR_HIP, std::string("paired kernel exchange areas: ") + hipGetErrorString(e));
+            }
+            w.xch = (double *)f->d_xch;
+            w.xsync = (unsigned *)f->d_xsync;
+        }
+        if (wave_any_lds_bytes(w) > WAVE_LDS_BUDGET) {
             fpf_feeder_destroy(f);
             return fail(ctx, FPF_ERR_UNSUPPORTED, "wave kernel: LDS budget exceeded");
         }
@@ -1456,6 +1592,8 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_partials);
     (void)hipFree(f->d_ticket);
     (void)hipFree(f->d_wave);
+    (void)hipFree(f->d_xch);
+    (void)hipFree(f->d_xsync);
     (void)hipFree(f->d_lay);
     (void)hipHostFree(f->h_stage);
     (void)hipFree(f->d_flag_count);
@@ -1917,8 +2055,9 @@ extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const d
     w.off_in_x = wh.off_in_x;
     w.temp_sym = wh.temp_sym;
     w.wps = wh.wps;
+    w.coop = wh.coop;
     w.ncode = h.ncode;
-    const int lds = !wh.ok ? 0 : (int)(wh.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w));
+    const int lds = !wh.ok ? 0 : (int)wave_any_lds_bytes(w);
     const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, lds, wh.ncomp, wh.nblk, wh.bdepth};
     std::memcpy(out, v, sizeof(v));
     return FPF_OK;

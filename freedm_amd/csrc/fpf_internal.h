@@ -162,6 +162,20 @@ struct WaveDev {
     const double *slot_lng;     // [C][L]
     const int32_t *slot_code;   // [C][L] 0-based line code
     const double *code_z;       // [ncode][4 or 9] complex
+    // paired wave-block kernel (fpf_wcoop.hip): feeders of 2049..4096 branches, one
+    // scenario on coop = 2 workgroups (8 wavefronts, C = 4 each), workgroup g holding
+    // the positions [g P, ...) of the depth-first order; the per-slot tables are
+    // [2][C][L].  slot_info there: bits 0-2 zero mask, 3 valid, 4-17 backward index
+    // + 1, 18-31 the subtree end's backward index (unsigned); slot_info2: forward
+    // index + 1.  Backward / forward indices number the gathered positions in
+    // position order, so workgroup 1 owns the entries from nb_split / nf_split on.
+    // The two workgroups exchange their scan values through xch (coop_nslot areas
+    // of coop_area doubles, one per scenario in flight) and xsync (arrival counts
+    // [nslot], area generations [nslot], error word).  coop = 0: not this kernel.
+    int32_t coop, nb_c, nf_c, nb_split, nf_split, coop_nslot, coop_area;
+    const int32_t *slot_info2;
+    double *xch;
+    unsigned *xsync;
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -249,6 +263,12 @@ size_t wave_lds_bytes(const WaveDev &w);
 hipError_t launch_transpose(const double *in, double *out, size_t rows, size_t cols, hipStream_t st);
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wblk_lds_bytes(const WaveDev &w);
+hipError_t launch_wcoop(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+size_t wcoop_lds_bytes(const WaveDev &w);
+constexpr int COOP_NSLOT = 1024;   // exchange areas of the paired kernel (scenarios in flight <= 256)
+inline size_t wave_any_lds_bytes(const WaveDev &w) {
+    return w.coop ? wcoop_lds_bytes(w) : (w.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w));
+}
 bool wblk_geometry(int n, int *wps, int *c);
 bool wave_geometry(int n, int *spw, int *c);
 int wave_scenarios_per_block(const WaveDev &w);

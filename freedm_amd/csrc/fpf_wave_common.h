@@ -107,6 +107,43 @@ __device__ __forceinline__ cx il_fast(cx s, cx v) {
     return mk(fma(s.re, v.re, s.im * v.im) * r, fma(s.re, v.im, -(s.im * v.re)) * r);
 }
 
+// the wavefront totals [W][8] (6 used: re/im per phase) summed over the waves
+// before wave wv (pre) and over all waves (tot): lane j < W reads wave j's
+// totals, a DPP scan over those lanes, the sums read back as wave-uniform
+// values.  Every wave computes the same scan, so tot (Ib(0) in the backward
+// sweep) is the same in every wave of the workgroup.
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+    return __hiloint2double(hi, lo);
+}
+template <int W, bool TOT>
+__device__ __forceinline__ void wave_prefix(const double *wt, int wv, int lane, double (&pre)[6], double (&tot)[6]) {
+    const int j = lane < W ? lane : 0;
+    const double2 *t2 = (const double2 *)(wt + 8 * j);
+    const double2 a = t2[0], b = t2[1], c = t2[2];
+    double t[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+#pragma unroll
+    for (int q = 0; q < 6; ++q) t[q] = lane < W ? t[q] : 0.0;
+    if (W > 1) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x111, 0xf, 0xf>(t[q]);
+    }
+    if (W > 2) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x112, 0xf, 0xf>(t[q]);
+    }
+    if (W > 4) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x114, 0xf, 0xf>(t[q]);
+    }
+    const int wu = __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        pre[q] = wu == 0 ? 0.0 : readlane_d(t[q], wu - 1);
+        if (TOT) tot[q] = readlane_d(t[q], W - 1);
+    }
+}
 // Outputs of node k, phase p (DPF_return7.cpp:222-253); returns (Re SL, |V|)
 __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn, int B, int k, int p, size_t s, cx v,
                                              cx il, cx ib) {

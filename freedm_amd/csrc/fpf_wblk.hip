@@ -63,43 +63,6 @@ namespace {
 constexpr int WB_C = 4;   // slots per lane
 constexpr int WB_BD = 6;  // block-chain depth resolved from registers (deeper: the LDS loop)
 
-// the wavefront totals [W][8] (6 used: re/im per phase) summed over the waves
-// before wave wv (pre) and over all waves (tot): lane j < W reads wave j's
-// totals, a DPP scan over those lanes, the sums read back as wave-uniform
-// values.  Every wave computes the same scan, so tot (Ib(0) in the backward
-// sweep) is the same in every wave of the workgroup.
-__device__ __forceinline__ double readlane_d(double x, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-    return __hiloint2double(hi, lo);
-}
-template <int W, bool TOT>
-__device__ __forceinline__ void wave_prefix(const double *wt, int wv, int lane, double (&pre)[6], double (&tot)[6]) {
-    const int j = lane < W ? lane : 0;
-    const double2 *t2 = (const double2 *)(wt + 8 * j);
-    const double2 a = t2[0], b = t2[1], c = t2[2];
-    double t[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-#pragma unroll
-    for (int q = 0; q < 6; ++q) t[q] = lane < W ? t[q] : 0.0;
-    if (W > 1) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x111, 0xf, 0xf>(t[q]);
-    }
-    if (W > 2) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x112, 0xf, 0xf>(t[q]);
-    }
-    if (W > 4) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x114, 0xf, 0xf>(t[q]);
-    }
-    const int wu = __builtin_amdgcn_readfirstlane(wv);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        pre[q] = wu == 0 ? 0.0 : readlane_d(t[q], wu - 1);
-        if (TOT) tot[q] = readlane_d(t[q], W - 1);
-    }
-}
 }  // namespace
 
 template <int W, bool FULL, int C>
@@ -722,6 +685,7 @@ WblkKernel pick_wblk(bool full) {
 }  // namespace
 
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
+    if (w.coop) return launch_wcoop(w, n_scen, pq, o, st);   // 2049..4096 branches: fpf_wcoop.hip
     // the full-output variant keeps IL and Ib of the last sweep (Vpolar / PQb /
     // PQL), and the zeroed-phase paths
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;

@@ -1,0 +1,631 @@
+// fpf_wcoop.hip -- the paired wave-block kernel (fast mode, fpf_opts.exact = 0)
+// for feeders of 2049..4096 branches: every sweep of DPF_return7
+// (Broker/src/vvc/DPF_return7.cpp:104-217) over two workgroups per scenario.
+//
+// One 2048-branch scenario already fills a CU (fpf_wblk.hip: V and the sweep
+// temporaries in 8 wavefronts' registers, the loads in LDS), so a larger one
+// takes two CUs.  The depth-first position order of fpf_wblk.hip is cut in two:
+// workgroup g holds the positions [g P, g P + P) (P = ceil(n / 2)), 8 wavefronts
+// x 64 lanes x C = 4 slots, with its slots' loads in its own LDS and V in
+// registers for the whole solve.  Each prefix scan (the backward sweep's subtree
+// sums of IL, :134-160; the forward sweep's path sums of the drops, :163-195) is
+// computed per workgroup; the two workgroups then exchange, through an L2-backed
+// area of their own, the workgroup totals and the scan values at the positions
+// they own that either side gathers (subtree ends; block taps and the positions
+// before lateral blocks).  Each side rebuilds the whole gathered array X in its
+// LDS, adding workgroup 0's total to workgroup 1's values, so every gather and
+// block offset is the global prefix -- two exchanges per sweep.  Ib(0) is the sum
+// of the two totals in one fixed order on both sides, so the convergence test
+// (:199-217) takes the same decision in both workgroups.
+//
+// Synchronisation: the members of scenario t are workgroups b and b + 8 (one
+// XCD), dispatched in order, so a waiting workgroup's partner is resident or
+// next in line.  A member publishes with agent-scope stores, waits for its
+// stores, then adds one to the area's arrival count; the other polls the count
+// (thread 0, with s_sleep between polls) and reads with agent-scope loads.  A wait
+// gives up after a bounded number of polls (the error word is set, every
+// workgroup of the launch stops at its next wait, the scenario reports status 1),
+// so a launch always drains.  The areas are reused round robin (COOP_NSLOT of
+// them); a scenario waits until the area's previous scenario has released it.
+//
+// Zeroed phases are declined on the host (the generic kernel runs them).
+#include <array>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <set>
+
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+#include "fpf_wave_common.h"
+
+namespace fpf {
+
+namespace {
+constexpr int CW = 8;                  // wavefronts per workgroup
+constexpr int CC = 4;                  // slots per lane
+constexpr int CL = 64 * CW;            // lanes (= threads) per workgroup
+constexpr int CBD = 6;                 // block-chain depth resolved from registers (the host checks)
+constexpr int SPIN = 1 << 21;          // polls before a wait gives up
+constexpr int AH = 48;                 // area header: backward totals [2][8], forward [2][8], final [2][8]
+
+__device__ __forceinline__ int ci_store_b(unsigned x) { return (int)((x >> 4) & 16383u) - 1; }
+__device__ __forceinline__ int ci_last(unsigned x) { return (int)(x >> 18); }
+__device__ __forceinline__ void ast(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ald(double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// thread 0 polls *w until pred(*w) (or the error word is set, or the polls run
+// out: then it sets the error word); the verdict is broadcast through LDS
+template <typename Pred>
+__device__ __forceinline__ bool coop_poll(unsigned *w, unsigned *err, int *flag, Pred pred) {
+    if (threadIdx.x == 0) {
+        int ok = 0;
+        for (int i = 0; i < SPIN; ++i) {
+            if (pred(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                ok = 1;
+                break;
+            }
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = ok;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+// every thread's area stores complete, then one arrival; wait: until both
+// members have arrived `target` times in total
+__device__ __forceinline__ bool coop_arrive(unsigned *cnt, unsigned target, unsigned *err, int *flag, bool wait) {
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!wait) return true;
+    return coop_poll(cnt, err, flag, [=](unsigned c) { return c >= target; });
+}
+
+// One exchange of a scan (the owned entries are in X as this workgroup's local
+// prefix values): the owned range of the index space [0, split) | [split, n) out
+// to the area xa [3][n] (one coalesced pass), the workgroup total to at[8 g ..];
+// after both arrivals the partner's range into X, workgroup 1's entries (on
+// either side) plus workgroup 0's total tt[0..5] (tt[6..11]: workgroup 1's)
+__device__ __forceinline__ bool coop_exchange(double2 *X, int XC, double *xa, int n, int split, int g,
+                                              const double (&tot6)[6], double *at, double *tt, unsigned *cnt,
+                                              unsigned target, unsigned *err, int *flag) {
+    const int tid = threadIdx.x;
+    __syncthreads();   // (the owned entries are in X)
+    const int lo = g ? split : 0, own = g ? n - split : split;
+    for (int i = tid; i < 3 * own; i += CL) {
+        const int p = i / own, e = lo + i - p * own;
+        const double2 x = X[p * XC + e];
+        ast(xa + 2 * (p * n + e), x.x);
+        ast(xa + 2 * (p * n + e) + 1, x.y);
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ast(at + 8 * g + q, tot6[q]);
+    }
+    if (!coop_arrive(cnt, target, err, flag, true)) return false;
+    if (tid < 12) tt[tid] = ald(at + (tid < 6 ? tid : tid + 2));
+    __syncthreads();
+    const int plo = g ? 0 : split, pn = g ? split : n - split;
+    for (int i = tid; i < 3 * pn; i += CL) {
+        const int p = i / pn, e = plo + i - p * pn;
+        double re = ald(xa + 2 * (p * n + e)), im = ald(xa + 2 * (p * n + e) + 1);
+        if (!g) {   // the partner is workgroup 1
+            re += tt[2 * p];
+            im += tt[2 * p + 1];
+        }
+        X[p * XC + e] = make_double2(re, im);
+    }
+    if (g) {
+        for (int i = tid; i < 3 * own; i += CL) {
+            const int p = i / own, e = lo + i - p * own;
+            const double2 x = X[p * XC + e];
+            X[p * XC + e] = make_double2(x.x + tt[2 * p], x.y + tt[2 * p + 1]);
+        }
+    }
+    __syncthreads();
+    return true;
+}
+}  // namespace
+
+template <bool FULL>
+__global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
+    extern __shared__ double2 lds[];
+    if (o.skip && *o.skip) return;   // (the multi-area solve's device-side stop)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int b = blockIdx.x, g = (b >> 3) & 1;
+    const int s = ((b >> 4) << 3) | (b & 7);   // this pair's scenario (members b, b + 8)
+    if (s >= B) return;                        // (both members of a padding pair)
+    const int nblk = f.nblk, nn = f.nn, nl = f.nl, XC = f.ncomp + 1, nbc = f.nb_c, nfc = f.nf_c;
+    const int ntz = f.temp_sym ? 4 : 9;
+    constexpr int PS = CC * CL + 1;   // Sld rows: slot c L + tid (row C L = 0)
+    // LDS: Zl per code | Sld [3][PS] (this workgroup's slots) | X [3][XC] (the whole
+    // gathered array; entry XC - 1 = 0) | block offsets [3][nblk] | V0 [3] (+1) |
+    // wave totals [2][W][8] | exchanged totals [16] | flag
+    double2 *const zc = lds;
+    double2 *const stg = zc + f.ncode * ntz;
+    double2 *const X = stg + 3 * PS;
+    double2 *const OFF = X + 3 * XC;
+    double2 *const V0S = OFF + 3 * nblk;
+    double *const wtb = (double *)(V0S + 4);
+    double *const wtf = wtb + 8 * CW;
+    double *const tt = wtf + 8 * CW;            // [24] the exchanged totals (backward 0..11, forward 12..17)
+    int *const flag = (int *)(tt + 24);
+    __shared__ int last_wg;
+
+    const int slot = s % f.coop_nslot;
+    double *const A = f.xch + (size_t)slot * f.coop_area;
+    double *const XB = A + AH, *const XF = XB + 6 * nbc;
+    unsigned *const cnt = f.xsync + slot, *const gen = f.xsync + f.coop_nslot + slot;
+    unsigned *const err = f.xsync + 2 * f.coop_nslot;
+    const int so = g * CC * CL;   // this workgroup's slot tables
+
+    // ---- this workgroup's slots: their loads P/Q (column s of pq, or its block in
+    // the scenario-major layout) into Sld scaled by 1/(bkva/3) (DPF_return7.cpp:46-50)
+    unsigned si[CC];
+    int i2[CC], bk[CC], cz[CC];
+    double lg[CC];
+    double sabs = 0.0;   // the guard record: sum |S_k|_1 over the slots
+    {
+        const double inv_s3 = 1.0 / f.s3;
+        int r[CC];
+        double x[CC][6];
+#pragma unroll
+        for (int c = 0; c < CC; ++c) r[c] = f.slot_row[so + c * CL + tid];
+#pragma unroll
+        for (int c = 0; c < CC; ++c)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const size_t e = o.smaj ? (size_t)s * 6 * nl + (size_t)q * nl + (r[c] < 0 ? 0 : r[c])
+                                        : ((size_t)q * nl + (r[c] < 0 ? 0 : r[c])) * B + s;
+                x[c][q] = __builtin_nontemporal_load(pq + e);
+            }
+#pragma unroll
+        for (int c = 0; c < CC; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx v = r[c] < 0 ? mk(0.0, 0.0) : mk(x[c][2 * p] * inv_s3, x[c][2 * p + 1] * inv_s3);
+                stx(stg, p * PS + c * CL + tid, v);
+                sabs += fabs(v.re) + fabs(v.im);
+            }
+#pragma unroll
+        for (int c = 0; c < CC; ++c) {
+            si[c] = (unsigned)f.slot_info[so + c * CL + tid];
+            i2[c] = f.slot_info2[so + c * CL + tid] - 1;
+            bk[c] = f.slot_blk[so + c * CL + tid];
+            cz[c] = f.slot_code[so + c * CL + tid] * ntz;
+            lg[c] = f.slot_lng[so + c * CL + tid];
+        }
+    }
+    for (int i = tid; i < f.ncode * ntz; i += CL) zc[i] = ld_global2(f.code_z, i);
+    if (tid < 3) {
+        X[tid * XC + XC - 1] = make_double2(0.0, 0.0);
+        double2 v0 = tid == 0 ? make_double2(f.V0[0], f.V0[1])
+                              : (tid == 1 ? make_double2(f.V0[2], f.V0[3]) : make_double2(f.V0[4], f.V0[5]));
+        if (o.vsrc) v0 = make_double2(o.vsrc[(size_t)(2 * tid) * B + s], o.vsrc[(size_t)(2 * tid + 1) * B + s]);
+        V0S[tid] = v0;
+    }
+    // this thread's block chain (thread b < nblk resolves block b), two indices per register
+    int bp[CBD];
+#pragma unroll
+    for (int j = 0; j < CBD; ++j) {
+        const bool ok = j < f.bdepth && tid < nblk;
+        bp[j] = ok ? f.blk_pairs[(2 * j) * nblk + tid] | (f.blk_pairs[(2 * j + 1) * nblk + tid] << 16)
+                   : (XC - 1) | ((XC - 1) << 16);
+    }
+    {
+        const double a = seg_incl<64>(sabs);
+        if (lane == 63) wtb[8 * wv + 7] = a;
+    }
+    // the exchange area: free once its previous scenario (s - nslot) has released it
+    const unsigned want = (unsigned)(s / f.coop_nslot);
+    bool alive = coop_poll(gen, err, flag, [=](unsigned v) { return v == want; });
+
+    cx v[CC][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const cx v0 = ldx(V0S, p);
+#pragma unroll
+        for (int c = 0; c < CC; ++c) v[c][p] = v0;   // V(0..Nl-1) = V0  (:92-96)
+    }
+    if (o.vinit_re) {   // the multi-area solve's warm start
+#pragma unroll
+        for (int c = 0; c < CC; ++c)
+            if ((si[c] >> 3) & 1) {
+                const int k = f.slot_node[so + c * CL + tid];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    v[c][p] = mk(o.vinit_re[((size_t)p * nn + k) * B + s], o.vinit_im[((size_t)p * nn + k) * B + s]);
+            }
+    }
+    cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    int it = 0;
+    bool conv = false;
+    double dmin = INFINITY, err2_last = 0.0;
+    unsigned arrivals = 0;   // this member's arrivals (both members: the same sequence)
+    for (; alive; ++it) {
+        // ---- load currents (:106-130)
+        cx il[CC][3], ib[CC][3];
+#pragma unroll
+        for (int c = 0; c < CC; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<false>(ldx(stg, p * PS + c * CL + tid), v[c][p]);
+
+        // ---- backward sweep (:134-160): this workgroup's prefix scan of IL
+        double sc6[6], pre[6], tot6[6];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = il[0][p];
+            ib[0][p] = acc;
+#pragma unroll
+            for (int c = 1; c < CC; ++c) { acc = cadd(acc, il[c][p]); ib[c][p] = acc; }
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<64>(sc6);
+        if (lane == 63) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) wtb[8 * wv + q] = sc6[q];
+        }
+        __syncthreads();
+        wave_prefix<CW, true>(wtb, wv, lane, pre, tot6);
+        cx exl[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            exl[p] = csub(mk(pre[2 * p] + sc6[2 * p], pre[2 * p + 1] + sc6[2 * p + 1]), ib[CC - 1][p]);
+#pragma unroll
+            for (int c = 0; c < CC; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // this workgroup's Einc
+        }
+        // the owned gathered entries (local values), then the exchange: the whole
+        // backward array in X, workgroup 1's entries carried by workgroup 0's total
+#pragma unroll
+        for (int c = 0; c < CC; ++c) {
+            const int ci = ci_store_b(si[c]);
+            if (ci >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
+            }
+        }
+        arrivals += 2;
+        if (!(alive = coop_exchange(X, XC, XB, nbc, f.nb_split, g, tot6, A, tt, cnt, arrivals, err, flag))) break;
+        cx tot[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            tot[p] = mk(tt[2 * p] + tt[6 + 2 * p], tt[2 * p + 1] + tt[6 + 2 * p + 1]);   // Ib(0), the same on both sides
+            // Ib = Einc[last] - Eexc; Eexc of slot c = Einc of slot c-1, of slot 0 the lane's prefix
+            const cx carry = g ? mk(tt[2 * p], tt[2 * p + 1]) : mk(0.0, 0.0);
+            cx eprev = cadd(exl[p], carry);
+#pragma unroll
+            for (int c = 0; c < CC; ++c) {
+                const cx e = cadd(ib[c][p], carry);
+                ib[c][p] = csub(ldx(X, p * XC + ci_last(si[c])), eprev);
+                eprev = e;
+            }
+        }
+
+        // ---- convergence on the substation branch (:199-217), compared as squares
+        double err2 = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const double dr = tot[p].re - ibo[p].re, di = tot[p].im - ibo[p].im;
+            err2 = fmax(err2, fma(dr, dr, di * di));
+            ibo[p] = tot[p];
+        }
+        conv = __builtin_amdgcn_readfirstlane(err2 < f.eps * f.eps ? 1 : 0) != 0;
+        const bool fin = conv || it == f.mxitr - 1;
+        if (fin) err2_last = err2;
+        if (o.flag_count) {   // the convergence guard (fpf_wblk.hip)
+            const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
+            if (dd <= 0x1p-9 * e2) dmin = fmin(dmin, dd);
+        }
+
+        // ---- branch drops lng * (Ib . Zl) (:163-178)
+        cx gd[CC][3];
+        double lp[3] = {0.0, 0.0, 0.0};
+        if (f.temp_sym) {
+#pragma unroll
+            for (int c = 0; c < CC; ++c) {
+                const cx m = ldx(zc, cz[c] + 3);
+                const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
+                const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx d = ldx(zc, cz[c] + a);
+                    const cx bb = ib[c][a];
+                    gd[c][a] = mk(lg[c] * fma(d.re, bb.re, fma(-d.im, bb.im, ms.re)),
+                                  lg[c] * fma(d.re, bb.im, fma(d.im, bb.re, ms.im)));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CC; ++c) {
+                cx tm[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) tm[j] = ldx(zc, cz[c] + j);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx t = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
+                    gd[c][a] = mk(lg[c] * t.re, lg[c] * t.im);
+                }
+            }
+        }
+        if (fin) {   // Re(drop . conj(Ib)) per phase: the VVC loss (fpf_wave.hip: the loss identity)
+#pragma unroll
+            for (int c = 0; c < CC; ++c)
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    lp[a] = fma(gd[c][a].re, ib[c][a].re, fma(gd[c][a].im, ib[c][a].im, lp[a]));
+        }
+
+        // ---- forward sweep (:163-195): V = V0 - A, A = Ginc + off(block)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = gd[0][p];
+#pragma unroll
+            for (int c = 1; c < CC; ++c) { acc = cadd(acc, gd[c][p]); gd[c][p] = acc; }
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<64>(sc6);
+        if (lane == 63) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) wtf[8 * wv + q] = sc6[q];
+        }
+        __syncthreads();
+        wave_prefix<CW, true>(wtf, wv, lane, pre, tot6);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx ex = csub(mk(pre[2 * p] + sc6[2 * p], pre[2 * p + 1] + sc6[2 * p + 1]), gd[CC - 1][p]);
+#pragma unroll
+            for (int c = 0; c < CC; ++c) gd[c][p] = cadd(ex, gd[c][p]);   // this workgroup's Ginc
+        }
+#pragma unroll
+        for (int c = 0; c < CC; ++c) {
+            if (i2[c] >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + i2[c], gd[c][p]);
+            }
+        }
+        arrivals += 2;
+        if (!(alive = coop_exchange(X, XC, XF, nfc, f.nf_split, g, tot6, A + 16, tt + 12, cnt, arrivals, err, flag)))
+            break;
+        // block offsets, one thread per block: V0 - off(b), off(b) = sum over b's
+        // block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
+        if (tid < nblk) {
+            cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+#pragma unroll
+            for (int j = 0; j < CBD; ++j) {
+                if (j < f.bdepth) {   // uniform; levels past a chain's depth read the zero entry
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
+                }
+                if (j & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx carry = g ? mk(tt[12 + 2 * p], tt[12 + 2 * p + 1]) : mk(0.0, 0.0);
+#pragma unroll
+            for (int c = 0; c < CC; ++c) v[c][p] = csub(ldx(OFF, p * nblk + bk[c]), cadd(gd[c][p], carry));
+        }
+
+        if (fin) {
+            // ---- the last sweep: V (and the full outputs) of this workgroup's nodes
+            // straight from registers, its part of the loss and of the V extremes
+            double mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+            for (int c = 0; c < CC; ++c) {
+                if ((si[c] >> 3) & 1) {
+                    const int k = f.slot_node[so + c * CL + tid];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        if (FULL) {
+                            emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                        } else {
+                            const size_t o3 = o.smaj ? (size_t)s * 3 * nn + (size_t)p * nn + k : ((size_t)p * nn + k) * B + s;
+                            if (o.v_re) o.v_re[o3] = v[c][p].re;
+                            if (o.v_im) o.v_im[o3] = v[c][p].im;
+                        }
+                        const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
+                        mn = fmin(mn, m2);
+                        mx = fmax(mx, m2);
+                    }
+                }
+            }
+            const double x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
+            mn = seg_reduce_min<64>(mn);
+            mx = seg_reduce_max<64>(mx);
+            if (lane == 63) {
+                wtb[8 * wv + 6] = x;
+                wtf[8 * wv + 6] = mn;
+                wtf[8 * wv + 7] = mx;
+            }
+            break;
+        }
+    }
+    __syncthreads();
+
+    // ---- the pair's results: workgroup 1 hands its sums over and leaves;
+    // workgroup 0 writes the per-scenario results, releases the area, and joins
+    // the fused batch aggregate [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over,
+    // n_under, n_scen] (one ticket per scenario, the last folds in scenario order)
+    if (g == 1) {
+        if (alive && tid == 0) {
+            double x = 0.0, mn = INFINITY, mx = -INFINITY, sa = 0.0;
+#pragma unroll
+            for (int w = 0; w < CW; ++w) {
+                x += wtb[8 * w + 6];
+                sa += wtb[8 * w + 7];
+                mn = fmin(mn, wtf[8 * w + 6]);
+                mx = fmax(mx, wtf[8 * w + 7]);
+            }
+            ast(A + 40, x);
+            ast(A + 41, mn);
+            ast(A + 42, mx);
+            ast(A + 43, sa);
+        }
+        if (alive) coop_arrive(cnt, 0, err, flag, false);
+        return;
+    }
+    if (alive) alive = coop_arrive(cnt, arrivals + 2, err, flag, true);
+    const bool agg = o.agg != nullptr;
+    if (tid == 0) {
+        double x = 0.0, mn = INFINITY, mx = -INFINITY, sa = 0.0;
+#pragma unroll
+        for (int w = 0; w < CW; ++w) {
+            x += wtb[8 * w + 6];
+            sa += wtb[8 * w + 7];
+            mn = fmin(mn, wtf[8 * w + 6]);
+            mx = fmax(mx, wtf[8 * w + 7]);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {   // the substation row
+            const cx v0p = ldx(V0S, p);
+            const double m2 = fma(v0p.re, v0p.re, v0p.im * v0p.im);
+            mn = fmin(mn, m2);
+            mx = fmax(mx, m2);
+        }
+        if (alive) {
+            x += ald(A + 40);
+            mn = fmin(mn, ald(A + 41));
+            mx = fmax(mx, ald(A + 42));
+            sa += ald(A + 43);
+            // release the area: the count back to 0, then the generation
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(gen, want + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            conv = false;   // an exchange gave up (the error word is set): status 1
+        }
+        const double m2min = mn;
+        x *= f.s3;
+        mn = sqrt(mn);
+        mx = sqrt(mx);
+        if (o.iters) o.iters[s] = it + 1;
+        if (o.status) o.status[s] = conv ? 0 : 1;
+        if (o.loss) o.loss[s] = x;
+        if (o.errmx) o.errmx[s] = sqrt(err2_last);
+        if (o.flag_count) {
+            // the guard band (fpf_wblk.hip), over both workgroups' loads
+            bool near = false;
+            if (dmin < INFINITY) {
+                const double tau = 1.25 * f.guard_k * 1.4142135623730951 * sa / sqrt(m2min);
+                near = dmin <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
+            }
+            if (o.guard) o.guard[s] = near ? 1 : 0;
+            if (near) guard_flag(o, s, nullptr, nullptr);
+        } else if (o.guard) {
+            o.guard[s] = 0;
+        }
+        if (o.vmin) o.vmin[s] = mn;
+        if (o.vmax) o.vmax[s] = mx;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx v0p = ldx(V0S, p);
+            // substation row 0: V0, Ib(0) = the last sweep's total, no load
+            if (FULL) {
+                emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0p, mk(0, 0), ibo[p]);
+            } else {
+                const size_t o3 = o.smaj ? (size_t)s * 3 * nn + (size_t)p * nn : (size_t)p * nn * B + s;
+                if (o.v_re) o.v_re[o3] = v0p.re;
+                if (o.v_im) o.v_im[o3] = v0p.im;
+            }
+            if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
+                const cx sbv = cmul(cmul(v0p, mk(f.s3, 0.0)), cconj(ibo[p]));
+                o.s_in[(size_t)(2 * p) * B + s] = sbv.re;
+                o.s_in[(size_t)(2 * p + 1) * B + s] = sbv.im;
+            }
+        }
+        if (agg) {
+            const double part[8] = {conv ? x : 0.0, conv ? mn : INFINITY, conv ? mx : -INFINITY, conv ? 1.0 : 0.0,
+                                    conv ? 0.0 : 1.0, conv && mx > f.ub_v ? 1.0 : 0.0, conv && mn < f.lb_v ? 1.0 : 0.0,
+                                    1.0};
+            double *dst = o.partials + 8 * (size_t)s;
+            for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_wg = t == (unsigned)B - 1u;
+        }
+    }
+    if (agg) {
+        __syncthreads();
+        if (last_wg) {
+            // thread i folds scenarios i, i + CL, ... in order, then a fixed tree
+            double a[8] = {0, INFINITY, -INFINITY, 0, 0, 0, 0, 0};
+            for (int j = tid; j < B; j += CL) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const double r = __hip_atomic_load(o.partials + 8 * (size_t)j + q, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                    a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
+                }
+            }
+            double *sh = (double *)stg;   // [8][CL] (Sld is dead; wcoop_lds_bytes covers it)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sh[q * CL + tid] = a[q];
+            __syncthreads();
+            for (int w = CL / 2; w > 0; w >>= 1) {
+                if (tid < w) {
+                    sh[0 * CL + tid] += sh[0 * CL + tid + w];
+                    sh[1 * CL + tid] = fmin(sh[1 * CL + tid], sh[1 * CL + tid + w]);
+                    sh[2 * CL + tid] = fmax(sh[2 * CL + tid], sh[2 * CL + tid + w]);
+#pragma unroll
+                    for (int q = 3; q < 8; ++q) sh[q * CL + tid] += sh[q * CL + tid + w];
+                }
+                __syncthreads();
+            }
+            if (tid < 8) o.agg[tid] = sh[tid * CL];
+            if (tid == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0 && o.flag_out)
+                *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+size_t wcoop_lds_bytes(const WaveDev &w) {
+    const size_t ntz = w.temp_sym ? 4 : 9, xc = (size_t)w.ncomp + 1;
+    return 16 * ((size_t)w.ncode * ntz + 3 * ((size_t)CC * CL + 1) + 3 * xc + 3 * (size_t)w.nblk + 4) +
+           2 * 8 * CW * 8 + 24 * 8 + 16;
+}
+
+hipError_t launch_wcoop(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
+    if (w.coop != 2 || w.wps != CW || w.C != CC || w.nblk > CL || w.bdepth > CBD || !w.xch || !w.xsync)
+        return hipErrorInvalidValue;
+    const bool full = o.vpolar || o.pqb || o.pql;
+    auto k = full ? dpf_wcoop_kernel<true> : dpf_wcoop_kernel<false>;
+    static std::mutex mu;
+    static std::set<std::array<int, 2>> attr_done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        const std::array<int, 2> key = {dev, (int)full};
+        if (!attr_done.count(key)) {
+            hipFuncAttributes fa{};
+            hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - (int)fa.sharedSizeBytes);
+            if (e != hipSuccess) return e;
+            attr_done.insert(key);
+        }
+    }
+    // arrival counts, generations and the error word start at 0 every launch
+    hipError_t e = hipMemsetAsync(w.xsync, 0, sizeof(unsigned) * (2 * (size_t)w.coop_nslot + 16), st);
+    if (e != hipSuccess) return e;
+    if (n_scen <= 0) return hipSuccess;
+    const unsigned grid = 16u * (unsigned)((n_scen + 7) / 8);   // scenario t: workgroups 16 (t / 8) + (t % 8) + {0, 8}
+    hipLaunchKernelGGL(k, dim3(grid), dim3(CL), wcoop_lds_bytes(w), st, w, n_scen, pq, o);
+    return hipGetLastError();
+}
+
+}  // namespace fpf

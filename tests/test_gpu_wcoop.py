@@ -1,0 +1,139 @@
+"""The paired wave-block kernel (fpf_wcoop.hip; fast mode on feeders of
+2049..4096 branches, one scenario on two workgroups that exchange their scan
+values every sweep) against the oracle and the exact generic kernel.
+
+Bar (north_star, as for the other fast kernels): V within 1e-10 relative and
+identical iteration counts and status on every scenario; PQb / PQL / Vpolar at
+1e-9 (angles 1e-8 deg), loss 1e-8, Vmin/Vmax 1e-10.  The reference:
+DPF_return7.cpp:8-263 (any Nl) and the VVC reductions (VoltVarCtrl.cpp:1152-1161,
+1201-1207), restated by oracle/ref_dpf.c.
+"""
+import numpy as np
+import pytest
+
+from freedm_amd import feeder as F
+from test_gpu_wblk import _check_full, _vrel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [2100, 3000, 4096])
+def test_wcoop_matches_oracle(n):
+    """Full outputs (the FULL variant) against the oracle, scenario by scenario;
+    the kernel is the paired one (the plan's 2 x 8 wavefronts)."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(n, n)
+    pq = F.scenario_loads(f, np.arange(24))
+    pf = PowerFlow(f)
+    assert pf.kernel == "wave" and pf.info["tile"] == 1
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (c["status"] == 0).all()
+    _check_full(r, c)
+
+
+def test_wcoop_mixed_sweeps_both_layouts():
+    """Loads scaled 0.05x .. 40x on the 4096-bus feeder: different sweep counts
+    and non-convergent scenarios (status 1 after 20 sweeps) in one batch, the
+    light outputs (V + scalars, device buffers) in both batch layouts, against
+    the oracle."""
+    import torch
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(4096, 4096)
+    B = 40
+    pq = np.ascontiguousarray(F.scenario_loads(f, np.arange(B)) * np.geomspace(0.05, 40.0, B)[None, None, :])
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (c["status"] == 1).any() and len(set(c["iters"][c["status"] == 0])) >= 3
+    conv = c["status"] == 0
+    dev = torch.device("cuda:0")
+    for layout in (0, 1):
+        pf = PowerFlow(f, layout=layout)
+        x = pq if layout == 0 else np.ascontiguousarray(pq.transpose(2, 0, 1))
+        sh = (3, pf.nn, B) if layout == 0 else (B, 3, pf.nn)
+        o = {"v_re": torch.empty(sh, dtype=torch.float64, device=dev),
+             "v_im": torch.empty(sh, dtype=torch.float64, device=dev),
+             "iters": torch.empty(B, dtype=torch.int32, device=dev),
+             "status": torch.empty(B, dtype=torch.int8, device=dev),
+             "loss": torch.empty(B, dtype=torch.float64, device=dev),
+             "vmin": torch.empty(B, dtype=torch.float64, device=dev),
+             "vmax": torch.empty(B, dtype=torch.float64, device=dev)}
+        pf.solve_device(torch.from_numpy(x).to(dev), o)
+        torch.cuda.synchronize()
+        r = {k: v.cpu().numpy() for k, v in o.items()}
+        vr, vi = (r["v_re"], r["v_im"]) if layout == 0 else (np.moveaxis(r["v_re"], 0, -1), np.moveaxis(r["v_im"], 0, -1))
+        assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+        e = _vrel(vr[..., conv], vi[..., conv], c["V_re"][..., conv], c["V_im"][..., conv])
+        print(f"layout {layout}: max V rel err {e:.3e}, sweeps {c['iters'][conv].min()}..{c['iters'][conv].max()}")
+        assert e <= 1e-10
+        np.testing.assert_allclose(r["vmin"][conv], c["vmin"][conv], rtol=1e-10)
+        np.testing.assert_allclose(r["vmax"][conv], c["vmax"][conv], rtol=1e-10)
+        np.testing.assert_allclose(r["loss"][conv], c["loss"][conv], rtol=1e-8)
+        pf.close()
+
+
+def test_wcoop_16384_scenarios():
+    """16 384 scenarios of the 4096-bus feeder in one launch (light outputs and
+    the fused aggregate; every exchange area reused 16 times): every scenario
+    against the exact generic kernel on the same device inputs (iteration counts
+    and status identical, V 1e-10, loss 1e-8, Vmin/Vmax 1e-10, the aggregate's
+    counts equal) and a strided sample against the oracle."""
+    import torch
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(4096, 4096)
+    B, NB = 16384, 512
+    base = F.scenario_loads(f, np.arange(NB), seed=16384)
+    dev = torch.device("cuda:0")
+    s = np.arange(B, dtype=np.int64)
+    mult = 0.9 + 0.2 * (((s * 2654435761) % 1000) / 1000.0)
+    d_pq = torch.from_numpy(base).to(dev)[:, :, torch.from_numpy(s % NB).to(dev)] * torch.from_numpy(mult).to(dev)
+
+    def run(pf):
+        nn = pf.nn
+        out = {"v_re": torch.empty((3, nn, B), dtype=torch.float64, device=dev),
+               "v_im": torch.empty((3, nn, B), dtype=torch.float64, device=dev),
+               "iters": torch.empty(B, dtype=torch.int32, device=dev),
+               "status": torch.empty(B, dtype=torch.int8, device=dev),
+               "loss": torch.empty(B, dtype=torch.float64, device=dev),
+               "vmin": torch.empty(B, dtype=torch.float64, device=dev),
+               "vmax": torch.empty(B, dtype=torch.float64, device=dev)}
+        agg = torch.zeros(8, dtype=torch.float64, device=dev)
+        pf.solve_device(d_pq, out, agg=agg)
+        torch.cuda.synchronize()
+        return out, agg.cpu().numpy()
+
+    fast = PowerFlow(f, device=0)
+    assert fast.kernel == "wave"
+    w, wa = run(fast)
+    assert wa[7] == B and wa[3] == B
+    idx = np.arange(0, B, 509)
+    ti = torch.from_numpy(idx).to(dev)
+    pq_s = np.ascontiguousarray(base[:, :, idx % NB] * mult[idx])
+    c = O.dpf_batch(f.Dl, f.Z, pq_s, nthreads=8)
+    assert (w["iters"][ti].cpu().numpy() == c["iters"]).all() and (w["status"][ti].cpu().numpy() == c["status"]).all()
+    assert _vrel(w["v_re"][:, :, ti].cpu().numpy(), w["v_im"][:, :, ti].cpu().numpy(), c["V_re"], c["V_im"]) <= 1e-10
+    np.testing.assert_allclose(w["loss"][ti].cpu().numpy(), c["loss"], rtol=1e-8)
+    exact = PowerFlow(f, device=0, exact=1)
+    assert exact.kernel == "generic"
+    g, ga = run(exact)
+    assert torch.equal(w["iters"], g["iters"]) and torch.equal(w["status"], g["status"])
+    a = w["v_re"] + 1j * w["v_im"]
+    b = g["v_re"] + 1j * g["v_im"]
+    assert float(((a - b).abs() / b.abs()).max()) <= 1e-10
+    del a, b
+    assert float(((w["loss"] - g["loss"]).abs() / g["loss"].abs()).max()) <= 1e-8
+    assert float(((w["vmin"] - g["vmin"]).abs() / g["vmin"]).max()) <= 1e-10
+    assert float(((w["vmax"] - g["vmax"]).abs() / g["vmax"]).max()) <= 1e-10
+    np.testing.assert_array_equal(wa[3:], ga[3:])
+    np.testing.assert_allclose(wa[:3], ga[:3], rtol=1e-8)
+
+
+def test_wcoop_declines_zeroed_phases_and_larger_feeders():
+    """Zeroed phases above 2048 branches and feeders above 4096 branches stay on
+    the generic kernel (bit-identical to the oracle in exact mode, its own tests)."""
+    from freedm_amd import PowerFlow
+    from test_gpu_wblk import _masked_feeder
+    assert PowerFlow(_masked_feeder(3000, 3000)).kernel == "generic"
+    assert PowerFlow(F.synthetic_feeder(4300, 4300)).kernel == "generic"

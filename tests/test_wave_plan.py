@@ -34,18 +34,23 @@ def test_123bus_plan():
     assert p["ncomp"] <= 32 and p["bdepth"] <= 4
 
 
-@pytest.mark.parametrize("n", [9, 34, 65, 200, 257, 300, 700, 1500, 2048, 2100])
+@pytest.mark.parametrize("n", [9, 34, 65, 200, 257, 300, 700, 1500, 2048, 2100, 3000, 4096, 4300])
 def test_plan_sizes(n):
     """Every feeder of at most 256 branches gets a per-wavefront geometry whose
     L x C slots hold its branches; 257..2048 branches the wave-block kernel
     (fpf_wblk.hip: one scenario per workgroup of wpb = 2, 4, 8 wavefronts, C = 4);
-    above that the wave kernels decline."""
+    2049..4096 the paired wave-block kernel (fpf_wcoop.hip: two workgroups of 8
+    wavefronts, C = 4, each holding half of the positions); above that the wave
+    kernels decline."""
     f = demo_feeder() if n == 9 else synthetic_feeder(n, n)
     nb = int((f.Dl[:, 0] != 0).sum())
     p = _plan(f)
-    assert p["ok"] == (1 if nb <= 2048 else 0)
+    assert p["ok"] == (1 if nb <= 4096 else 0)
     if p["ok"] and nb <= 256:
         assert (64 // p["spw"]) * p["C"] >= nb and p["lds"] <= 159 * 1024
+    elif p["ok"] and nb > 2048:
+        assert (p["spw"], p["C"], p["wpb"]) == (1, 4, 8)
+        assert 2 * 64 * 8 * 4 >= nb and p["lds"] <= 159 * 1024
     elif p["ok"]:
         assert p["spw"] == 1 and p["C"] == 4 and p["wpb"] in (2, 4, 8)
         assert 64 * p["wpb"] * 4 >= nb > 64 * (p["wpb"] // 2) * 4
