@@ -327,6 +327,55 @@ def _copy_bandwidth(torch, dev, nbytes=1 << 30, reps=10):
     return gbs
 
 
+def _wave_kernel_name(nb: int) -> str:
+    """The fast-mode kernel of a feeder of nb branches: the per-wavefront wave
+    kernel (<= 256), the wave-block kernel (257..2048), the paired wave-block
+    kernel (2049..4096; fpf_wcoop.hip)."""
+    return "dpf_wave_kernel" if nb <= 256 else ("dpf_wblk_kernel" if nb <= 2048 else "dpf_wcoop_kernel")
+
+
+def _diag_4096(torch, local, stream, dev):
+    """Diagnostic leg: a 4096-bus synthetic feeder x 16 384 scenarios (scenario
+    major, 512 seeded scenarios x a per-scenario load multiplier) on the paired
+    wave-block kernel, beside the exact generic kernel on the same device inputs
+    (the only other kernel that solves feeders of more than 2048 branches):
+    launch times, the state-resident roofline fraction, and the fast kernel's
+    agreement with the exact one (iteration counts, max V relative difference)."""
+    from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
+    f = synthetic_feeder(4096, 4096)
+    B = 16384
+    base = torch.from_numpy(scenario_loads(f, np.arange(512), seed=16384)).to(dev)
+    ids = torch.arange(B, device=dev)
+    mult = 0.9 + 0.2 * ((ids * 2654435761) % 1000).double() / 1000.0
+    d = (base[:, :, ids % 512] * mult).permute(2, 0, 1).contiguous()
+    del base
+    out = {}
+    for name, exact in (("fast", 0), ("exact", 1)):
+        pf = PowerFlow(f, device=local, exact=exact, layout=1)
+        pf.reserve(B)
+        ms, o = _kernel_ms(torch, pf, d, B, 3, 1, stream, dev)
+        out[name] = (ms, o, pf.kernel, pf.info["nb"], pf.nn)
+        pf.close()
+    (msf, of, kf, nb, nn), (mse, oe, ke, _, _) = out["fast"], out["exact"]
+    a = of["v_re"] + 1j * of["v_im"]
+    b = oe["v_re"] + 1j * oe["v_im"]
+    vrel = float(((a - b).abs() / b.abs()).max().item())
+    del a, b
+    bpa = bytes_alg_per_scenario(nb, nn)
+    conv = int((of["status"] == 0).sum().item())
+    return {"workload": f"diagnostic: {nn}-bus synthetic feeder, {B} scenarios per launch (scenario major)",
+            "kernel": _wave_kernel_name(nb) if kf == "wave" else kf, "kernel_ms": msf,
+            "converged_scenarios_per_s": conv / (msf / 1e3),
+            "roofline_frac": bpa * B / (msf / 1e3) / 1e9 / HBM_PEAK_GBS, "bytes_alg_per_scenario": bpa,
+            "mean_sweeps": float(of["iters"].double().mean().item()),
+            "exact_kernel": ke, "exact_kernel_ms": mse, "speedup_vs_exact": mse / msf,
+            "iters_equal_exact": bool(torch.equal(of["iters"], oe["iters"])),
+            "status_equal_exact": bool(torch.equal(of["status"], oe["status"])),
+            "max_v_rel_diff_vs_exact": vrel,
+            "note": "tests/test_gpu_wcoop.py checks the same batch against the oracle (strided sample) and the "
+                    "exact kernel (every scenario)"}
+
+
 def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
     """Average launch time (HIP events on the launch stream) of `steps`
     back-to-back solves of the device batch d_pq, plus the iterations."""
@@ -490,7 +539,7 @@ def main():
     # wave-block kernel (257..2048, one scenario per workgroup), both with the
     # state on chip; exact mode the tiled or the generic kernel
     kname = {"tiled": "fpf_rtc_tiled" if pf.info["specialized"] else "dpf_tiled_kernel",
-             "wave": "dpf_wave_kernel" if nb <= 256 else "dpf_wblk_kernel", "generic": "dpf_generic3_kernel"}[pf.kernel]
+             "wave": _wave_kernel_name(nb), "generic": "dpf_generic3_kernel"}[pf.kernel]
     if pf.kernel == "generic":
         # the state streams through HBM every sweep (SURVEY 8(d) config 3 model)
         bytes_launch = bytes_alg_streaming(nb, nn, k_sum / args.steps, B)
@@ -602,6 +651,8 @@ def main():
                     pf3.info["nb"], pf3.nn, float(o3["iters"].double().mean().item()), 1))}
             del d3, o3
             pf3.close()
+            # feeders of 2049..4096 branches: the paired wave-block kernel
+            res["diag_4096bus"] = _diag_4096(torch, local, stream, dev)
             copy = _copy_bandwidth(torch, dev)
             res["hbm_copy_check"] = {"device_copy_gbs": copy, "spec_gbs": HBM_PEAK_GBS,
                                      "copy_frac_of_spec": copy / HBM_PEAK_GBS,

@@ -87,13 +87,28 @@ __device__ __forceinline__ bool coop_arrive(unsigned *cnt, unsigned target, unsi
     return coop_poll(cnt, err, flag, [=](unsigned c) { return c >= target; });
 }
 
+// The exchange area through a buffer resource: 16-byte sc1 (write-through)
+// stores and sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility: every
+// byte stored sc1, each storing wave waits for its stores before the arrival,
+// every load of the bytes an sc1 load after the poll and a workgroup barrier)
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, int off, double re, double im) {
+    const d2v v = {re, im};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, off, 0, 16);
+}
+__device__ __forceinline__ d2v bld(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
 // One exchange of a scan (the owned entries are in X as this workgroup's local
 // prefix values): the owned range of the index space [0, split) | [split, n) out
-// to the area xa [3][n] (one coalesced pass), the workgroup total to at[8 g ..];
-// after both arrivals the partner's range into X, workgroup 1's entries (on
-// either side) plus workgroup 0's total tt[0..5] (tt[6..11]: workgroup 1's)
-__device__ __forceinline__ bool coop_exchange(double2 *X, int XC, double *xa, int n, int split, int g,
-                                              const double (&tot6)[6], double *at, double *tt, unsigned *cnt,
+// to the area's entries [3][n] complex at byte xoff (one coalesced pass), the
+// workgroup total to the totals [2][8] at byte toff; after both arrivals the
+// partner's range into X, workgroup 1's entries (on either side) plus workgroup
+// 0's total; both totals to tt (T0 re/im per phase, then T1)
+__device__ __forceinline__ bool coop_exchange(double2 *X, int XC, __amdgpu_buffer_rsrc_t r, int xoff, int toff, int n,
+                                              int split, int g, const double (&tot6)[6], double *tt, unsigned *cnt,
                                               unsigned target, unsigned *err, int *flag) {
     const int tid = threadIdx.x;
     __syncthreads();   // (the owned entries are in X)
@@ -101,35 +116,54 @@ __device__ __forceinline__ bool coop_exchange(double2 *X, int XC, double *xa, in
     for (int i = tid; i < 3 * own; i += CL) {
         const int p = i / own, e = lo + i - p * own;
         const double2 x = X[p * XC + e];
-        ast(xa + 2 * (p * n + e), x.x);
-        ast(xa + 2 * (p * n + e) + 1, x.y);
+        bst(r, xoff + 16 * (p * n + e), x.x, x.y);
     }
     if (tid == 0) {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) ast(at + 8 * g + q, tot6[q]);
+        for (int p = 0; p < 3; ++p) bst(r, toff + 64 * g + 16 * p, tot6[2 * p], tot6[2 * p + 1]);
     }
-    if (!coop_arrive(cnt, target, err, flag, true)) return false;
-    if (tid < 12) tt[tid] = ald(at + (tid < 6 ? tid : tid + 2));
-    __syncthreads();
+    // (a wait that gave up reads garbage and the caller finishes the sweep with it:
+    // no early exit in the sweep loop)
+    const bool ok = coop_arrive(cnt, target, err, flag, true);
+    // workgroup 0's total (the carry) loaded beside the entries (every load of a
+    // thread in flight at once: the hand-off costs one load latency)
+    d2v t0[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) t0[p] = bld(r, toff + 16 * p);
+    const d2v tmine = bld(r, toff + 64 * (tid < 6 ? tid / 3 : 0) + 16 * (tid < 6 ? tid % 3 : 0));
     const int plo = g ? 0 : split, pn = g ? split : n - split;
-    for (int i = tid; i < 3 * pn; i += CL) {
-        const int p = i / pn, e = plo + i - p * pn;
-        double re = ald(xa + 2 * (p * n + e)), im = ald(xa + 2 * (p * n + e) + 1);
-        if (!g) {   // the partner is workgroup 1
-            re += tt[2 * p];
-            im += tt[2 * p + 1];
+    constexpr int U = 4;
+    for (int i0 = 0; i0 < 3 * pn; i0 += U * CL) {
+        d2v x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * CL + tid, p = i / pn, e = plo + i - p * pn;
+            x[u] = bld(r, i < 3 * pn ? xoff + 16 * (p * n + e) : toff);
         }
-        X[p * XC + e] = make_double2(re, im);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * CL + tid, p = i / pn, e = plo + i - p * pn;
+            if (i < 3 * pn) {
+                // workgroup 1's entries (the partner's when g = 0) carry workgroup 0's total
+                const d2v c = p == 0 ? t0[0] : (p == 1 ? t0[1] : t0[2]);
+                X[p * XC + e] = g ? make_double2(x[u].x, x[u].y) : make_double2(x[u].x + c.x, x[u].y + c.y);
+            }
+        }
     }
     if (g) {
         for (int i = tid; i < 3 * own; i += CL) {
             const int p = i / own, e = lo + i - p * own;
             const double2 x = X[p * XC + e];
-            X[p * XC + e] = make_double2(x.x + tt[2 * p], x.y + tt[2 * p + 1]);
+            const d2v c = p == 0 ? t0[0] : (p == 1 ? t0[1] : t0[2]);
+            X[p * XC + e] = make_double2(x.x + c.x, x.y + c.y);
         }
     }
+    if (tid < 6) {
+        tt[2 * tid] = tmine.x;
+        tt[2 * tid + 1] = tmine.y;
+    }
     __syncthreads();
-    return true;
+    return ok;
 }
 }  // namespace
 
@@ -160,7 +194,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
 
     const int slot = s % f.coop_nslot;
     double *const A = f.xch + (size_t)slot * f.coop_area;
-    double *const XB = A + AH, *const XF = XB + 6 * nbc;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(A, 0, 8 * f.coop_area, 0x00020000);
     unsigned *const cnt = f.xsync + slot, *const gen = f.xsync + f.coop_nslot + slot;
     unsigned *const err = f.xsync + 2 * f.coop_nslot;
     const int so = g * CC * CL;   // this workgroup's slot tables
@@ -168,8 +202,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
     // ---- this workgroup's slots: their loads P/Q (column s of pq, or its block in
     // the scenario-major layout) into Sld scaled by 1/(bkva/3) (DPF_return7.cpp:46-50)
     unsigned si[CC];
-    int i2[CC], bk[CC], cz[CC];
-    double lg[CC];
+    unsigned sx[CC];   // bits 0-8 block, 9-22 forward index + 1, 23-31 code * ntz (the host checks the widths)
     double sabs = 0.0;   // the guard record: sum |S_k|_1 over the slots
     {
         const double inv_s3 = 1.0 / f.s3;
@@ -196,10 +229,8 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
 #pragma unroll
         for (int c = 0; c < CC; ++c) {
             si[c] = (unsigned)f.slot_info[so + c * CL + tid];
-            i2[c] = f.slot_info2[so + c * CL + tid] - 1;
-            bk[c] = f.slot_blk[so + c * CL + tid];
-            cz[c] = f.slot_code[so + c * CL + tid] * ntz;
-            lg[c] = f.slot_lng[so + c * CL + tid];
+            sx[c] = (unsigned)f.slot_blk[so + c * CL + tid] | ((unsigned)f.slot_info2[so + c * CL + tid] << 9) |
+                    ((unsigned)(f.slot_code[so + c * CL + tid] * ntz) << 23);
         }
     }
     for (int i = tid; i < f.ncode * ntz; i += CL) zc[i] = ld_global2(f.code_z, i);
@@ -292,7 +323,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             }
         }
         arrivals += 2;
-        if (!(alive = coop_exchange(X, XC, XB, nbc, f.nb_split, g, tot6, A, tt, cnt, arrivals, err, flag))) break;
+        alive = coop_exchange(X, XC, rs, 8 * AH, 0, nbc, f.nb_split, g, tot6, tt, cnt, arrivals, err, flag) && alive;
         cx tot[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -317,7 +348,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             ibo[p] = tot[p];
         }
         conv = __builtin_amdgcn_readfirstlane(err2 < f.eps * f.eps ? 1 : 0) != 0;
-        const bool fin = conv || it == f.mxitr - 1;
+        const bool fin = conv || it == f.mxitr - 1 || !alive;   // (!alive: an exchange gave up)
         if (fin) err2_last = err2;
         if (o.flag_count) {   // the convergence guard (fpf_wblk.hip)
             const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
@@ -330,15 +361,17 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         if (f.temp_sym) {
 #pragma unroll
             for (int c = 0; c < CC; ++c) {
-                const cx m = ldx(zc, cz[c] + 3);
+                const int czc = (int)(sx[c] >> 23);
+                const double lgc = f.slot_lng[so + c * CL + tid];
+                const cx m = ldx(zc, czc + 3);
                 const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
                 const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
-                    const cx d = ldx(zc, cz[c] + a);
+                    const cx d = ldx(zc, czc + a);
                     const cx bb = ib[c][a];
-                    gd[c][a] = mk(lg[c] * fma(d.re, bb.re, fma(-d.im, bb.im, ms.re)),
-                                  lg[c] * fma(d.re, bb.im, fma(d.im, bb.re, ms.im)));
+                    gd[c][a] = mk(lgc * fma(d.re, bb.re, fma(-d.im, bb.im, ms.re)),
+                                  lgc * fma(d.re, bb.im, fma(d.im, bb.re, ms.im)));
                 }
             }
         } else {
@@ -346,11 +379,12 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             for (int c = 0; c < CC; ++c) {
                 cx tm[9];
 #pragma unroll
-                for (int j = 0; j < 9; ++j) tm[j] = ldx(zc, cz[c] + j);
+                for (int j = 0; j < 9; ++j) tm[j] = ldx(zc, (int)(sx[c] >> 23) + j);
+                const double lgc = f.slot_lng[so + c * CL + tid];
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
                     const cx t = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
-                    gd[c][a] = mk(lg[c] * t.re, lg[c] * t.im);
+                    gd[c][a] = mk(lgc * t.re, lgc * t.im);
                 }
             }
         }
@@ -386,14 +420,15 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         }
 #pragma unroll
         for (int c = 0; c < CC; ++c) {
-            if (i2[c] >= 0) {
+            const int i2 = (int)((sx[c] >> 9) & 16383u) - 1;
+            if (i2 >= 0) {
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(X, p * XC + i2[c], gd[c][p]);
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + i2, gd[c][p]);
             }
         }
         arrivals += 2;
-        if (!(alive = coop_exchange(X, XC, XF, nfc, f.nf_split, g, tot6, A + 16, tt + 12, cnt, arrivals, err, flag)))
-            break;
+        alive = coop_exchange(X, XC, rs, 8 * AH + 48 * nbc, 128, nfc, f.nf_split, g, tot6, tt + 12, cnt, arrivals, err,
+                              flag) && alive;
         // block offsets, one thread per block: V0 - off(b), off(b) = sum over b's
         // block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
         if (tid < nblk) {
@@ -415,7 +450,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         for (int p = 0; p < 3; ++p) {
             const cx carry = g ? mk(tt[12 + 2 * p], tt[12 + 2 * p + 1]) : mk(0.0, 0.0);
 #pragma unroll
-            for (int c = 0; c < CC; ++c) v[c][p] = csub(ldx(OFF, p * nblk + bk[c]), cadd(gd[c][p], carry));
+            for (int c = 0; c < CC; ++c) v[c][p] = csub(ldx(OFF, p * nblk + (int)(sx[c] & 511u)), cadd(gd[c][p], carry));
         }
 
         if (fin) {
