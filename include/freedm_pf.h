@@ -192,7 +192,9 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
  * serialises them across streams with an event per feeder (each waits for the
  * previous one), so they may be enqueued on different streams.  Other solves on
  * one feeder may overlap across streams only when they run the wave kernels
- * (fast mode, feeders of at most 2048 branches), every per-scenario output they
+ * (fast mode, feeders of at most 2048 branches; the paired kernel of 2049..4096
+ * branches exchanges through areas of the feeder, so its solves share one
+ * stream), every per-scenario output they
  * use is the caller's (NULL outputs fall back to buffers of the feeder) and they
  * produce no aggregate; the generic and tiled kernels' scratch and layout
  * buffers and the guard's flag list belong to the feeder, so any other mix must
@@ -275,7 +277,9 @@ long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
  * wavefronts per workgroup, LDS bytes per workgroup, gathered scan entries,
  * blocks, block-chain depth}.  Feeders of 257..2048 branches get the
  * wave-block kernel's plan: one scenario per workgroup of (wavefronts per
- * workgroup) wavefronts, reported with 1 scenario per wavefront.
+ * workgroup) wavefronts, reported with 1 scenario per wavefront; feeders of
+ * 2049..4096 branches the paired kernel's (one scenario on two such workgroups
+ * of 8 wavefronts, each holding half of the positions; LDS bytes per workgroup).
  * Returns FPF_OK or FPF_ERR_*. */
 int         fpf_feeder_wave_plan(const double *dl, int nl, int ncols,
                                  const double *z, int z_rows, int z_cols,
