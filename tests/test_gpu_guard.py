@@ -44,7 +44,7 @@ def _near_eps(n, n_pairs=8):
     return f, np.ascontiguousarray(np.concatenate([a, b], axis=2)), np.concatenate([ma, mb])
 
 
-@pytest.mark.parametrize("n", [123, 2048])
+@pytest.mark.parametrize("n", [123, 2048, 3000])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_near_eps_iterations_identical(n, layout):
     from freedm_amd import PowerFlow
@@ -116,7 +116,7 @@ def test_near_eps_device_paths(n):
     m.close()
 
 
-@pytest.mark.parametrize("n,B", [(123, 4096), (2048, 256)])
+@pytest.mark.parametrize("n,B", [(123, 4096), (2048, 256), (3000, 128)])
 def test_guard_quiet_on_ordinary_batch(n, B):
     """On an ordinary batch no decision is anywhere near eps: nothing is flagged
     (the fast path runs alone) and errmx equals the oracle's within the band."""

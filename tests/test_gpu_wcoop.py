@@ -137,3 +137,53 @@ def test_wcoop_declines_zeroed_phases_and_larger_feeders():
     from test_gpu_wblk import _masked_feeder
     assert PowerFlow(_masked_feeder(3000, 3000)).kernel == "generic"
     assert PowerFlow(F.synthetic_feeder(4300, 4300)).kernel == "generic"
+
+
+def test_wcoop_areas_equal_monolithic():
+    """The multi-area solve (fpf_areas_*: per-scenario source voltages, the
+    children's source power, warm starts, the device-side stop) on a 3000-bus
+    feeder whose root area needs the paired kernel: V equals the monolithic
+    solve to 1e-10."""
+    from freedm_amd import AreaPowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(3000, 3000)
+    Dl = f.Dl
+    nn = int((Dl[:, 0] != 0).sum()) + 1
+    kids = [[] for _ in range(nn)]
+    for m in range(Dl.shape[0]):
+        if Dl[m, 0] != 0:
+            kids[0 if m == 0 else int(Dl[m, 1])].append(int(Dl[m, 2]))
+    size = np.ones(nn, dtype=np.int64)
+    for k in range(nn - 1, 0, -1):   # (children carry larger bus numbers on the synthetic feeder)
+        for c in kids[k]:
+            size[k] += size[c]
+    # two disjoint subtrees of 80..300 buses as the child areas
+    inside = np.zeros(nn, dtype=bool)
+    tops = []
+    for k in range(nn - 1, 0, -1):
+        if len(tops) < 2 and 80 <= size[k] <= 300 and not inside[k]:
+            st = [k]
+            sub = []
+            while st:
+                x = st.pop()
+                sub.append(x)
+                st.extend(kids[x])
+            if inside[sub].any():
+                continue
+            inside[sub] = True
+            tops.append(k)
+    assert len(tops) == 2
+    node_area = F.subtree_node_areas(f, tops)
+    assert (node_area == 0).sum() > 2049
+    pq = F.scenario_loads(f, np.arange(16))
+    ap = AreaPowerFlow(f, node_area)
+    r = ap.solve(pq, tol=1e-13, max_outer=100)
+    o = O.default_opts()
+    o.eps = 1e-13
+    o.mxitr = 200
+    c = O.dpf_batch(f.Dl, f.Z, pq, opts=o, nthreads=8)
+    assert (c["status"] == 0).all() and (r["status"] == 0).all(), r["note"]
+    v = r["V_re"] + 1j * r["V_im"]
+    vc = c["V_re"] + 1j * c["V_im"]
+    assert float(np.max(np.abs(v - vc) / np.abs(vc))) <= 1e-10
+    np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-8)
