@@ -601,7 +601,13 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     // the wave-block kernel's prefix sums over up to 2048 positions that difference
     // of two ~1 p.u. values misses the 1e-10 bar on the small result (3.8e-10 on the
     // 2048-bus test feeder), so such feeders keep the generic kernel there
-    if (wps && has_rel) return no("wave-block kernel: a live phase below a zeroed one (the generic kernel runs it)");
+    if (coop && has_rel) return no("paired wave-block kernel: a live phase below a zeroed one (the generic kernel runs it)");
+    // with a live phase below a zeroed ancestor m the wave-block kernel's forward
+    // scan is segmented at block heads (block-local path sums, fpf_wblk.hip): V(k)
+    // = A(m) - A(k) is then a difference of two small path sums (the unsegmented
+    // prefix sums over up to 2048 positions lost ~6 digits there: 3.8e-10
+    // relative); block offsets sum the taps' values only
+    const bool seg = wps && !coop && has_rel;
     // positions whose scan values other slots gather, in two index spaces that
     // share one LDS array X (the backward values are dead before the forward
     // ones are stored): backward = subtree ends; forward = taps, the positions
@@ -615,7 +621,7 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     auto needf = [&](int q) { if (cf[q] < 0) cf[q] = nf_c++; };
     for (int b = 1; b < nblk; ++b) {
         needf(pos[par[bfirst[b]]]);
-        needf(pos[bfirst[b]] - 1);
+        if (!seg) needf(pos[bfirst[b]] - 1);
     }
     for (int k = 1; k < nn; ++k)
         for (int p = 0; p < 3; ++p)
@@ -706,14 +712,14 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     int bdepth = 0;
     for (int b = 1; b < nblk; ++b) {
         for (int j = b; j != 0; j = blk[par[bfirst[j]]])
-            chainp[b].push_back({cf[pos[par[bfirst[j]]]], cf[pos[bfirst[j]] - 1]});
+            chainp[b].push_back({cf[pos[par[bfirst[j]]]], seg ? -1 : cf[pos[bfirst[j]] - 1]});
         bdepth = std::max(bdepth, (int)chainp[b].size());
     }
     w.pairs.assign((size_t)std::max(bdepth, 1) * 2 * nblk, ncomp);
     for (int b = 1; b < nblk; ++b)
         for (size_t j = 0; j < chainp[b].size(); ++j) {
             w.pairs[(2 * j) * nblk + b] = chainp[b][j].first;
-            w.pairs[(2 * j + 1) * nblk + b] = chainp[b][j].second;
+            w.pairs[(2 * j + 1) * nblk + b] = chainp[b][j].second < 0 ? ncomp : chainp[b][j].second;
         }
     const size_t S = (size_t)C * L;
     w.row.assign(S, -1);
@@ -727,7 +733,9 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
         const NodeOp &nd = h.node[k];
         w.row[i] = nd.row;
         w.node[i] = k;
-        w.info[i] = (nd.mask & 7) | 8 | ((cb[q] + 1) << 4) | (cb[q + size[k] - 1] << 13) | ((cf[q] + 1) << 22);
+        w.info[i] = (int32_t)((uint32_t)((nd.mask & 7) | 8 | ((cb[q] + 1) << 4) | (cb[q + size[k] - 1] << 13) |
+                                         ((cf[q] + 1) << 22)) |
+                              (seg && bfirst[blk[k]] == k ? 0x80000000u : 0u));   // bit 31: block head (segmented scan)
         w.blk[i] = blk[k];
         for (int p = 0; p < 3; ++p)
             if (mref[k][p] >= 1) w.mref[(p * C + c) * L + lane] = cf[pos[mref[k][p]]];
@@ -808,6 +816,7 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
         probe.ncomp = ncomp;
         probe.temp_sym = w.temp_sym;
         probe.ncode = h.ncode;
+        probe.has_rel = has_rel;
         if (wblk_lds_bytes(probe) > WAVE_LDS_BUDGET) return no("wave-block kernel: the scenario's loads exceed LDS");
         w.wpb = w.wpb_big_batch = wps;
         w.ok = true;
@@ -2056,6 +2065,7 @@ extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const d
     w.temp_sym = wh.temp_sym;
     w.wps = wh.wps;
     w.coop = wh.coop;
+    w.has_rel = wh.has_rel;
     w.ncode = h.ncode;
     const int lds = !wh.ok ? 0 : (int)wave_any_lds_bytes(w);
     const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, lds, wh.ncomp, wh.nblk, wh.bdepth};

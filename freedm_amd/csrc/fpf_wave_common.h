@@ -53,6 +53,37 @@ __device__ __forceinline__ void seg_incl_n(double (&x)[N]) {
     }
 }
 
+// DPP move of a 32-bit int; lanes without a source read 0
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_i(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, CTRL, RM, BM, true);
+}
+
+// one Hillis-Steele step of a segmented scan: (x, f) <- (s, fs) o (x, f) with
+// (a, g) o (b, h) = (h ? b : a + b, g | h), (s, fs) the DPP source
+template <int CTRL, int RM, int BM, int N>
+__device__ __forceinline__ void segf_step(double (&x)[N], int &f) {
+    double sv[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) sv[i] = dpp_d<CTRL, RM, BM>(x[i]);
+    const int fs = dpp_i<CTRL, RM, BM>(f);
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = f ? x[i] : x[i] + sv[i];
+    f |= fs;
+}
+
+// segmented inclusive scan over the 64 lanes of a wavefront (f != 0: a segment
+// head lies in this lane's part), the steps of seg_incl_n
+template <int N>
+__device__ __forceinline__ void segf_incl64(double (&x)[N], int &f) {
+    segf_step<0x111, 0xf, 0xf>(x, f);
+    segf_step<0x112, 0xf, 0xf>(x, f);
+    segf_step<0x114, 0xf, 0xf>(x, f);
+    segf_step<0x118, 0xf, 0xf>(x, f);
+    segf_step<0x142, 0xa, 0xf>(x, f);
+    segf_step<0x143, 0xc, 0xf>(x, f);
+}
+
 // the value of the segment's last lane
 template <int L>
 __device__ __forceinline__ double seg_last(double x, int seg) {
@@ -144,6 +175,25 @@ __device__ __forceinline__ void wave_prefix(const double *wt, int wv, int lane, 
         if (TOT) tot[q] = readlane_d(t[q], W - 1);
     }
 }
+// wave_prefix for a scan segmented at heads: wt[8 j + 6] != 0 marks a wave
+// with a head; pre = the segmented combine of waves 0 .. wv-1 (0 for wave 0)
+template <int W>
+__device__ __forceinline__ void wave_prefix_seg(const double *wt, int wv, int lane, double (&pre)[6]) {
+    const int j = lane < W ? lane : 0;
+    const double2 *t2 = (const double2 *)(wt + 8 * j);
+    const double2 a = t2[0], b = t2[1], c = t2[2], d = t2[3];
+    double t[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    int fl = lane < W && d.x != 0.0 ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) t[q] = lane < W ? t[q] : 0.0;
+    if (W > 1) segf_step<0x111, 0xf, 0xf>(t, fl);
+    if (W > 2) segf_step<0x112, 0xf, 0xf>(t, fl);
+    if (W > 4) segf_step<0x114, 0xf, 0xf>(t, fl);
+    const int wu = __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) pre[q] = wu == 0 ? 0.0 : readlane_d(t[q], wu - 1);
+}
+
 // Outputs of node k, phase p (DPF_return7.cpp:222-253); returns (Re SL, |V|)
 __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn, int B, int k, int p, size_t s, cx v,
                                              cx il, cx ib) {
@@ -183,6 +233,7 @@ __device__ __forceinline__ bool si_valid(int x) { return (x >> 3) & 1; }
 __device__ __forceinline__ int si_store_b(int x) { return ((x >> 4) & 511) - 1; }   // -1: not gathered
 __device__ __forceinline__ int si_last(int x) { return (x >> 13) & 511; }
 __device__ __forceinline__ int si_store_f(int x) { return ((x >> 22) & 511) - 1; }  // -1: not gathered
+__device__ __forceinline__ bool si_head(int x) { return x < 0; }   // bit 31: a block head (wave-block kernel)
 
 // segment-wide reductions by the DPP scan pattern; the segment's last lane holds
 // the result.  Lanes without a source keep +inf (bound_ctrl off, old = +inf).

@@ -65,7 +65,7 @@ constexpr int WB_BD = 6;  // block-chain depth resolved from registers (deeper: 
 
 }  // namespace
 
-template <int W, bool FULL, int C>
+template <int W, bool FULL, int C, bool SEG>
 __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
                                                              OutDev o) {
     constexpr int L = 64 * W, NT = 64 * W;
@@ -83,7 +83,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double2 *const stg = zc + f.ncode * ntz;
     double2 *const X = stg + 3 * PS;
     double2 *const OFF = X + 3 * XC;
-    double2 *const V0S = OFF + 3 * nblk;
+    double2 *const OFFA = OFF + 3 * nblk;   // [3][nblk] off(b) itself (has_rel only)
+    double2 *const V0S = OFF + 3 * nblk * (f.has_rel ? 2 : 1);
     double *const wtb = (double *)(V0S + 4);
     double *const wtf = wtb + 8 * W;
     double *const vx = wtf + 8 * W;             // [3][2] per-phase Vmin / Vmax (zeroed phases)
@@ -341,95 +342,193 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
         }
 
-        // ---- forward sweep (:163-195): V = V0 - A, A = Ginc + off(block)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            cx acc = g[0][p];
-#pragma unroll
-            for (int c = 1; c < C; ++c) { acc = cadd(acc, g[c][p]); g[c][p] = acc; }
-            sc6[2 * p] = acc.re;
-            sc6[2 * p + 1] = acc.im;
-        }
-        seg_incl_n<64>(sc6);
-        if (lane == 63) {
-#pragma unroll
-            for (int q = 0; q < 6; ++q) wtf[8 * wv + q] = sc6[q];
-        }
-        __syncthreads();
-        wave_prefix<W, false>(wtf, wv, lane, pre, tot6);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            const cx ex = csub(mk(pre[2 * p] + sc6[2 * p], pre[2 * p + 1] + sc6[2 * p + 1]), g[C - 1][p]);
-#pragma unroll
-            for (int c = 0; c < C; ++c) g[c][p] = cadd(ex, g[c][p]);   // Ginc at this slot
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const int ci = si_store_f(si[c]);
-            if (ci >= 0) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
-            }
-        }
-        if (!WABL(8)) __syncthreads();
-        // block offsets, one thread per block, stored as V0 - off(b): off(b) = sum over
-        // b's block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
-        if (chain_regs) {
-            if (tid < nblk) {
-                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
-#pragma unroll
-                for (int j = 0; j < WB_BD; ++j) {
-                    if (j < bdepth) {   // uniform; levels past a chain's depth read the zero entry
-#pragma unroll
-                        for (int p = 0; p < 3; ++p)
-                            of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
-                    }
-                    // (two levels' twelve reads in flight at a time: the registers of
-                    // all of them at once would spill)
-                    if (j & 1) __builtin_amdgcn_sched_barrier(0);
-                }
-#pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
-            }
-        } else
-        for (int b = tid; b < nblk; b += NT) {
-            cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
-            for (int j = 0; j < bdepth; ++j) {
-                const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
-#pragma unroll
-                for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
-            }
-#pragma unroll
-            for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
-        }
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
+        if (SEG) {
+            // ---- forward sweep (:163-195): V = V0 - A(k), A(k) = off(block) + Gseg(k),
+            // Gseg the block-local path sum of the drops (a prefix scan segmented at
+            // the block heads: every block is a run of consecutive positions, each the
+            // child of the one before), off(b) = the sum over b's block-ancestor chain
+            // of Gseg at the taps.  Lane-local part, resetting at heads:
+            int hf = 0;   // a block head among this lane's slots
+    #pragma unroll
+            for (int c = 0; c < C; ++c) hf |= si_head(si[c]) ? 1 : 0;
+    #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const cx vr = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
-                if (FULL) g[c][p] = vr;
-                v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
+                cx acc = g[0][p];
+    #pragma unroll
+                for (int c = 1; c < C; ++c) { acc = si_head(si[c]) ? g[c][p] : cadd(acc, g[c][p]); g[c][p] = acc; }
+                sc6[2 * p] = acc.re;
+                sc6[2 * p + 1] = acc.im;
             }
-        if (FULL && f.has_rel) {
-            // below a zeroed ancestor m: V(k,p) = A(m) - A(k) = Vr(k) - Vr(m), Vr = V0 - A
-            // before the zeroing (held in g); the forward entries (block offsets are
-            // read) carry Vr now
-#pragma unroll
+            // the wave's segmented scan over the lanes' (total, head) pairs; the lane
+            // before's inclusive value by wave_shr:1 (lane 0: none)
+            int hs = hf;
+            segf_incl64(sc6, hs);
+            double pv[6];
+    #pragma unroll
+            for (int q = 0; q < 6; ++q) pv[q] = dpp_d<0x138, 0xf, 0xf>(sc6[q]);
+            const int hp = dpp_i<0x138, 0xf, 0xf>(hs);
+            if (lane == 63) {
+    #pragma unroll
+                for (int q = 0; q < 6; ++q) wtf[8 * wv + q] = sc6[q];
+                wtf[8 * wv + 6] = hs ? 1.0 : 0.0;
+            }
+            __syncthreads();
+            wave_prefix_seg<W>(wtf, wv, lane, pre);
+    #pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                // the carry into this lane: the segment running in from the lanes and
+                // waves before, up to this lane's first head
+                const cx lc = hp ? mk(pv[2 * p], pv[2 * p + 1]) : mk(pre[2 * p] + pv[2 * p], pre[2 * p + 1] + pv[2 * p + 1]);
+                bool seen = false;
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    seen = seen || si_head(si[c]);
+                    if (!seen) g[c][p] = cadd(lc, g[c][p]);   // Gseg at this slot
+                }
+            }
+    #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const int ci = si_store_f(si[c]);
                 if (ci >= 0) {
-#pragma unroll
+    #pragma unroll
                     for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
                 }
             }
-            __syncthreads();
-#pragma unroll
-            for (int c = 0; c < C; ++c)
-#pragma unroll
+            if (!WABL(8)) __syncthreads();
+            // block offsets, one thread per block, stored as V0 - off(b) (and off(b)
+            // itself for the restart below a zeroed phase); one X read per chain level
+            if (chain_regs) {
+                if (tid < nblk) {
+                    cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    #pragma unroll
+                    for (int j = 0; j < WB_BD; ++j) {
+                        if (j < bdepth) {   // uniform; levels past a chain's depth read the zero entry
+    #pragma unroll
+                            for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], ldx(X, p * XC + (bp[j] & 0xffff)));
+                        }
+                    }
+    #pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
+                        if (FULL && f.has_rel) stx(OFFA, p * nblk + tid, of[p]);
+                    }
+                }
+            } else
+            for (int b = tid; b < nblk; b += NT) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+                for (int j = 0; j < bdepth; ++j) {
+                    const int pa = pairs[(2 * j) * nblk + b];
+    #pragma unroll
+                    for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], ldx(X, p * XC + pa));
+                }
+    #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    const int mr = f.slot_mref[(p * C + c) * L + tid];
-                    if (mr >= 0 && !((si_mask(si[c]) >> p) & 1)) v[c][p] = csub(g[c][p], ldx(X, p * XC + mr));
+                    stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
+                    if (FULL && f.has_rel) stx(OFFA, p * nblk + b, of[p]);
+                }
+            }
+            __syncthreads();
+    #pragma unroll
+            for (int c = 0; c < C; ++c)
+    #pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const cx vr = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
+                    v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
+                }
+            if (FULL && f.has_rel) {
+                // below a zeroed ancestor m: V(k,p) = A(m) - A(k) (:180-195: the path
+                // restarts from 0 at m), both small path sums; the forward entries (the
+                // block offsets are read) carry A now
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int ci = si_store_f(si[c]);
+                    if (ci >= 0) {
+    #pragma unroll
+                        for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, cadd(ldx(OFFA, p * nblk + bk[c]), g[c][p]));
+                    }
+                }
+                __syncthreads();
+    #pragma unroll
+                for (int c = 0; c < C; ++c)
+    #pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        const int mr = f.slot_mref[(p * C + c) * L + tid];
+                        if (mr >= 0 && !((si_mask(si[c]) >> p) & 1))
+                            v[c][p] = csub(ldx(X, p * XC + mr), cadd(ldx(OFFA, p * nblk + bk[c]), g[c][p]));
+                    }
+            }
+        } else {
+            // (feeders without a live phase below a zeroed one: one global prefix scan,
+            // off(b) from the differences Ginc[tap] - Ginc[first - 1]; 5 % faster than
+            // the segmented scan on config 3)
+            // ---- forward sweep (:163-195): V = V0 - A, A = Ginc + off(block)
+    #pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                cx acc = g[0][p];
+    #pragma unroll
+                for (int c = 1; c < C; ++c) { acc = cadd(acc, g[c][p]); g[c][p] = acc; }
+                sc6[2 * p] = acc.re;
+                sc6[2 * p + 1] = acc.im;
+            }
+            seg_incl_n<64>(sc6);
+            if (lane == 63) {
+    #pragma unroll
+                for (int q = 0; q < 6; ++q) wtf[8 * wv + q] = sc6[q];
+            }
+            __syncthreads();
+            wave_prefix<W, false>(wtf, wv, lane, pre, tot6);
+    #pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx ex = csub(mk(pre[2 * p] + sc6[2 * p], pre[2 * p + 1] + sc6[2 * p + 1]), g[C - 1][p]);
+    #pragma unroll
+                for (int c = 0; c < C; ++c) g[c][p] = cadd(ex, g[c][p]);   // Ginc at this slot
+            }
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int ci = si_store_f(si[c]);
+                if (ci >= 0) {
+    #pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+                }
+            }
+            if (!WABL(8)) __syncthreads();
+            // block offsets, one thread per block, stored as V0 - off(b): off(b) = sum over
+            // b's block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
+            if (chain_regs) {
+                if (tid < nblk) {
+                    cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    #pragma unroll
+                    for (int j = 0; j < WB_BD; ++j) {
+                        if (j < bdepth) {   // uniform; levels past a chain's depth read the zero entry
+    #pragma unroll
+                            for (int p = 0; p < 3; ++p)
+                                of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
+                        }
+                        // (two levels' twelve reads in flight at a time: the registers of
+                        // all of them at once would spill)
+                        if (j & 1) __builtin_amdgcn_sched_barrier(0);
+                    }
+    #pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
+                }
+            } else
+            for (int b = tid; b < nblk; b += NT) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+                for (int j = 0; j < bdepth; ++j) {
+                    const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
+    #pragma unroll
+                    for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
+                }
+    #pragma unroll
+                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
+            }
+            __syncthreads();
+    #pragma unroll
+            for (int c = 0; c < C; ++c)
+    #pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const cx vr = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
+                    v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
                 }
         }
 
@@ -658,7 +757,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 size_t wblk_lds_bytes(const WaveDev &w) {
     const size_t ntz = w.temp_sym ? 4 : 9, xc = (size_t)w.ncomp + 1, nt = 64 * (size_t)w.wps;
     const size_t zc = 16 * (size_t)w.ncode * ntz;
-    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk + 4) + 8 * 16 * (size_t)w.wps + 64 +
+    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk * (w.has_rel ? 2 : 1) + 4) +
+                        8 * 16 * (size_t)w.wps + 64 +
                         4 * 2 * (size_t)w.bdepth * w.nblk;
     return zc + std::max(rest, 8 * 8 * nt);   // the last workgroup's fold reuses the space after zc
 }
@@ -679,8 +779,9 @@ bool wblk_geometry(int n, int *wps, int *c) {
 namespace {
 typedef void (*WblkKernel)(WaveDev, int, const double *, OutDev);
 template <int W, int C>
-WblkKernel pick_wblk(bool full) {
-    return full ? dpf_wblk_kernel<W, true, C> : dpf_wblk_kernel<W, false, C>;
+WblkKernel pick_wblk(bool full, bool seg) {
+    // (a live phase below a zeroed one implies zeroed phases: the full variant)
+    return seg ? dpf_wblk_kernel<W, true, C, true> : (full ? dpf_wblk_kernel<W, true, C, false> : dpf_wblk_kernel<W, false, C, false>);
 }
 }  // namespace
 
@@ -688,10 +789,14 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
     if (w.coop) return launch_wcoop(w, n_scen, pq, o, st);   // 2049..4096 branches: fpf_wcoop.hip
     // the full-output variant keeps IL and Ib of the last sweep (Vpolar / PQb /
     // PQL), and the zeroed-phase paths
-    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
+    // (the tables of a feeder with a live phase below a zeroed one are built for
+    // the segmented forward scan: fpf_api.cpp analyse_wave)
+    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask, seg = w.has_rel != 0;
     WblkKernel k = nullptr;
-    if (w.C == WB_C) k = w.wps == 2 ? pick_wblk<2, WB_C>(full) : (w.wps == 4 ? pick_wblk<4, WB_C>(full) : (w.wps == 8 ? pick_wblk<8, WB_C>(full) : nullptr));
-    else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full) : (w.wps == 4 ? pick_wblk<4, 8>(full) : nullptr);
+    if (w.C == WB_C)
+        k = w.wps == 2 ? pick_wblk<2, WB_C>(full, seg)
+                       : (w.wps == 4 ? pick_wblk<4, WB_C>(full, seg) : (w.wps == 8 ? pick_wblk<8, WB_C>(full, seg) : nullptr));
+    else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full, seg) : (w.wps == 4 ? pick_wblk<4, 8>(full, seg) : nullptr);
     if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB: a per-device setting, once per (device, variant)
     static std::mutex mu;
@@ -700,7 +805,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> lk(mu);
-        const std::array<int, 3> key = {dev, w.wps * 16 + w.C, (int)full};
+        const std::array<int, 3> key = {dev, w.wps * 16 + w.C, (int)full + 2 * (int)seg};
         if (!attr_done.count(key)) {
             hipFuncAttributes fa{};
             hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
