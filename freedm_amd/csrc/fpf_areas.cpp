@@ -37,7 +37,11 @@
 
 namespace fpf {
 hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, int nl, int B, double *dst,
-                             hipStream_t st);
+                             double *dst2, hipStream_t st);
+hipError_t areas_add_rows(double *work, const double *base, int nl, int B, const AreaKids &k, const int32_t *ctl,
+                          hipStream_t st);
+hipError_t areas_gather_vsrc_all(const double *v_re, const double *v_im, int nn, int B, const AreaKids &k, double *diff,
+                                 const int32_t *ctl, hipStream_t st);
 hipError_t areas_add_row(double *work, const double *base, int nl, int lrow, int B, const double *add,
                          const int32_t *ctl, hipStream_t st);
 hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
@@ -78,6 +82,7 @@ struct fpf_areas {
     int nl = 0, ncols = 0, nn = 0;
     double lb_v = 0.96, ub_v = 1.05;   // the hosting counters of the aggregate (fpf_opts)
     bool warm = true;                  // warm-started area solves (FPF_AREAS_WARM=0: flat V0 each time)
+    int last_outer = 0;                // the previous solve's outer iterations (the first chunk's size)
     std::vector<Area> area;      // index = area id, parents before children
     std::vector<int> order;      // solve order
     int cap = 0, vcap = 0;
@@ -416,28 +421,28 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     AHIP(a, hipMemcpyAsync(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice, st));
     AHIP(a, hipMemsetAsync(a->d_res, 0, RES_HEAD, st));
     AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b, st));
-    for (Area &A : a->area) {
-        AHIP(a, areas_gather_rows(a->d_pq, a->nl, A.d_rows, A.nl, B, A.d_base, st));
-        // the working loads: the area's own (the rows a child hangs off are
-        // rewritten every iteration)
-        AHIP(a, hipMemcpyAsync(A.d_work, A.d_base, sizeof(double) * 6 * A.nl * b, hipMemcpyDeviceToDevice, st));
-        AHIP(a, hipMemsetAsync(A.d_sin, 0, sizeof(double) * 6 * b, st));
-        AHIP(a, hipMemsetAsync(A.d_vsrc, 0, sizeof(double) * 6 * b, st));
-    }
+    // the area's loads and its working copy (the rows a child hangs off are
+    // rewritten from the second iteration on: the first adds no child source power,
+    // so neither the source powers nor the source voltages need clearing -- the
+    // first check never stops the loop)
+    for (Area &A : a->area) AHIP(a, areas_gather_rows(a->d_pq, a->nl, A.d_rows, A.nl, B, A.d_base, A.d_work, st));
     const int single = a->area.size() == 1 ? 1 : 0;
     // from the second outer iteration on, every area solve starts from its own V of
     // the previous one (a warm start: its sweeps then only follow the boundary's
     // move, instead of ~10 sweeps from the flat V0 to the inner tolerance)
-    auto enqueue_iteration = [&](bool warm) -> int {
+    auto enqueue_iteration = [&](bool first, bool warm) -> int {
         for (int ar : a->order) {
             Area &A = a->area[ar];
             // the boundary rows = their own load + the child's source power of the
-            // previous iteration (every other row of d_work is the base, copied once)
-            for (const auto &k : A.kids)
-                AHIP(a, areas_add_row(A.d_work, A.d_base, A.nl, k.first, B, a->area[k.second].d_sin, ctl, st));
-            if (A.parent >= 0) {
-                const Area &P = a->area[A.parent];
-                AHIP(a, areas_gather_vsrc(P.d_vre, P.d_vim, P.nn, A.lb, B, A.d_vsrc, a->d_diff, ctl, st));
+            // previous iteration (every other row of d_work is the base, copied once);
+            // all of an area's children in one launch (AREA_MAX_KIDS at a time)
+            for (size_t j0 = 0; !first && j0 < A.kids.size(); j0 += AREA_MAX_KIDS) {
+                AreaKids k{};
+                for (size_t j = j0; j < A.kids.size() && k.n < AREA_MAX_KIDS; ++j, ++k.n) {
+                    k.lrow[k.n] = A.kids[j].first;
+                    k.ptr[k.n] = a->area[A.kids[j].second].d_sin;
+                }
+                AHIP(a, areas_add_rows(A.d_work, A.d_base, A.nl, B, k, ctl, st));
             }
             fpf_outputs o;
             std::memset(&o, 0, sizeof(o));
@@ -452,6 +457,17 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
                                                 A.parent >= 0 ? A.d_vsrc : nullptr, A.d_sin, FPF_LAYOUT_SCEN_FASTEST,
                                                 nullptr, ctl, warm ? A.d_vre : nullptr, warm ? A.d_vim : nullptr);
             if (r < 0) return afail(a, r, std::string("area solve: ") + fpf_last_error(a->ctx));
+            // this area's V at every child's boundary bus: the children's source
+            // voltages of this iteration (solved next, in order), one launch
+            for (size_t j0 = 0; j0 < A.kids.size(); j0 += AREA_MAX_KIDS) {
+                AreaKids k{};
+                for (size_t j = j0; j < A.kids.size() && k.n < AREA_MAX_KIDS; ++j, ++k.n) {
+                    const Area &Ch = a->area[A.kids[j].second];
+                    k.lrow[k.n] = Ch.lb;
+                    k.ptr[k.n] = Ch.d_vsrc;
+                }
+                AHIP(a, areas_gather_vsrc_all(A.d_vre, A.d_vim, A.nn, B, k, a->d_diff, ctl, st));
+            }
         }
         AHIP(a, areas_check(a->d_diff, B, tol, single, ctl, last, st));
         return FPF_OK;
@@ -462,19 +478,27 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     hipEvent_t ev[2] = {nullptr, nullptr};
     AHIP(a, hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
     AHIP(a, hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    // the first chunk is as long as the previous solve's loop (repeated studies of
+    // one feeder converge in about as many outer iterations), and its flag is read
+    // at once: a solve that needs no more then enqueues no no-op iterations
+    const int first_chunk = a->last_outer >= K ? std::min(a->last_outer, max_outer) : 0;
     int enq = 0, chunk = 0;
     bool stop = false;
     while (!stop && enq < max_outer) {
-        for (int i = 0; i < K && enq < max_outer; ++i, ++enq) {
-            rc = enqueue_iteration(enq > 0 && a->warm);
+        const int n_it = chunk == 0 && first_chunk ? first_chunk : K;
+        for (int i = 0; i < n_it && enq < max_outer; ++i, ++enq) {
+            rc = enqueue_iteration(enq == 0, enq > 0 && a->warm);
             if (rc) break;
         }
         if (rc) break;
         AHIP(a, hipMemcpyAsync(h_ctl[chunk & 1], ctl, 8, hipMemcpyDeviceToHost, st));
         AHIP(a, hipEventRecord(ev[chunk & 1], st));
-        if (chunk > 0) {
+        if (chunk == 0 && first_chunk) {
+            AHIP(a, hipEventSynchronize(ev[0]));
+            stop = h_ctl[0][0] != 0;
+        } else if (chunk > 0) {
             AHIP(a, hipEventSynchronize(ev[(chunk - 1) & 1]));
-            stop = h_ctl[(chunk - 1) & 1][0] != 0;
+            stop = stop || h_ctl[(chunk - 1) & 1][0] != 0;
         }
         ++chunk;
     }
@@ -505,6 +529,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     const int32_t *h_c = (const int32_t *)a->h_res;
     const bool conv = h_c[0] != 0;
     const int outer = h_c[1];
+    a->last_outer = outer;
     double h_last;
     std::memcpy(&h_last, a->h_res + 16, 8);
     const double *h_loss = (const double *)(a->h_res + RES_HEAD), *h_vmin = h_loss + b, *h_vmax = h_vmin + b;

@@ -7,17 +7,21 @@
 #include <cmath>
 #include <cstdint>
 
+#include "fpf_internal.h"
+
 namespace fpf {
 namespace {
 
-// dst[f][r][s] = src[f][row[r]][s] (row[r] < 0: a separator row, 0)
+// dst[f][r][s] = src[f][row[r]][s] (row[r] < 0: a separator row, 0), also into dst2 when given
 __global__ void gather_rows_kernel(const double *__restrict__ src, int nl_src, const int32_t *__restrict__ row, int nl,
-                                   int B, double *__restrict__ dst) {
+                                   int B, double *__restrict__ dst, double *__restrict__ dst2) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     const int fr = blockIdx.y;   // f * nl + r
     if (s >= B) return;
     const int f = fr / nl, r = fr % nl, m = row[r];
-    dst[(size_t)fr * B + s] = m < 0 ? 0.0 : src[((size_t)f * nl_src + m) * B + s];
+    const double x = m < 0 ? 0.0 : src[((size_t)f * nl_src + m) * B + s];
+    dst[(size_t)fr * B + s] = x;
+    if (dst2) dst2[(size_t)fr * B + s] = x;
 }
 
 // The kernels of one outer iteration do nothing once the loop has converged
@@ -31,6 +35,35 @@ __global__ void add_row_kernel(double *__restrict__ work, const double *__restri
     if (s >= B || ctl[0]) return;
     const size_t i = ((size_t)f * nl + lrow) * B + s;
     work[i] = base[i] + add[(size_t)f * B + s];
+}
+
+// every child row of one area: work[f][lrow_j][s] = base[f][lrow_j][s] + add_j[f][s]
+__global__ void add_rows_kernel(double *__restrict__ work, const double *__restrict__ base, int nl, int B, AreaKids k,
+                                const int32_t *__restrict__ ctl) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int f = blockIdx.y % 6, j = blockIdx.y / 6;
+    if (s >= B || ctl[0]) return;
+    const size_t i = ((size_t)f * nl + k.lrow[j]) * B + s;
+    work[i] = base[i] + k.ptr[j][(size_t)f * B + s];
+}
+
+// every child of one area after its solve: vsrc_j = V(node lb_j) of this area; diff = max move
+__global__ void gather_vsrc_all_kernel(const double *__restrict__ v_re, const double *__restrict__ v_im, int nn, int B,
+                                       AreaKids k, double *__restrict__ diff, const int32_t *__restrict__ ctl) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B || ctl[0]) return;
+    double d = diff[s];
+    for (int j = 0; j < k.n; ++j) {
+        double *const vsrc = k.ptr[j];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const double re = v_re[((size_t)p * nn + k.lrow[j]) * B + s], im = v_im[((size_t)p * nn + k.lrow[j]) * B + s];
+            d = fmax(d, fmax(fabs(re - vsrc[(size_t)(2 * p) * B + s]), fabs(im - vsrc[(size_t)(2 * p + 1) * B + s])));
+            vsrc[(size_t)(2 * p) * B + s] = re;
+            vsrc[(size_t)(2 * p + 1) * B + s] = im;
+        }
+    }
+    diff[s] = d;
 }
 
 // vsrc[2p][s], vsrc[2p+1][s] = V(p, node lb) of the parent area; diff[s] = max(diff[s], |change|)
@@ -110,8 +143,20 @@ inline dim3 grid(int B, int y) { return dim3((unsigned)((B + 255) / 256), (unsig
 }  // namespace
 
 hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, int nl, int B, double *dst,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(gather_rows_kernel, grid(B, 6 * nl), dim3(256), 0, st, src, nl_src, row, nl, B, dst);
+                             double *dst2, hipStream_t st) {
+    hipLaunchKernelGGL(gather_rows_kernel, grid(B, 6 * nl), dim3(256), 0, st, src, nl_src, row, nl, B, dst, dst2);
+    return hipGetLastError();
+}
+hipError_t areas_add_rows(double *work, const double *base, int nl, int B, const AreaKids &k, const int32_t *ctl,
+                          hipStream_t st) {
+    if (k.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(add_rows_kernel, grid(B, 6 * k.n), dim3(256), 0, st, work, base, nl, B, k, ctl);
+    return hipGetLastError();
+}
+hipError_t areas_gather_vsrc_all(const double *v_re, const double *v_im, int nn, int B, const AreaKids &k, double *diff,
+                                 const int32_t *ctl, hipStream_t st) {
+    if (k.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_vsrc_all_kernel, grid(B, 1), dim3(256), 0, st, v_re, v_im, nn, B, k, diff, ctl);
     return hipGetLastError();
 }
 hipError_t areas_add_row(double *work, const double *base, int nl, int lrow, int B, const double *add,

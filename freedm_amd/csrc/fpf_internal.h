@@ -265,6 +265,16 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
 size_t wblk_lds_bytes(const WaveDev &w);
 hipError_t launch_wcoop(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wcoop_lds_bytes(const WaveDev &w);
+// the multi-area solve's fused exchange kernels (fpf_areas_kernels.hip): up to
+// AREA_MAX_KIDS children of one area per launch -- the local row of a child's
+// bus and its source power (add_rows), or the child's boundary bus and its
+// source-voltage array (gather_vsrc_all)
+constexpr int AREA_MAX_KIDS = 8;
+struct AreaKids {
+    int n;
+    int lrow[AREA_MAX_KIDS];
+    double *ptr[AREA_MAX_KIDS];
+};
 constexpr int COOP_NSLOT = 1024;   // exchange areas of the paired kernel (scenarios in flight <= 256)
 inline size_t wave_any_lds_bytes(const WaveDev &w) {
     return w.coop ? wcoop_lds_bytes(w) : (w.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w));
