@@ -187,3 +187,17 @@ def test_wcoop_areas_equal_monolithic():
     vc = c["V_re"] + 1j * c["V_im"]
     assert float(np.max(np.abs(v - vc) / np.abs(vc))) <= 1e-10
     np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-8)
+
+
+@pytest.mark.parametrize("B", [1, 9, 17])
+def test_wcoop_small_and_ragged_batches(B):
+    """Batches that leave padding pairs in the last group of 8 scenarios (the
+    grid is 16 workgroups per 8 scenarios): every real scenario against the
+    oracle, the padding members exit without touching an exchange area."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(2100, 2100)
+    pq = F.scenario_loads(f, np.arange(B))
+    r = PowerFlow(f).solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    _check_full(r, c)
