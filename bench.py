@@ -376,6 +376,62 @@ def _diag_4096(torch, local, stream, dev):
                     "exact kernel (every scenario)"}
 
 
+def _diag_heavy(torch, local, stream, dev):
+    """Diagnostic leg: the config-2 and config-3 feeders at their full batch sizes
+    under heavier, mixed loads (each scenario's loads scaled by a factor spread
+    over 1.5 .. 3.0: 6 .. 12 sweeps instead of the calibrated batches' 5), on the
+    fast kernels, beside the exact generic kernel on the same device inputs:
+    launch times, mean sweeps, identical iteration counts and status, max V
+    relative difference (the parity margin at full size)."""
+    from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
+    out = {}
+    for name, n, B, lay in (("config2_heavy", 123, 4096, 0), ("config3_heavy", 2048, 65536, 1)):
+        f = synthetic_feeder(n, n)
+        NB = min(B, 1024)
+        base = torch.from_numpy(scenario_loads(f, np.arange(NB), seed=B + 7)).to(dev)
+        ids = torch.arange(B, device=dev)
+        mult = 1.5 * torch.pow(torch.tensor(2.0, dtype=torch.float64, device=dev),
+                               ((ids * 2654435761) % 1000).double() / 999.0)   # 1.5 .. 3.0
+        d = base[:, :, ids % NB] * mult
+        if lay == 1:
+            d = d.permute(2, 0, 1).contiguous()
+        del base
+        legs = {}
+        for kind, exact in (("fast", 0), ("exact", 1)):
+            pf = PowerFlow(f, device=local, exact=exact, layout=lay)
+            pf.reserve(B)
+            ms, o = _kernel_ms(torch, pf, d, B, 3, 1, stream, dev)
+            legs[kind] = (ms, o, pf.kernel, pf.info["nb"], pf.nn)
+            pf.close()
+        (msf, of, kf, nb, nn), (mse, oe, ke, _, _) = legs["fast"], legs["exact"]
+        conv = oe["status"] == 0
+        vrel = 0.0
+        for c0 in range(0, B, 4096):   # (in scenario chunks: the 2048-bus V is 6.4 GB per part)
+            sl = (slice(c0, c0 + 4096),) if lay == 1 else (slice(None), slice(None), slice(c0, c0 + 4096))
+            a = torch.complex(of["v_re"][sl], of["v_im"][sl])
+            b = torch.complex(oe["v_re"][sl], oe["v_im"][sl])
+            cc = conv[c0:c0 + 4096]
+            cm = cc.view(-1, 1, 1) if lay == 1 else cc.view(1, 1, -1)
+            r = torch.where(cm, (a - b).abs() / b.abs(), torch.zeros_like(b.real))
+            vrel = max(vrel, float(r.max().item()))
+            del a, b, r
+        del d
+        bpa = bytes_alg_per_scenario(nb, nn)
+        it = of["iters"].double()
+        out[name] = {"workload": f"{nn}-bus synthetic feeder x {B} scenarios, loads x 1.5 .. 3.0",
+                     "kernel": _wave_kernel_name(nb) if kf == "wave" else kf, "kernel_ms": msf,
+                     "converged_scenarios_per_s": int(conv.sum().item()) / (msf / 1e3),
+                     "roofline_frac": bpa * B / (msf / 1e3) / 1e9 / HBM_PEAK_GBS,
+                     "mean_sweeps": float(it.mean().item()), "min_sweeps": int(it.min().item()),
+                     "max_sweeps": int(it.max().item()), "vmin": float(of["vmin"][conv].min().item()),
+                     "exact_kernel": ke, "exact_kernel_ms": mse,
+                     "iters_equal_exact": bool(torch.equal(of["iters"], oe["iters"])),
+                     "status_equal_exact": bool(torch.equal(of["status"], oe["status"])),
+                     "max_v_rel_diff_vs_exact": vrel}
+        del of, oe
+    return out
+
+
 def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
     """Average launch time (HIP events on the launch stream) of `steps`
     back-to-back solves of the device batch d_pq, plus the iterations."""
@@ -653,6 +709,9 @@ def main():
             pf3.close()
             # feeders of 2049..4096 branches: the paired wave-block kernel
             res["diag_4096bus"] = _diag_4096(torch, local, stream, dev)
+            # the calibrated batches run 5 sweeps each: the same feeders under heavier,
+            # mixed loads at full size, with the parity margin against the exact kernel
+            res["diag_heavy"] = _diag_heavy(torch, local, stream, dev)
             copy = _copy_bandwidth(torch, dev)
             res["hbm_copy_check"] = {"device_copy_gbs": copy, "spec_gbs": HBM_PEAK_GBS,
                                      "copy_frac_of_spec": copy / HBM_PEAK_GBS,
