@@ -42,10 +42,6 @@ hipError_t areas_add_rows(double *work, const double *base, int nl, int B, const
                           hipStream_t st);
 hipError_t areas_gather_vsrc_all(const double *v_re, const double *v_im, int nn, int B, const AreaKids &k, double *diff,
                                  const int32_t *ctl, hipStream_t st);
-hipError_t areas_add_row(double *work, const double *base, int nl, int lrow, int B, const double *add,
-                         const int32_t *ctl, hipStream_t st);
-hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
-                             const int32_t *ctl, hipStream_t st);
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
                                hipStream_t st);
 hipError_t areas_fold_results(int B, const double *loss, const double *vmin, const double *vmax, const int8_t *status,

@@ -27,16 +27,6 @@ __global__ void gather_rows_kernel(const double *__restrict__ src, int nl_src, c
 // The kernels of one outer iteration do nothing once the loop has converged
 // (ctl[0] != 0: iterations enqueued before the host looked are no-ops).
 
-// work[f][lrow][s] = base[f][lrow][s] + add[f][s]  for the 6 load fields (P1 Q1 P2 Q2 P3 Q3)
-__global__ void add_row_kernel(double *__restrict__ work, const double *__restrict__ base, int nl, int lrow, int B,
-                               const double *__restrict__ add, const int32_t *__restrict__ ctl) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    const int f = blockIdx.y;
-    if (s >= B || ctl[0]) return;
-    const size_t i = ((size_t)f * nl + lrow) * B + s;
-    work[i] = base[i] + add[(size_t)f * B + s];
-}
-
 // every child row of one area: work[f][lrow_j][s] = base[f][lrow_j][s] + add_j[f][s]
 __global__ void add_rows_kernel(double *__restrict__ work, const double *__restrict__ base, int nl, int B, AreaKids k,
                                 const int32_t *__restrict__ ctl) {
@@ -62,23 +52,6 @@ __global__ void gather_vsrc_all_kernel(const double *__restrict__ v_re, const do
             vsrc[(size_t)(2 * p) * B + s] = re;
             vsrc[(size_t)(2 * p + 1) * B + s] = im;
         }
-    }
-    diff[s] = d;
-}
-
-// vsrc[2p][s], vsrc[2p+1][s] = V(p, node lb) of the parent area; diff[s] = max(diff[s], |change|)
-__global__ void gather_vsrc_kernel(const double *__restrict__ v_re, const double *__restrict__ v_im, int nn, int lb,
-                                   int B, double *__restrict__ vsrc, double *__restrict__ diff,
-                                   const int32_t *__restrict__ ctl) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B || ctl[0]) return;
-    double d = diff[s];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        const double re = v_re[((size_t)p * nn + lb) * B + s], im = v_im[((size_t)p * nn + lb) * B + s];
-        d = fmax(d, fmax(fabs(re - vsrc[(size_t)(2 * p) * B + s]), fabs(im - vsrc[(size_t)(2 * p + 1) * B + s])));
-        vsrc[(size_t)(2 * p) * B + s] = re;
-        vsrc[(size_t)(2 * p + 1) * B + s] = im;
     }
     diff[s] = d;
 }
@@ -157,16 +130,6 @@ hipError_t areas_gather_vsrc_all(const double *v_re, const double *v_im, int nn,
                                  const int32_t *ctl, hipStream_t st) {
     if (k.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(gather_vsrc_all_kernel, grid(B, 1), dim3(256), 0, st, v_re, v_im, nn, B, k, diff, ctl);
-    return hipGetLastError();
-}
-hipError_t areas_add_row(double *work, const double *base, int nl, int lrow, int B, const double *add,
-                         const int32_t *ctl, hipStream_t st) {
-    hipLaunchKernelGGL(add_row_kernel, grid(B, 6), dim3(256), 0, st, work, base, nl, lrow, B, add, ctl);
-    return hipGetLastError();
-}
-hipError_t areas_gather_vsrc(const double *v_re, const double *v_im, int nn, int lb, int B, double *vsrc, double *diff,
-                             const int32_t *ctl, hipStream_t st) {
-    hipLaunchKernelGGL(gather_vsrc_kernel, grid(B, 1), dim3(256), 0, st, v_re, v_im, nn, lb, B, vsrc, diff, ctl);
     return hipGetLastError();
 }
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
