@@ -2,7 +2,7 @@
 # round 3: the whole GPU suite and smoke on the current build
 set -o pipefail
 export TMPDIR=/tmp
-D=gpurun_out/r03p
+D=gpurun_out/${RUN:-r03p}
 mkdir -p $D
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1 || { echo "GPU SUITE FAILED"; tail -60 $D/pytest.log; exit 1; }
 tail -2 $D/pytest.log
