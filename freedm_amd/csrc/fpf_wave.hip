@@ -51,6 +51,15 @@
 
 namespace fpf {
 
+// STG row r at index r + r / 16 (FPF_WAVE_SWZ, default on): a lane's slots sit 4
+// positions apart (position q = lane C + c), so the 16-byte Sld reads of 16
+// consecutive lanes hit rows 4 apart -- 4 of the 16 bank groups, a 4-way
+// conflict; one pad row every 16 spreads them over all 16
+#ifndef FPF_WAVE_SWZ
+#define FPF_WAVE_SWZ 1
+#endif
+__host__ __device__ __forceinline__ int swz_row(int r) { return FPF_WAVE_SWZ ? r + (r >> 4) : r; }
+
 // diagnostic ablation build (make ablate): FPF_WAVE_DBG bits switch pieces off;
 // results are wrong when set.  Compiled out of the product.
 #if defined(FPF_WAVE_ABL)
@@ -150,7 +159,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     const int pair_n = (2 * bdepth * nblk + 3) & ~3;
     int *const knode = pairs + pair_n;                                // [C][L] node of each slot
     constexpr int SROW = SPB + 1;
-    const int PSTR = (nl + 1) * SROW;                                 // double2 per phase plane of STG
+    const int PSTR = (swz_row(nl) + 1) * SROW;                        // double2 per phase plane of STG
     double2 *const stg = (double2 *)(knode + C * L);
     double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
@@ -167,7 +176,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int r = f.slot_row[c * L + li];
-        sb[c] = (r < 0 ? nl : r) * SROW + sc;
+        sb[c] = swz_row(r < 0 ? nl : r) * SROW + sc;
         si[c] = f.slot_info[c * L + li];
         bk[c] = f.slot_blk[c * L + li];
     }
@@ -181,12 +190,14 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         // element (f, row, j) of pq -> STG[f / 2][row][j].{re, im}
         auto spos = [&](int fr, int j) {
             const int fq = fr / nl, r = fr - fq * nl;
-            return 2 * (((fq >> 1) * (nl + 1) + r) * SROW + j) + (fq & 1);
+            return 2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(r)) * SROW + j) + (fq & 1);
         };
         // the same for a known (field, row)
-        auto spos2 = [&](int fq, int r, int j) { return 2 * (((fq >> 1) * (nl + 1) + r) * SROW + j) + (fq & 1); };
+        auto spos2 = [&](int fq, int r, int j) {
+            return 2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(r)) * SROW + j) + (fq & 1);
+        };
         if ((int)threadIdx.x < 3 * SROW)   // the zero row of each phase plane
-            stg[((int)threadIdx.x / SROW) * PSTR + nl * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
+            stg[((int)threadIdx.x / SROW) * PSTR + swz_row(nl) * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
         if (o.smaj) {
@@ -683,7 +694,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     const int k = knode[c * L + li];
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
-                        stx(stg, p * PSTR + (k - 1) * SROW + sc, v[c][p]);   // over the scenario's own Sld
+                        stx(stg, p * PSTR + swz_row(k - 1) * SROW + sc, v[c][p]);   // over the scenario's own Sld
                         if (FULL) {
                             emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
                             const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
@@ -751,7 +762,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                         const int k = k0 + li;
                         double m = 0.0;
                         if (k < nn) {
-                            const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + (k - 1) * SROW + sc);
+                            const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
                             m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
                         }
                         const bool nz = k < nn && m != 0.0;
@@ -794,7 +805,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         for (int k = li; k < nn; k += L) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + (k - 1) * SROW + sc);
+                const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
                 const double m2 = fma(vv.re, vv.re, vv.im * vv.im);
                 mn = fmin(mn, m2);
                 mx = fmax(mx, m2);
@@ -823,7 +834,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             for (int k = li; k < nn; k += L) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + (k - 1) * SROW + sc);
+                    const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
                     const double d = fma(vv.re, vv.re, vv.im * vv.im);
                     if (d > 0.0) m2 = fmin(m2, d);
                 }
@@ -882,7 +893,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         while (w.fq >= 3) { w.fq -= 3; ++j; }
         for (int i = threadIdx.x; i < total; i += NT) {
             const int p = w.fq, k = w.rr;
-            const double2 vv = k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + (k - 1) * SROW + j];
+            const double2 vv = k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + swz_row(k - 1) * SROW + j];
             if (o.v_re) __builtin_nontemporal_store(vv.x, o.v_re + (size_t)s0 * per + i);
             if (o.v_im) __builtin_nontemporal_store(vv.y, o.v_im + (size_t)s0 * per + i);
             w.next();
@@ -903,7 +914,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 const int i = i0 + u * NT + (int)threadIdx.x;
                 const int j = (int)threadIdx.x % SPB, p = w.fq, k = w.rr;
                 vv[u] = i >= total ? make_double2(0.0, 0.0)
-                                   : (k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + (k - 1) * SROW + j]);
+                                   : (k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + swz_row(k - 1) * SROW + j]);
                 w.next();
             }
 #pragma unroll
@@ -978,7 +989,7 @@ size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
     const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4 + REGION_EXTRA) | 1);
-    const size_t stage = 16 * 3 * ((size_t)w.nl + 1) * (spb + 1);   // STG: Sld in place, then V
+    const size_t stage = 16 * 3 * ((size_t)swz_row(w.nl) + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
     const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
     return temp + pairs + std::max(stage + regions, agg);
