@@ -67,7 +67,7 @@ struct fpf_feeder {
     // waves per workgroup of large batches
     void *d_wave = nullptr;
     WaveDev wdev{}, wdev_big{};
-    void *d_xch = nullptr, *d_xsync = nullptr;   // the paired wave-block kernel's exchange
+    void *d_xch = nullptr, *d_xsync = nullptr, *d_xvm = nullptr;   // the paired wave-block kernel's exchange
     // the partials + ticket scratch is shared by every aggregating launch on
     // this feeder (fused wave/specialised aggregate, fpf_aggregate_device): a
     // launch on another stream than the previous one first waits for it
@@ -431,7 +431,6 @@ static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps
                          const std::vector<int> &par, const std::vector<int> &at, const std::vector<int> &pos,
                          const std::vector<int> &blk, const std::vector<int> &size, const std::vector<int> &bfirst) {
     auto no = [&](const std::string &why) { w.ok = false; w.why = why; };
-    if (has_mask) return no("paired wave-block kernel: zeroed phases (the generic kernel runs them)");
     const int L = 64 * wps, P = (n + 1) / 2;
     if (P > C * L || n - P > C * L) return no("paired wave-block kernel: more than 2 x 2048 positions");
     if (nblk > L || maxd > 6) return no("paired wave-block kernel: block chains beyond the register-resolved form");
@@ -479,7 +478,7 @@ static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps
         const NodeOp &nd = h.node[k];
         w.row[i] = nd.row;
         w.node[i] = k;
-        w.info[i] = (int32_t)(8u | ((uint32_t)(cb[q] + 1) << 4) | ((uint32_t)cb[q + size[k] - 1] << 18));
+        w.info[i] = (int32_t)((uint32_t)(nd.mask & 7) | 8u | ((uint32_t)(cb[q] + 1) << 4) | ((uint32_t)cb[q + size[k] - 1] << 18));
         w.info2[i] = cf[q] + 1;
         w.blk[i] = blk[k];
         w.lng[i] = h.at(nd.row, 4);
@@ -506,7 +505,7 @@ static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps
     w.bdepth = bdepth;
     w.ncomp = ncomp;
     w.has_rel = 0;
-    w.has_mask = 0;
+    w.has_mask = has_mask;
     w.off_in_x = 0;
     w.wps = wps;
     w.coop = 2;
@@ -1519,6 +1518,14 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             }
             w.xch = (double *)f->d_xch;
             w.xsync = (unsigned *)f->d_xsync;
+            if (wh.has_mask) {   // the zeroed phases' |V| rows (the V_abc_list ranking)
+                e = hipMalloc(&f->d_xvm, sizeof(double) * (size_t)w.coop_nslot * 3 * h.nn);
+                if (e != hipSuccess) {
+                    fpf_feeder_destroy(f);
+                    return fail(ctx, FPF_ERR_HIP, std::string("paired kernel |V| rows: ") + hipGetErrorString(e));
+                }
+                w.xvm = (double *)f->d_xvm;
+            }
         }
         if (wave_any_lds_bytes(w) > WAVE_LDS_BUDGET) {
             fpf_feeder_destroy(f);
@@ -1603,6 +1610,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_wave);
     (void)hipFree(f->d_xch);
     (void)hipFree(f->d_xsync);
+    (void)hipFree(f->d_xvm);
     (void)hipFree(f->d_lay);
     (void)hipHostFree(f->h_stage);
     (void)hipFree(f->d_flag_count);

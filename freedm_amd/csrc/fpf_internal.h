@@ -176,6 +176,7 @@ struct WaveDev {
     const int32_t *slot_info2;
     double *xch;
     unsigned *xsync;
+    double *xvm;                // zeroed phases: per area [3][nn] |V| of the last sweep (the V_abc_list ranking)
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).

@@ -28,7 +28,10 @@
 // so a launch always drains.  The areas are reused round robin (COOP_NSLOT of
 // them); a scenario waits until the area's previous scenario has released it.
 //
-// Zeroed phases are declined on the host (the generic kernel runs them).
+// Zeroed phases as in the wave-block kernel (V = 0 on the phase, the loss over
+// PQL, the general V_abc_list extremes: both workgroups' |V| of the last sweep
+// through a scratch row, ranked in node order by workgroup 0); a live phase below
+// a zeroed one is declined on the host (the generic kernel runs it).
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
 #pragma unroll
         for (int c = 0; c < CC; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<false>(ldx(stg, p * PS + c * CL + tid), v[c][p]);
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(stg, p * PS + c * CL + tid), v[c][p]);   // 0 on a zeroed phase
 
         // ---- backward sweep (:134-160): this workgroup's prefix scan of IL
         double sc6[6], pre[6], tot6[6];
@@ -450,7 +453,10 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         for (int p = 0; p < 3; ++p) {
             const cx carry = g ? mk(tt[12 + 2 * p], tt[12 + 2 * p + 1]) : mk(0.0, 0.0);
 #pragma unroll
-            for (int c = 0; c < CC; ++c) v[c][p] = csub(ldx(OFF, p * nblk + (int)(sx[c] & 511u)), cadd(gd[c][p], carry));
+            for (int c = 0; c < CC; ++c) {
+                const cx vr = csub(ldx(OFF, p * nblk + (int)(sx[c] & 511u)), cadd(gd[c][p], carry));
+                v[c][p] = (FULL && ((si[c] >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
+            }
         }
 
         if (fin) {
@@ -476,7 +482,27 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
                     }
                 }
             }
-            const double x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
+            double xl = lp[0] + lp[1] + lp[2];
+            if (FULL && f.has_mask) {
+                // zeroed phases: the reference's loss over PQL (the loss identity needs
+                // every phase live): this workgroup's part of sum Re(V conj(IL)); |V| of
+                // its nodes to the scenario's scratch row for the general V_abc_list
+                // extremes (workgroup 0 ranks the whole feeder after the last exchange)
+                double *const xv = f.xvm + (size_t)slot * 3 * nn;
+                xl = 0.0;
+#pragma unroll
+                for (int c = 0; c < CC; ++c) {
+                    if ((si[c] >> 3) & 1) {
+                        const int k = f.slot_node[so + c * CL + tid];
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) {
+                            xl = fma(v[c][p].re, il[c][p].re, fma(v[c][p].im, il[c][p].im, xl));
+                            ast(xv + (size_t)p * nn + k, sqrt(fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im)));
+                        }
+                    }
+                }
+            }
+            const double x = seg_incl<64>(xl);
             mn = seg_reduce_min<64>(mn);
             mx = seg_reduce_max<64>(mx);
             if (lane == 63) {
@@ -512,6 +538,63 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         return;
     }
     if (alive) alive = coop_arrive(cnt, arrivals + 2, err, flag, true);
+    if (FULL && f.has_mask) {
+        // ---- zeroed phases, the general V_abc_list (V_abc_list.cpp:7-81,
+        // VoltVarCtrl.cpp:1201-1207): per phase the first K_p nonzero |V| in node
+        // order, zero padded.  Both workgroups' |V| into this workgroup's LDS (Sld
+        // is dead; every load in flight), then one wave per phase ranks 64 nodes a
+        // step by ballot; also min over every nonzero |V|^2 (the guard band)
+        double *const mag = (double *)stg;   // [3][nn]
+        double *const xv = f.xvm + (size_t)slot * 3 * nn;
+        for (int i0 = 0; i0 < 3 * nn; i0 += 8 * CL) {
+            double r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * CL + tid;
+                r[u] = i < 3 * nn ? ald(xv + i) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * CL + tid;
+                if (i < 3 * nn) mag[i] = r[u];
+            }
+        }
+        __syncthreads();
+        double mz = INFINITY;
+        for (int p = wv; p < 3; p += CW) {
+            const int K = f.K[p];
+            int cntk = 0;
+            double mn = INFINITY, mx = -INFINITY;
+            for (int k0 = 0; k0 < nn; k0 += 64) {
+                const int k = k0 + lane;
+                double m = 0.0;
+                if (k < nn) {
+                    if (k == 0) {
+                        const cx v0p = ldx(V0S, p);
+                        m = sqrt(fma(v0p.re, v0p.re, v0p.im * v0p.im));
+                    } else {
+                        m = mag[p * nn + k];
+                    }
+                }
+                const bool nz = k < nn && m != 0.0;
+                if (nz) mz = fmin(mz, m * m);
+                const unsigned long long bal = __ballot(nz);
+                const int rank = cntk + __popcll(bal & ((1ull << lane) - 1ull));
+                if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
+                cntk += __popcll(bal);
+            }
+            if (cntk < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+            mn = seg_reduce_min<64>(mn);
+            mx = seg_reduce_max<64>(mx);
+            if (lane == 63) {
+                tt[2 * p] = mn;
+                tt[2 * p + 1] = mx;
+            }
+        }
+        mz = seg_reduce_min<64>(mz);
+        if (lane == 63) tt[8 + wv] = mz;
+        __syncthreads();
+    }
     const bool agg = o.agg != nullptr;
     if (tid == 0) {
         double x = 0.0, mn = INFINITY, mx = -INFINITY, sa = 0.0;
@@ -541,10 +624,23 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         } else {
             conv = false;   // an exchange gave up (the error word is set): status 1
         }
-        const double m2min = mn;
-        x *= f.s3;
-        mn = sqrt(mn);
-        mx = sqrt(mx);
+        double m2min = mn;
+        if (FULL && f.has_mask) {
+            // PQb(0).re - sum_k PQL(k).re, V0 conj(Ib(0)) of the last sweep (fpf_wblk.hip)
+            double sb0 = 0.0;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sb0 += cmul(cmul(ldx(V0S, p), mk(f.s3, 0.0)), cconj(ibo[p])).re;
+            x = sb0 - f.s3 * x;
+            mn = fmin(fmin(tt[0], tt[2]), tt[4]);
+            mx = fmax(fmax(tt[1], tt[3]), tt[5]);
+            m2min = INFINITY;
+#pragma unroll
+            for (int w = 0; w < CW; ++w) m2min = fmin(m2min, tt[8 + w]);
+        } else {
+            x *= f.s3;
+            mn = sqrt(mn);
+            mx = sqrt(mx);
+        }
         if (o.iters) o.iters[s] = it + 1;
         if (o.status) o.status[s] = conv ? 0 : 1;
         if (o.loss) o.loss[s] = x;
@@ -633,9 +729,11 @@ size_t wcoop_lds_bytes(const WaveDev &w) {
 }
 
 hipError_t launch_wcoop(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
-    if (w.coop != 2 || w.wps != CW || w.C != CC || w.nblk > CL || w.bdepth > CBD || !w.xch || !w.xsync)
+    if (w.coop != 2 || w.wps != CW || w.C != CC || w.nblk > CL || w.bdepth > CBD || !w.xch || !w.xsync ||
+        (w.has_mask && !w.xvm) || w.has_rel)
         return hipErrorInvalidValue;
-    const bool full = o.vpolar || o.pqb || o.pql;
+    // the full-output variant keeps IL and Ib of the last sweep, and the zeroed-phase paths
+    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
     auto k = full ? dpf_wcoop_kernel<true> : dpf_wcoop_kernel<false>;
     static std::mutex mu;
     static std::set<std::array<int, 2>> attr_done;

@@ -130,12 +130,86 @@ def test_wcoop_16384_scenarios():
     np.testing.assert_allclose(wa[:3], ga[:3], rtol=1e-8)
 
 
-def test_wcoop_declines_zeroed_phases_and_larger_feeders():
-    """Zeroed phases above 2048 branches and feeders above 4096 branches stay on
-    the generic kernel (bit-identical to the oracle in exact mode, its own tests)."""
+def _single_phase_subtrees(n, seed):
+    """Synthetic feeder whose laterals 3 and 7 are phase-B-only with everything
+    below them (a phase-B-only line code on every row of the two subtrees, their
+    phase-A and -C loads removed): zeroed phases without a live phase below a
+    zeroed one -- the physical case (single-phase laterals)."""
+    f = F.synthetic_feeder(n, seed)
+    Dl = f.Dl.copy()
+    Z = np.vstack([f.Z, np.diag([0, 0.3 + 0.8j, 0])])
+    code = Z.shape[0] // 3
+    seps = np.flatnonzero(Dl[:, 0] == 0)
+    nn = int((Dl[:, 0] != 0).sum()) + 1
+    kids = [[] for _ in range(nn)]
+    row_of = {}
+    for m in range(Dl.shape[0]):
+        if Dl[m, 0] != 0:
+            kids[0 if m == 0 else int(Dl[m, 1])].append(int(Dl[m, 2]))
+            row_of[int(Dl[m, 2])] = m
+    for i in (3, 7):
+        st = [int(Dl[seps[i] + 1, 2])]
+        while st:
+            k = st.pop()
+            Dl[row_of[k], 3] = code
+            Dl[row_of[k], [6, 7, 10, 11]] = 0
+            st.extend(kids[k])
+    return F.Feeder(Dl, Z, name=f"synthetic-{n}bus-single-phase-laterals")
+
+
+@pytest.mark.parametrize("n", [3000, 4096])
+def test_wcoop_zeroed_phases(n):
+    """Zeroed phases on the paired kernel (single-phase laterals: a phase-B-only
+    line code on two laterals, DPF_return7.cpp:180-192): V = 0 on the zeroed
+    phases and the -180/+180 angle pattern, the loss over PQL, the general
+    V_abc_list extremes (Lnum_p + 1 < Nn: both workgroups' |V| ranked in node
+    order), against the oracle at the fast-mode bar."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    from test_gpu_parity import _fast_mode_outputs_match
+    from test_gpu_wblk import _close
+    f = _single_phase_subtrees(n, n)
+    pq = F.scenario_loads(f, np.arange(24), pv_frac=0.0)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (c["status"] == 0).all() and (c["Vpolar"][0::2] == 0).any()
+    nn = int((f.Dl[:, 0] != 0).sum()) + 1
+    assert min(O.lnum(f.Dl, f.Z)) + 1 < nn
+    pf = PowerFlow(f)
+    assert pf.kernel == "wave" and pf.info["tile"] == 1
+    r = pf.solve(pq)
+    assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+    assert _vrel(r["V_re"], r["V_im"], c["V_re"], c["V_im"]) <= 1e-10
+    _close(r["loss"], c["loss"], 1e-8)
+    np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
+    np.testing.assert_allclose(r["vmax"], c["vmax"], rtol=1e-10)
+    _fast_mode_outputs_match(r, c, c["status"] == 0)
+    # the light outputs (V + scalars) on the device, scenario-major
+    import torch
+    dev = torch.device("cuda:0")
+    pf1 = PowerFlow(f, layout=1)
+    B = pq.shape[2]
+    o = {"v_re": torch.empty((B, 3, pf1.nn), dtype=torch.float64, device=dev),
+         "v_im": torch.empty((B, 3, pf1.nn), dtype=torch.float64, device=dev),
+         "iters": torch.empty(B, dtype=torch.int32, device=dev),
+         "loss": torch.empty(B, dtype=torch.float64, device=dev),
+         "vmin": torch.empty(B, dtype=torch.float64, device=dev),
+         "vmax": torch.empty(B, dtype=torch.float64, device=dev)}
+    pf1.solve_device(torch.from_numpy(np.ascontiguousarray(pq.transpose(2, 0, 1))).to(dev), o)
+    torch.cuda.synchronize()
+    assert (o["iters"].cpu().numpy() == c["iters"]).all()
+    vr, vi = np.moveaxis(o["v_re"].cpu().numpy(), 0, -1), np.moveaxis(o["v_im"].cpu().numpy(), 0, -1)
+    assert _vrel(vr, vi, c["V_re"], c["V_im"]) <= 1e-10
+    np.testing.assert_allclose(o["vmin"].cpu().numpy(), c["vmin"], rtol=1e-10)
+    np.testing.assert_allclose(o["loss"].cpu().numpy(), c["loss"], rtol=1e-8)
+
+
+def test_wcoop_declines_restart_and_larger_feeders():
+    """A live phase below a zeroed one above 2048 branches and feeders above 4096
+    branches stay on the generic kernel (bit-identical to the oracle in exact
+    mode, its own tests)."""
     from freedm_amd import PowerFlow
     from test_gpu_wblk import _masked_feeder
-    assert PowerFlow(_masked_feeder(3000, 3000)).kernel == "generic"
+    assert PowerFlow(_masked_feeder(3000, 3000, restart=True)).kernel == "generic"
     assert PowerFlow(F.synthetic_feeder(4300, 4300)).kernel == "generic"
 
 
