@@ -2004,6 +2004,15 @@ int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf
     };
     rc = bring_back();
     if (rc) return rc;
+    if (f->wdev.coop) {
+        // the paired kernel's error word (a hand-off wait that gave up: its scenarios
+        // report status 1); the host API says so instead of returning silently
+        unsigned werr = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&werr, f->wdev.xsync + 2 * (size_t)f->wdev.coop_nslot, sizeof(werr),
+                                   hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (werr) return fail(ctx, FPF_ERR_HIP, "paired wave-block kernel: an exchange wait gave up");
+    }
     if (guarded && h_flag[0] > 0) {
         // some decisions fell within the guard band: re-solve those scenarios on the
         // exact kernel (results and aggregate in place), then bring everything back again
