@@ -66,3 +66,16 @@ def test_2048bus_plan():
     assert p["ok"] == 1 and (p["spw"], p["C"], p["wpb"]) == (1, 4, 8)
     assert 16 * 3 * (f.nl + 1) < p["lds"] <= 159 * 1024
     assert p["ncomp"] <= 510 and p["nblk"] <= 511
+
+
+def test_paired_plan_zeroed_phases():
+    """The paired kernel's plan (2049..4096 branches) accepts single-phase laterals
+    (zeroed phases with nothing live below them) and declines a live phase below
+    a zeroed one (the generic kernel runs it)."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_wcoop import _single_phase_subtrees
+    from test_gpu_wblk import _masked_feeder
+    p = _plan(_single_phase_subtrees(3000, 3000))
+    assert p["ok"] == 1 and (p["spw"], p["C"], p["wpb"]) == (1, 4, 8) and p["lds"] <= 159 * 1024
+    assert _plan(_masked_feeder(3000, 3000, restart=True))["ok"] == 0
