@@ -170,6 +170,31 @@ __device__ __forceinline__ bool coop_exchange(double2 *X, int XC, __amdgpu_buffe
 }
 }  // namespace
 
+#ifdef FPF_STAMPS
+// diagnostic build only (tools/coop_stamps.py): thread 0 of each of the first 64
+// workgroups records s_memtime at stage boundaries, [64][128]: 0 entry, 1 staged,
+// 2 area acquired, 4 + 8 it + k in sweep it < 14 (k = 0 top, 1 backward scan,
+// 2 backward exchange, 3 drops, 4 forward scan, 5 forward exchange, 6 V),
+// 120 after the loop, 121 workgroup 0's final wait
+__device__ unsigned long long *fpf_coop_stamp_buf = nullptr;
+__device__ unsigned fpf_coop_stamp_base = 0;   // the first recorded workgroup
+#define CSTAMP(idx)                                                                                    \
+    do {                                                                                               \
+        const unsigned w_ = blockIdx.x - fpf_coop_stamp_base;                                          \
+        if (fpf_coop_stamp_buf && threadIdx.x == 0 && w_ < 64u && (idx) < 128)                         \
+            fpf_coop_stamp_buf[w_ * 128 + (idx)] = __builtin_amdgcn_s_memtime();                        \
+    } while (0)
+extern "C" int fpf_debug_set_coop_stamp_buffer(void *dptr, unsigned base) {
+    unsigned long long *p = (unsigned long long *)dptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fpf_coop_stamp_base), &base, sizeof(base)) != hipSuccess) return -3;
+    return hipMemcpyToSymbol(HIP_SYMBOL(fpf_coop_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#define CSTAMP_IT(k) CSTAMP(it < 14 ? 4 + 8 * it + (k) : 999)
+#else
+#define CSTAMP(idx) ((void)0)
+#define CSTAMP_IT(k) ((void)0)
+#endif
+
 template <bool FULL>
 __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
     extern __shared__ double2 lds[];
@@ -178,6 +203,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
     const int b = blockIdx.x, g = (b >> 3) & 1;
     const int s = ((b >> 4) << 3) | (b & 7);   // this pair's scenario (members b, b + 8)
     if (s >= B) return;                        // (both members of a padding pair)
+    CSTAMP(0);
     const int nblk = f.nblk, nn = f.nn, nl = f.nl, XC = f.ncomp + 1, nbc = f.nb_c, nfc = f.nf_c;
     const int ntz = f.temp_sym ? 4 : 9;
     constexpr int PS = CC * CL + 1;   // Sld rows: slot c L + tid (row C L = 0)
@@ -258,7 +284,9 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
     }
     // the exchange area: free once its previous scenario (s - nslot) has released it
     const unsigned want = (unsigned)(s / f.coop_nslot);
+    CSTAMP(1);
     bool alive = coop_poll(gen, err, flag, [=](unsigned v) { return v == want; });
+    CSTAMP(2);
 
     cx v[CC][3];
 #pragma unroll
@@ -283,6 +311,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
     double dmin = INFINITY, err2_last = 0.0;
     unsigned arrivals = 0;   // this member's arrivals (both members: the same sequence)
     for (; alive; ++it) {
+        CSTAMP_IT(0);
         // ---- load currents (:106-130)
         cx il[CC][3], ib[CC][3];
 #pragma unroll
@@ -326,7 +355,9 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             }
         }
         arrivals += 2;
+        CSTAMP_IT(1);
         alive = coop_exchange(X, XC, rs, 8 * AH, 0, nbc, f.nb_split, g, tot6, tt, cnt, arrivals, err, flag) && alive;
+        CSTAMP_IT(2);
         cx tot[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -399,6 +430,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
                     lp[a] = fma(gd[c][a].re, ib[c][a].re, fma(gd[c][a].im, ib[c][a].im, lp[a]));
         }
 
+        CSTAMP_IT(3);
         // ---- forward sweep (:163-195): V = V0 - A, A = Ginc + off(block)
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -430,8 +462,10 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             }
         }
         arrivals += 2;
+        CSTAMP_IT(4);
         alive = coop_exchange(X, XC, rs, 8 * AH + 48 * nbc, 128, nfc, f.nf_split, g, tot6, tt + 12, cnt, arrivals, err,
                               flag) && alive;
+        CSTAMP_IT(5);
         // block offsets, one thread per block: V0 - off(b), off(b) = sum over b's
         // block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
         if (tid < nblk) {
@@ -459,6 +493,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             }
         }
 
+        CSTAMP_IT(6);
         if (fin) {
             // ---- the last sweep: V (and the full outputs) of this workgroup's nodes
             // straight from registers, its part of the loss and of the V extremes
@@ -514,6 +549,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         }
     }
     __syncthreads();
+    CSTAMP(120);
 
     // ---- the pair's results: workgroup 1 hands its sums over and leaves;
     // workgroup 0 writes the per-scenario results, releases the area, and joins
@@ -538,6 +574,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         return;
     }
     if (alive) alive = coop_arrive(cnt, arrivals + 2, err, flag, true);
+    CSTAMP(121);
     if (FULL && f.has_mask) {
         // ---- zeroed phases, the general V_abc_list (V_abc_list.cpp:7-81,
         // VoltVarCtrl.cpp:1201-1207): per phase the first K_p nonzero |V| in node
