@@ -1,7 +1,12 @@
 """Benchmark: converged power-flow scenarios/s on the 123-bus feeder (BASELINE.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+N > 1: bench.py starts N rank processes itself (one per GPU, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment) before
+anything touches a device, and exits with their status; under a launcher
+(python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N) the
+ranks come from the launcher's environment instead.
 
 Workload = BASELINE config 2: synthetic 123-bus feeder (seed 123), a batch of
 4096 seeded load/DER scenarios per GPU (weak scaling; scenario ids are global,
@@ -455,6 +460,59 @@ def _kernel_ms(torch, pf, d_pq, B, steps, warmup, stream, dev, want_v=True):
     return e0.elapsed_time(e1) / steps, out
 
 
+def rank_launch_specs(n: int, argv: list, port: int, base_env: dict | None = None) -> list:
+    """(command, environment) of each of the n rank processes `bench.py --gpus n`
+    starts when no launcher set WORLD_SIZE: the same script and arguments, one
+    rank per GPU (LOCAL_RANK r -> cuda:r), rendezvous on 127.0.0.1:port."""
+    env0 = dict(os.environ if base_env is None else base_env)
+    specs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        specs.append(([sys.executable, os.path.abspath(__file__)] + list(argv), env))
+    return specs
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """Start the n rank processes (rank_launch_specs) and wait for them; if one
+    fails the others are stopped (they would wait at a barrier).  Returns the
+    first non-zero exit status, else 0.  Called before this process imports
+    anything that initialises a GPU (device_count does not, on this image)."""
+    import subprocess
+    import torch
+    n_vis = torch.cuda.device_count()
+    gloo = os.environ.get("FPF_BENCH_BACKEND", "nccl") == "gloo"
+    if n > n_vis and not gloo:
+        print(f"bench.py: --gpus {n} but {n_vis} GPU(s) visible (FPF_BENCH_BACKEND=gloo rehearses more ranks "
+              "than GPUs on shared devices)", file=sys.stderr, flush=True)
+        return 2
+    procs = [subprocess.Popen(cmd, env=env) for cmd, env in rank_launch_specs(n, argv, _free_port())]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            q.kill()
+    return rc
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] == "--multi-leg":   # (bench.py's own child, _multi_leg_child)
         print(json.dumps(multi_leg(int(sys.argv[2]))), flush=True)
@@ -482,6 +540,14 @@ def main():
                          "the Infinity Cache cannot hold them; 1: re-solve one batch)")
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 throughput leg of the config-2 run")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, started here before any device is touched
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -616,6 +682,8 @@ def main():
             "value": value,
             "unit": "scenarios/s",
             "n_gpus": world,
+            "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "backend": backend if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,

@@ -13,7 +13,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libfreedm_pf.so")
 
-ABI_VERSION = 2   # include/freedm_pf.h FPF_ABI_VERSION
+ABI_VERSION = 3   # include/freedm_pf.h FPF_ABI_VERSION
 FPF_OK, FPF_ERR_ARG, FPF_ERR_TOPOLOGY, FPF_ERR_HIP, FPF_ERR_NOMEM, FPF_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
 FPF_CONVERGED, FPF_NONCONVERGED = 0, 1
 FPF_KERNEL_AUTO, FPF_KERNEL_GENERIC, FPF_KERNEL_TILED, FPF_KERNEL_WAVE = 0, 1, 2, 3
@@ -26,7 +26,7 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_multi_create", "fpf_multi_destroy", "fpf_multi_last_error", "fpf_multi_solve", "fpf_multi_get_feeder",
            "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_gradient_at", "fpf_vvc_round",
-           "fpf_vvc_gradient_batch"]
+           "fpf_vvc_gradient_batch", "fpf_feeder_check"]
 
 
 class FpfOpts(C.Structure):
@@ -112,6 +112,7 @@ def load(path: str | None = None):
     L.fpf_solve_batch.argtypes = [vp, C.c_int, _dp, C.POINTER(FpfOutputs), C.POINTER(FpfAggregate)]
     L.fpf_solve_batch_device.argtypes = [vp, C.c_int, vp, C.POINTER(FpfOutputs), vp, vp]
     L.fpf_aggregate_device.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp]
+    L.fpf_feeder_check.argtypes = [vp, vp]
     L.fpf_feeder_rtc_source.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
                                         C.c_char_p, C.c_size_t]
     L.fpf_feeder_rtc_source.restype = C.c_long
@@ -171,7 +172,7 @@ def load(path: str | None = None):
                                              C.POINTER(C.c_int8)]
         L.fpf_vvc_gradient_batch.restype = C.c_int
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
-                 "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device"):
+                 "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_check"):
         getattr(L, name).restype = C.c_int
     if L.fpf_abi_version() != ABI_VERSION:
         raise RuntimeError("libfreedm_pf ABI mismatch")

@@ -68,6 +68,7 @@ struct fpf_feeder {
     void *d_wave = nullptr;
     WaveDev wdev{}, wdev_big{};
     void *d_xch = nullptr, *d_xsync = nullptr, *d_xvm = nullptr;   // the paired wave-block kernel's exchange
+    unsigned *h_xerr = nullptr;   // its sticky fault word (pinned, coherent; the kernel sets it at system scope)
     // the partials + ticket scratch is shared by every aggregating launch on
     // this feeder (fused wave/specialised aggregate, fpf_aggregate_device): a
     // launch on another stream than the previous one first waits for it
@@ -111,6 +112,7 @@ static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
     if (ctx) ctx->err = msg;
     return code;
 }
+int fpf::feeder_fail(fpf_feeder *f, int code, const std::string &msg) { return fail(f ? f->ctx : nullptr, code, msg); }
 
 #define HIPCHK(ctx, expr)                                                                      \
     do {                                                                                       \
@@ -434,6 +436,9 @@ static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps
     const int L = 64 * wps, P = (n + 1) / 2;
     if (P > C * L || n - P > C * L) return no("paired wave-block kernel: more than 2 x 2048 positions");
     if (nblk > L || maxd > 6) return no("paired wave-block kernel: block chains beyond the register-resolved form");
+    // the kernel packs block (9 bits), forward index + 1 (14 bits) and line code (9
+    // bits) into one register per slot (fpf_wcoop.hip sx)
+    if (h.ncode > 512) return no("paired wave-block kernel: more than 512 line codes");
     std::vector<char> isb(n, 0), isf(n, 0);
     for (int q = 0; q < n; ++q) isb[q + size[at[q]] - 1] = 1;
     for (int b = 1; b < nblk; ++b) {
@@ -1518,6 +1523,23 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
             }
             w.xch = (double *)f->d_xch;
             w.xsync = (unsigned *)f->d_xsync;
+            // the sticky fault word: host memory the kernel writes when an exchange
+            // gives up, so the asynchronous entry reports it without a synchronisation
+            e = hipHostMalloc((void **)&f->h_xerr, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+            if (e != hipSuccess) {
+                fpf_feeder_destroy(f);
+                return fail(ctx, FPF_ERR_HIP, std::string("paired kernel fault word: ") + hipGetErrorString(e));
+            }
+            *(volatile unsigned *)f->h_xerr = 0;
+            e = hipHostGetDevicePointer((void **)&w.xerr_host, f->h_xerr, 0);
+            if (e != hipSuccess) {
+                fpf_feeder_destroy(f);
+                return fail(ctx, FPF_ERR_HIP, std::string("paired kernel fault word: ") + hipGetErrorString(e));
+            }
+            // polls before a hand-off wait gives up; FPF_TEST_COOP_SPIN (tests only)
+            // makes every wait give up at once to exercise the fault path
+            w.coop_spin = 1 << 21;
+            if (const char *sp = getenv("FPF_TEST_COOP_SPIN")) w.coop_spin = std::max(0, atoi(sp));
             if (wh.has_mask) {   // the zeroed phases' |V| rows (the V_abc_list ranking)
                 e = hipMalloc(&f->d_xvm, sizeof(double) * (size_t)w.coop_nslot * 3 * h.nn);
                 if (e != hipSuccess) {
@@ -1611,6 +1633,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_xch);
     (void)hipFree(f->d_xsync);
     (void)hipFree(f->d_xvm);
+    if (f->h_xerr) (void)hipHostFree(f->h_xerr);
     (void)hipFree(f->d_lay);
     (void)hipHostFree(f->h_stage);
     (void)hipFree(f->d_flag_count);
@@ -1742,8 +1765,28 @@ int fpf::fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const
     return FPF_OK;
 }
 
+// The paired kernel's sticky fault word (set by a launch whose exchange wait gave
+// up; its scenarios have status FPF_EXCHANGE_FAILED): FPF_ERR_EXCHANGE once, then clear
+int fpf::take_exchange_fault(fpf_feeder *f) {
+    if (!f || !f->h_xerr || !__atomic_load_n(f->h_xerr, __ATOMIC_ACQUIRE)) return FPF_OK;
+    __atomic_store_n(f->h_xerr, 0u, __ATOMIC_RELEASE);
+    return fail(f->ctx, FPF_ERR_EXCHANGE,
+                "paired wave-block kernel: an exchange wait gave up (scenarios with status FPF_EXCHANGE_FAILED)");
+}
+
+extern "C" int fpf_feeder_check(fpf_feeder *f, void *stream) {
+    if (!f) return FPF_ERR_ARG;
+    fpf_ctx *ctx = f->ctx;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return fpf::take_exchange_fault(f);
+}
+
 extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out,
                                       double *d_agg, void *stream) {
+    // an earlier launch's asynchronous fault is reported first (nothing enqueued)
+    const int rc = fpf::take_exchange_fault(f);
+    if (rc) return rc;
     return fpf::solve_batch_device_ex(f, n_scen, d_pq, d_out, d_agg, stream, nullptr, nullptr,
                                       f ? f->opts.layout : 0);
 }
@@ -2004,14 +2047,12 @@ int fpf::solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf
     };
     rc = bring_back();
     if (rc) return rc;
-    if (f->wdev.coop) {
-        // the paired kernel's error word (a hand-off wait that gave up: its scenarios
-        // report status 1); the host API says so instead of returning silently
-        unsigned werr = 0;
-        HIPCHK(ctx, hipMemcpyAsync(&werr, f->wdev.xsync + 2 * (size_t)f->wdev.coop_nslot, sizeof(werr),
-                                   hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        if (werr) return fail(ctx, FPF_ERR_HIP, "paired wave-block kernel: an exchange wait gave up");
+    // the paired kernel's fault word (a hand-off wait that gave up: those scenarios
+    // report FPF_EXCHANGE_FAILED, results are in place); the stream is synchronised
+    rc = fpf::take_exchange_fault(f);
+    if (rc) {
+        if (agg) std::memcpy(agg, h_agg, sizeof(h_agg));
+        return rc;
     }
     if (guarded && h_flag[0] > 0) {
         // some decisions fell within the guard band: re-solve those scenarios on the

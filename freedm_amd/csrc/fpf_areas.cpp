@@ -522,6 +522,13 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     if (u.v_re) AHIP(a, hipMemcpyAsync(u.v_re, a->d_vre, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost, st));
     if (u.v_im) AHIP(a, hipMemcpyAsync(u.v_im, a->d_vim, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost, st));
     AHIP(a, hipStreamSynchronize(st));
+    for (int ar : a->order) {   // a paired-kernel area whose exchange gave up (FPF_EXCHANGE_FAILED)
+        const int fr = take_exchange_fault(a->area[ar].feeder);
+        if (fr) {
+            a->err = "area " + std::to_string(ar) + ": " + fpf_last_error(a->ctx);
+            return fr;
+        }
+    }
     const int32_t *h_c = (const int32_t *)a->h_res;
     const bool conv = h_c[0] != 0;
     const int outer = h_c[1];

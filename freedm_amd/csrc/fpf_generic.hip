@@ -338,7 +338,7 @@ __global__ __launch_bounds__(1024) void dpf_aggregate_kernel(int B, int chunk, c
             nc += 1;
             if (vmax[s] > ub_v) no += 1;
             if (vmin[s] < lb_v) nu += 1;
-        } else {
+        } else if (status[s] == FPF_NONCONVERGED) {   // (not FPF_EXCHANGE_FAILED)
             nnc += 1;
         }
     }

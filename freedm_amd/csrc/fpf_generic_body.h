@@ -45,7 +45,7 @@ __device__ void block_aggregate(int lo, int hi, const int8_t *status, const doub
             nc += 1;
             if (vmax[s] > ub_v) no += 1;
             if (vmin[s] < lb_v) nu += 1;
-        } else {
+        } else if (status[s] == FPF_NONCONVERGED) {   // (not FPF_EXCHANGE_FAILED)
             nnc += 1;
         }
     }

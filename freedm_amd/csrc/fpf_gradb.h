@@ -36,6 +36,8 @@ struct GradPhaseDev {
 hipError_t launch_gradb_setup(const GradPhaseDev &P, int B, int c0, int nb, const double *vpolar, double *A,
                               double *rhs, int8_t *gstat, hipStream_t st);
 // lambda' = inv(J^T) Fx: LU with partial pivoting + solve per matrix (rhs overwritten)
+// whether the LU of an nf x nf system fits the kernel's LDS (nf <= 6400)
+bool gradb_lu_fits(int nf);
 hipError_t launch_gradb_lu(int nf, int nb, double *A, double *rhs, int8_t *sing, hipStream_t st);
 hipError_t launch_gradb_g(const GradPhaseDev &P, int c0, int nb, const double *sol, int ld, double *g, hipStream_t st);
 

@@ -177,6 +177,8 @@ struct WaveDev {
     double *xch;
     unsigned *xsync;
     double *xvm;                // zeroed phases: per area [3][nn] |V| of the last sweep (the V_abc_list ranking)
+    unsigned *xerr_host;        // sticky: set (system scope) when an exchange wait gave up; pinned host memory
+    int32_t coop_spin;          // polls before a wait gives up (2^21; FPF_TEST_COOP_SPIN overrides, tests only)
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
@@ -245,6 +247,11 @@ int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const f
 // the exact re-solve of the scenarios a deferred (d_flag_out) guarded solve flagged
 int fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                        void *stream, int layout);
+// record msg as the feeder's context's last error (fpf_last_error) and return code
+int feeder_fail(fpf_feeder *f, int code, const std::string &msg);
+// FPF_ERR_EXCHANGE (with the message) if the feeder's paired-kernel fault word is
+// set, clearing it; FPF_OK otherwise (fpf_api.cpp)
+int take_exchange_fault(fpf_feeder *f);
 // fpf_solve_batch in an explicit batch layout (internal callers build their own
 // batches in FPF_LAYOUT_SCEN_FASTEST whatever the feeder's fpf_opts.layout)
 int solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf_outputs *out, fpf_aggregate *agg,

@@ -420,6 +420,10 @@ extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const
             if (scal[i].host && nd > 0)
                 std::memcpy((char *)scal[i].host + (size_t)lo[d] * scal[i].esz, m->h_scal[d] + soff[i], nd * scal[i].esz);
     }
+    for (int d = 0; d < m->n; ++d) {   // a paired-kernel exchange that gave up (FPF_EXCHANGE_FAILED)
+        const int fr = fpf_feeder_check(m->feeder[d], (void *)m->stream[d]);
+        if (fr) return mfail(m, fr, std::string("device ") + std::to_string(d) + ": " + fpf_last_error(m->ctx[d]));
+    }
     fpf_aggregate a;
     a.loss_sum = h[8];
     a.vmin = h[16];

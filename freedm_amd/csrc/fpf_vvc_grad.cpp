@@ -527,7 +527,8 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
         !n_loads || ld < 1 || ncols < 12)
         return FPF_ERR_ARG;
     fpf_feeder_info in;
-    if (fpf_feeder_get_info(feeder, &in) != FPF_OK || in.nl != nl) return FPF_ERR_ARG;
+    if (fpf_feeder_get_info(feeder, &in) != FPF_OK || in.nl != nl)
+        return fpf::feeder_fail(feeder, FPF_ERR_ARG, "fpf_vvc_gradient_batch: ctrl_dl rows differ from the feeder's");
     if (n_scen == 0) return 0;
     const int B = n_scen, nn = in.nn;
     const size_t b = (size_t)B;
@@ -538,13 +539,19 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
             const bool c = (int)ctrl_dl[(size_t)(6 + 2 * x) * nl + i] != 0;
             const double *row = pq + ((size_t)(2 * x) * nl + i) * b;
             for (int s = 0; s < B; ++s)
-                if (((int)row[s] != 0) != c) return FPF_ERR_ARG;
+                if (((int)row[s] != 0) != c)
+                    return fpf::feeder_fail(feeder, FPF_ERR_ARG,
+                                            "fpf_vvc_gradient_batch: scenario " + std::to_string(s) + ", row " +
+                                                std::to_string(i) + ", phase " + std::to_string(x) +
+                                                ": its (int) load test differs from ctrl_dl's (VoltVarCtrl.cpp:354-398)");
         }
     const double bkva = fpf_feeder_bkva(feeder), bkv = fpf_feeder_bkv(feeder);
     hipStream_t st = nullptr;
-#define GCHK(expr)                                      \
-    do {                                                \
-        if ((expr) != hipSuccess) return FPF_ERR_HIP;   \
+#define GCHK(expr)                                                                                      \
+    do {                                                                                                \
+        const hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                           \
+            return fpf::feeder_fail(feeder, FPF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
     // ---- the base solves (VoltVarCtrl.cpp:1141), scenario fastest
     DevBuf d_pq, d_vp, d_it, d_stt, d_loss, d_vmin, d_vmax, d_gst;
@@ -576,6 +583,8 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
     GCHK(hipMemcpy(h_loss.data(), d_loss.p, sizeof(double) * b, hipMemcpyDeviceToHost));
     GCHK(hipMemcpy(h_vmin.data(), d_vmin.p, sizeof(double) * b, hipMemcpyDeviceToHost));
     GCHK(hipMemcpy(h_vmax.data(), d_vmax.p, sizeof(double) * b, hipMemcpyDeviceToHost));
+    rc = fpf::take_exchange_fault(feeder);   // (the copies above synchronised the device)
+    if (rc) return rc;
     int s0 = -1;
     for (int s = 0; s < B && s0 < 0; ++s)
         if (h_st[s] == FPF_CONVERGED) s0 = s;
@@ -599,7 +608,13 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
     GradPlan plan;
     std::string err;
     rc = build_plan(Table{ctrl_dl, nl}, ncols, z, z_rows, vp0.data(), nn, bkva, bkv, plan, &err);
-    if (rc != FPF_OK) return rc;
+    if (rc != FPF_OK) return fpf::feeder_fail(feeder, rc, "fpf_vvc_gradient_batch: " + err);
+    for (int x = 0; x < 3; ++x)   // the device LU keeps two rows of the matrix in LDS
+        if (!fpf::gradb_lu_fits(2 * plan.ph[x].lnum))
+            return fpf::feeder_fail(feeder, FPF_ERR_UNSUPPORTED,
+                                    "fpf_vvc_gradient_batch: phase " + std::to_string(x) + " has " +
+                                        std::to_string(plan.ph[x].lnum) +
+                                        " load nodes; the device LU holds at most 3200 (fpf_vvc_gradient runs it)");
     GCHK(hipMemcpy(d_gst.p, h_gst.data(), b, hipMemcpyHostToDevice));
     DevBuf d_g;
     GCHK(hipMalloc(&d_g.p, sizeof(double) * b * 3 * ld));

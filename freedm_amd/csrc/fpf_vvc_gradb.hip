@@ -249,9 +249,11 @@ __global__ __launch_bounds__(LU_NT) void gradb_lu_kernel(int nf, double *__restr
 }
 }  // namespace
 
+bool gradb_lu_fits(int nf) { return (2 * sizeof(double) + 2 * sizeof(int)) * (size_t)nf <= 150 * 1024; }
+
 hipError_t launch_gradb_lu(int nf, int nb, double *A, double *rhs, int8_t *sing, hipStream_t st) {
     const size_t lds = (2 * sizeof(double) + 2 * sizeof(int)) * (size_t)nf;
-    if (lds > 150 * 1024) return hipErrorInvalidValue;   // nf <= 6400 (feeders of ~3200 buses)
+    if (!gradb_lu_fits(nf)) return hipErrorInvalidValue;   // nf <= 6400 (feeders of ~3200 buses)
     if (lds > 64 * 1024) {
         // dynamic LDS above the default 64 KiB: a per-device setting
         static std::mutex mu;

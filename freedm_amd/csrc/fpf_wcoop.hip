@@ -24,7 +24,8 @@
 // stores, then adds one to the area's arrival count; the other polls the count
 // (thread 0, with s_sleep between polls) and reads with agent-scope loads.  A wait
 // gives up after a bounded number of polls (the error word is set, every
-// workgroup of the launch stops at its next wait, the scenario reports status 1),
+// workgroup of the launch stops at its next wait, the scenario reports status
+// FPF_EXCHANGE_FAILED and the feeder's sticky host word is set),
 // so a launch always drains.  The areas are reused round robin (COOP_NSLOT of
 // them); a scenario waits until the area's previous scenario has released it.
 //
@@ -49,7 +50,6 @@ constexpr int CW = 8;                  // wavefronts per workgroup
 constexpr int CC = 4;                  // slots per lane
 constexpr int CL = 64 * CW;            // lanes (= threads) per workgroup
 constexpr int CBD = 6;                 // block-chain depth resolved from registers (the host checks)
-constexpr int SPIN = 1 << 21;          // polls before a wait gives up
 constexpr int AH = 48;                 // area header: backward totals [2][8], forward [2][8], final [2][8]
 
 __device__ __forceinline__ int ci_store_b(unsigned x) { return (int)((x >> 4) & 16383u) - 1; }
@@ -62,10 +62,10 @@ __device__ __forceinline__ double ald(double *p) { return __hip_atomic_load(p, _
 // thread 0 polls *w until pred(*w) (or the error word is set, or the polls run
 // out: then it sets the error word); the verdict is broadcast through LDS
 template <typename Pred>
-__device__ __forceinline__ bool coop_poll(unsigned *w, unsigned *err, int *flag, Pred pred) {
+__device__ __forceinline__ bool coop_poll(unsigned *w, unsigned *err, int *flag, int spin, Pred pred) {
     if (threadIdx.x == 0) {
         int ok = 0;
-        for (int i = 0; i < SPIN; ++i) {
+        for (int i = 0; i < spin; ++i) {
             if (pred(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 ok = 1;
                 break;
@@ -82,12 +82,13 @@ __device__ __forceinline__ bool coop_poll(unsigned *w, unsigned *err, int *flag,
 
 // every thread's area stores complete, then one arrival; wait: until both
 // members have arrived `target` times in total
-__device__ __forceinline__ bool coop_arrive(unsigned *cnt, unsigned target, unsigned *err, int *flag, bool wait) {
+__device__ __forceinline__ bool coop_arrive(unsigned *cnt, unsigned target, unsigned *err, int *flag, int spin,
+                                            bool wait) {
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!wait) return true;
-    return coop_poll(cnt, err, flag, [=](unsigned c) { return c >= target; });
+    return coop_poll(cnt, err, flag, spin, [=](unsigned c) { return c >= target; });
 }
 
 // The exchange area through a buffer resource: 16-byte sc1 (write-through)
@@ -112,7 +113,7 @@ __device__ __forceinline__ d2v bld(__amdgpu_buffer_rsrc_t r, int off) {
 // 0's total; both totals to tt (T0 re/im per phase, then T1)
 __device__ __forceinline__ bool coop_exchange(double2 *X, int XC, __amdgpu_buffer_rsrc_t r, int xoff, int toff, int n,
                                               int split, int g, const double (&tot6)[6], double *tt, unsigned *cnt,
-                                              unsigned target, unsigned *err, int *flag) {
+                                              unsigned target, unsigned *err, int *flag, int spin) {
     const int tid = threadIdx.x;
     __syncthreads();   // (the owned entries are in X)
     const int lo = g ? split : 0, own = g ? n - split : split;
@@ -127,7 +128,7 @@ __device__ __forceinline__ bool coop_exchange(double2 *X, int XC, __amdgpu_buffe
     }
     // (a wait that gave up reads garbage and the caller finishes the sweep with it:
     // no early exit in the sweep loop)
-    const bool ok = coop_arrive(cnt, target, err, flag, true);
+    const bool ok = coop_arrive(cnt, target, err, flag, spin, true);
     // workgroup 0's total (the carry) loaded beside the entries (every load of a
     // thread in flight at once: the hand-off costs one load latency)
     d2v t0[3];
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
     // ---- this workgroup's slots: their loads P/Q (column s of pq, or its block in
     // the scenario-major layout) into Sld scaled by 1/(bkva/3) (DPF_return7.cpp:46-50)
     unsigned si[CC];
-    unsigned sx[CC];   // bits 0-8 block, 9-22 forward index + 1, 23-31 code * ntz (the host checks the widths)
+    unsigned sx[CC];   // bits 0-8 block, 9-22 forward index + 1, 23-31 line code (< 512: analyse_coop checks the widths)
     double sabs = 0.0;   // the guard record: sum |S_k|_1 over the slots
     {
         const double inv_s3 = 1.0 / f.s3;
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         for (int c = 0; c < CC; ++c) {
             si[c] = (unsigned)f.slot_info[so + c * CL + tid];
             sx[c] = (unsigned)f.slot_blk[so + c * CL + tid] | ((unsigned)f.slot_info2[so + c * CL + tid] << 9) |
-                    ((unsigned)(f.slot_code[so + c * CL + tid] * ntz) << 23);
+                    ((unsigned)f.slot_code[so + c * CL + tid] << 23);
         }
     }
     for (int i = tid; i < f.ncode * ntz; i += CL) zc[i] = ld_global2(f.code_z, i);
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
     // the exchange area: free once its previous scenario (s - nslot) has released it
     const unsigned want = (unsigned)(s / f.coop_nslot);
     CSTAMP(1);
-    bool alive = coop_poll(gen, err, flag, [=](unsigned v) { return v == want; });
+    bool alive = coop_poll(gen, err, flag, f.coop_spin, [=](unsigned v) { return v == want; });
     CSTAMP(2);
 
     cx v[CC][3];
@@ -356,7 +357,8 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         }
         arrivals += 2;
         CSTAMP_IT(1);
-        alive = coop_exchange(X, XC, rs, 8 * AH, 0, nbc, f.nb_split, g, tot6, tt, cnt, arrivals, err, flag) && alive;
+        alive = coop_exchange(X, XC, rs, 8 * AH, 0, nbc, f.nb_split, g, tot6, tt, cnt, arrivals, err, flag, f.coop_spin) &&
+                alive;
         CSTAMP_IT(2);
         cx tot[3];
 #pragma unroll
@@ -395,7 +397,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         if (f.temp_sym) {
 #pragma unroll
             for (int c = 0; c < CC; ++c) {
-                const int czc = (int)(sx[c] >> 23);
+                const int czc = (int)(sx[c] >> 23) * 4;
                 const double lgc = f.slot_lng[so + c * CL + tid];
                 const cx m = ldx(zc, czc + 3);
                 const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             for (int c = 0; c < CC; ++c) {
                 cx tm[9];
 #pragma unroll
-                for (int j = 0; j < 9; ++j) tm[j] = ldx(zc, (int)(sx[c] >> 23) + j);
+                for (int j = 0; j < 9; ++j) tm[j] = ldx(zc, (int)(sx[c] >> 23) * 9 + j);
                 const double lgc = f.slot_lng[so + c * CL + tid];
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         arrivals += 2;
         CSTAMP_IT(4);
         alive = coop_exchange(X, XC, rs, 8 * AH + 48 * nbc, 128, nfc, f.nf_split, g, tot6, tt + 12, cnt, arrivals, err,
-                              flag) && alive;
+                              flag, f.coop_spin) && alive;
         CSTAMP_IT(5);
         // block offsets, one thread per block: V0 - off(b), off(b) = sum over b's
         // block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
@@ -570,10 +572,10 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             ast(A + 42, mx);
             ast(A + 43, sa);
         }
-        if (alive) coop_arrive(cnt, 0, err, flag, false);
+        if (alive) coop_arrive(cnt, 0, err, flag, f.coop_spin, false);
         return;
     }
-    if (alive) alive = coop_arrive(cnt, arrivals + 2, err, flag, true);
+    if (alive) alive = coop_arrive(cnt, arrivals + 2, err, flag, f.coop_spin, true);
     CSTAMP(121);
     if (FULL && f.has_mask) {
         // ---- zeroed phases, the general V_abc_list (V_abc_list.cpp:7-81,
@@ -659,7 +661,11 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(gen, want + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            conv = false;   // an exchange gave up (the error word is set): status 1
+            // an exchange gave up (the launch's error word is set): the scenario's
+            // status is FPF_EXCHANGE_FAILED, never a non-convergence, and the
+            // feeder's sticky word (host memory) tells the host API
+            conv = false;
+            if (f.xerr_host) __hip_atomic_store(f.xerr_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         double m2min = mn;
         if (FULL && f.has_mask) {
@@ -679,7 +685,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
             mx = sqrt(mx);
         }
         if (o.iters) o.iters[s] = it + 1;
-        if (o.status) o.status[s] = conv ? 0 : 1;
+        if (o.status) o.status[s] = conv ? 0 : (alive ? 1 : 3);
         if (o.loss) o.loss[s] = x;
         if (o.errmx) o.errmx[s] = sqrt(err2_last);
         if (o.flag_count) {
@@ -715,7 +721,7 @@ __global__ __launch_bounds__(CL, 2) void dpf_wcoop_kernel(WaveDev f, int B, cons
         }
         if (agg) {
             const double part[8] = {conv ? x : 0.0, conv ? mn : INFINITY, conv ? mx : -INFINITY, conv ? 1.0 : 0.0,
-                                    conv ? 0.0 : 1.0, conv && mx > f.ub_v ? 1.0 : 0.0, conv && mn < f.lb_v ? 1.0 : 0.0,
+                                    conv || !alive ? 0.0 : 1.0, conv && mx > f.ub_v ? 1.0 : 0.0, conv && mn < f.lb_v ? 1.0 : 0.0,
                                     1.0};
             double *dst = o.partials + 8 * (size_t)s;
             for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

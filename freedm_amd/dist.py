@@ -56,8 +56,9 @@ def aggregate_results(status, loss, vmin, vmax, lb_v: float = 0.96, ub_v: float 
     conv = status == 0
     vmin = np.asarray(vmin)[conv]
     vmax = np.asarray(vmax)[conv]
+    # n_nonconv: status FPF_NONCONVERGED (1) only; FPF_EXCHANGE_FAILED (3) is neither
     return np.array([np.asarray(loss)[conv].sum(), vmin.min(initial=np.inf), vmax.max(initial=-np.inf),
-                     conv.sum(), (~conv).sum(), (vmax > ub_v).sum(), (vmin < lb_v).sum(), status.size],
+                     conv.sum(), (status == 1).sum(), (vmax > ub_v).sum(), (vmin < lb_v).sum(), status.size],
                     dtype=np.float64)
 
 

@@ -21,7 +21,8 @@ import numpy as np
 from . import _lib
 from .feeder import Feeder
 
-__all__ = ["PowerFlow", "MultiPowerFlow", "AreaPowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError"]
+__all__ = ["PowerFlow", "MultiPowerFlow", "AreaPowerFlow", "VPQ", "DPF_return7", "DPFError", "NonConvergedError",
+           "ExchangeError", "FPF_EXCHANGE_FAILED"]
 
 
 class DPFError(RuntimeError):
@@ -30,6 +31,27 @@ class DPFError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"fpf error {code}: {msg}")
         self.code = code
+
+
+FPF_ERR_EXCHANGE = -6       # include/freedm_pf.h
+FPF_EXCHANGE_FAILED = 3     # per-scenario status: a paired-kernel exchange gave up
+
+
+class ExchangeError(DPFError):
+    """A paired-kernel exchange wait gave up (FPF_ERR_EXCHANGE; feeders of
+    2049..4096 branches, two workgroups per scenario): the scenarios concerned
+    have status FPF_EXCHANGE_FAILED (3).  `results` holds the batch's outputs
+    when the host entry raised it."""
+
+    def __init__(self, code: int, msg: str, results: dict | None = None):
+        super().__init__(code, msg)
+        self.results = results
+
+
+def _raise(rc: int, msg: str, results: dict | None = None):
+    if rc == FPF_ERR_EXCHANGE:
+        raise ExchangeError(rc, msg, results)
+    raise DPFError(rc, msg)
 
 
 class NonConvergedError(DPFError):
@@ -158,7 +180,8 @@ class PowerFlow:
         agg = _lib.FpfAggregate()
         rc = L.fpf_solve_batch(self.h, B, pq.ctypes.data_as(_lib._dp), C.byref(out), C.byref(agg))
         if rc < 0:
-            raise DPFError(rc, self.ctx.err())
+            r["aggregate"] = agg.as_dict()
+            _raise(rc, self.ctx.err(), r)
         r["n_nonconv"] = rc
         r["aggregate"] = agg.as_dict()
         return r
@@ -179,7 +202,18 @@ class PowerFlow:
             st = stream if isinstance(stream, int) else int(stream.cuda_stream)
         rc = L.fpf_solve_batch_device(self.h, B, _ptr(pq), C.byref(o), _ptr(agg), st)
         if rc < 0:
-            raise DPFError(rc, self.ctx.err())
+            _raise(rc, self.ctx.err())
+
+    def check(self, stream=None) -> None:
+        """fpf_feeder_check: wait for the stream, then raise ExchangeError if a
+        paired-kernel launch on this feeder gave up an exchange since the last
+        report (asynchronous faults of solve_device)."""
+        st = None
+        if stream is not None:
+            st = stream if isinstance(stream, int) else int(stream.cuda_stream)
+        rc = _lib.load().fpf_feeder_check(self.h, st)
+        if rc < 0:
+            _raise(rc, self.ctx.err())
 
     def bind_device(self, pq, out: dict, agg=None, stream=None):
         """Pre-bind the ctypes arguments of a device solve (and optional aggregate)
@@ -201,7 +235,7 @@ class PowerFlow:
             aggregate is produced by the same launch (specialised kernel)."""
             rc = fs(h, B, pq_p, o_ref, None if agg is None else C.c_void_p(_ptr(agg)), st)
             if rc < 0:
-                raise DPFError(rc, self.ctx.err())
+                _raise(rc, self.ctx.err())
 
         def aggregate(dst):
             rc = fa(h, B, C.c_void_p(_ptr(out["status"])), C.c_void_p(_ptr(out["loss"])), C.c_void_p(_ptr(out["vmin"])),

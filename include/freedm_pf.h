@@ -48,7 +48,8 @@
 extern "C" {
 #endif
 
-#define FPF_ABI_VERSION 2   /* 2: fpf_outputs.errmx / .guard, fpf_opts.no_guard */
+#define FPF_ABI_VERSION 3   /* 2: fpf_outputs.errmx / .guard, fpf_opts.no_guard;
+                               3: FPF_EXCHANGE_FAILED, FPF_ERR_EXCHANGE, fpf_feeder_check */
 
 /* return codes */
 #define FPF_OK               0
@@ -58,12 +59,21 @@ extern "C" {
 #define FPF_ERR_HIP         -3   /* HIP runtime failure                                    */
 #define FPF_ERR_NOMEM       -4
 #define FPF_ERR_UNSUPPORTED -5   /* requested kernel cannot run this feeder               */
+#define FPF_ERR_EXCHANGE    -6   /* a paired-kernel exchange wait gave up (feeders of     */
+                                 /* 2049..4096 branches: two workgroups per scenario hand */
+                                 /* their scan values over through L2); the scenarios     */
+                                 /* concerned have status FPF_EXCHANGE_FAILED             */
 
 /* per-scenario status */
 #define FPF_CONVERGED        0
 #define FPF_NONCONVERGED     1   /* no errmx < eps within mxitr sweeps; the reference     */
                                  /* throws (DPF_return7.cpp:100-101,242); we return the   */
                                  /* state after the last sweep                            */
+#define FPF_EXCHANGE_FAILED  3   /* not a solve outcome: the two workgroups of a paired-  */
+                                 /* kernel scenario could not exchange (a hardware or     */
+                                 /* dispatch fault); V is not a result.  Counted neither  */
+                                 /* as converged nor as non-converged in fpf_aggregate    */
+                                 /* (n_scen - n_conv - n_nonconv of them)                 */
 
 /* kernel selection */
 #define FPF_KERNEL_AUTO      0   /* fast mode: wave if the feeder allows it; then tiled   */
@@ -104,8 +114,11 @@ typedef struct fpf_opts {
                           Ib(0) in another order than the reference, so a scenario whose
                           errmx lands within the rounding band of eps at some sweep could
                           stop one sweep apart from it (DPF_return7.cpp:199-210).  Such
-                          scenarios are flagged in the kernel (band: 4 (Nb + 16) 2^-53
-                          sum_k |IL_k|_1, the scan's worst-case rounding difference) and
+                          scenarios are flagged in the kernel (band: 4 (Nb + 24) 2^-53
+                          sum_k |IL_k|_1, the scan's worst-case rounding difference, with
+                          sum_k |IL_k|_1 bounded by 1.25 sqrt(2) sum_k |S_k|_1 / min|V|
+                          where the kernel forms it from the loads; fpf_api.cpp
+                          guard_factor) and
                           re-solved on the exact kernel, whose decisions are the reference's
                           order of operations.  1: no guard (diagnostics). */
     int    reserved[3];
@@ -158,7 +171,7 @@ typedef struct fpf_aggregate {
     double vmin;       /* min over converged scenarios                 */
     double vmax;       /* max over converged scenarios                 */
     double n_conv;
-    double n_nonconv;
+    double n_nonconv;  /* status FPF_NONCONVERGED (FPF_EXCHANGE_FAILED is neither)        */
     double n_over;     /* converged with vmax > ub_v                   */
     double n_under;    /* converged with vmin < lb_v                   */
     double n_scen;
@@ -199,9 +212,17 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
  * produce no aggregate; the generic and tiled kernels' scratch and layout
  * buffers and the guard's flag list belong to the feeder, so any other mix must
  * share one stream (or be serialised by the caller).
- * Returns FPF_OK or an error (the non-converged count is in d_agg / status). */
+ * Returns FPF_OK or an error (the non-converged count is in d_agg / status).
+ * Asynchronous faults: a paired-kernel launch whose exchange gave up sets a
+ * sticky word of the feeder; the next fpf_solve_batch_device or
+ * fpf_feeder_check on the feeder returns FPF_ERR_EXCHANGE (and clears it)
+ * without enqueueing anything. */
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);
+/* Wait for `stream` (a hipStream_t, NULL = the default stream), then report the
+ * feeder's asynchronous faults: FPF_ERR_EXCHANGE if a paired-kernel launch on it
+ * gave up an exchange since the last report (the word is cleared), else FPF_OK. */
+int         fpf_feeder_check(fpf_feeder *feeder, void *stream);
 
 /* ---- Multi-GPU study: one process, n GPUs of a node.
  * fpf_multi_create uploads the feeder to devices 0..n_gpus-1 (one context,
@@ -347,7 +368,9 @@ int         fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, const 
  * Carlo over load scenarios): scenario s is ctrl_dl with its load columns 6..11
  * replaced by pq[.][.][s] (host, [6][Nl][n_scen], scenario fastest).  The base
  * solves, the V lists, Fx, J (long double sums as double-double), the LU solves
- * (rocSOLVER batched getrf/getrs, partial pivoting) and g run on the device; Y,
+ * (a hand-written batched LU with partial pivoting, one workgroup per matrix, its
+ * pivot row and column in LDS: at most 3200 load nodes per phase) and g run on
+ * the device; Y,
  * the branch lists and the load lists are shared.  Every scenario's (int) load
  * tests (columns 6, 8, 10) must equal ctrl_dl's (else FPF_ERR_ARG): they fix the
  * load lists.  g [n_scen][3][ld]; load_nodes [3][ld] and n_loads [3] (shared);
@@ -355,8 +378,9 @@ int         fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, const 
  * Vmax_orig, sweeps; gstatus [n_scen]: 0 ok, 1 the base solve did not converge
  * (the reference throws), 2 singular J, 3 V_abc_list rows differ from the first
  * converged scenario's (g and stats[0..3] are 0 unless 0).  Returns the number
- * of scenarios with gstatus != 0, or FPF_ERR_* (FPF_ERR_UNSUPPORTED: no
- * librocsolver). */
+ * of scenarios with gstatus != 0, or FPF_ERR_* (FPF_ERR_UNSUPPORTED: a phase
+ * with more than 3200 load nodes -- fpf_vvc_gradient solves those on the host;
+ * FPF_ERR_EXCHANGE: a paired-kernel base solve's exchange gave up). */
 int         fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
                                    const double *z, int z_rows, int z_cols, int n_scen, const double *pq,
                                    double beta0, int ld, double *g, double *load_nodes, int *n_loads,

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_and_reports_abi():
     from freedm_amd import _lib
     L = ctypes.CDLL(_lib.LIB_PATH)
-    assert L.fpf_abi_version() == 2
+    assert L.fpf_abi_version() == 3
     o = _lib.FpfOpts()
     L.fpf_opts_default(ctypes.byref(o))
     assert (o.bkva, o.bkv, o.eps, o.mxitr) == (1000.0, 12.47, 1e-4, 20)

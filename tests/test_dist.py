@@ -78,24 +78,59 @@ def test_world2_gloo_study_aggregate():
     assert got[0][7] == N_STUDY and got[0][3] + got[0][4] == N_STUDY
 
 
-@pytest.mark.gpu
-def test_bench_two_ranks_share_one_gpu():
-    """bench.py's multi-rank path with the HIP kernels: 2 ranks over gloo on the
-    box's GPU (ranks beyond the visible GPUs share them); the study aggregate
-    covers both ranks' shards."""
-    import json
-    import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_rank_launch_specs():
+    """`bench.py --gpus 8` without a launcher starts 8 rank processes itself: the
+    same script and arguments, RANK = LOCAL_RANK = r (cuda:r), WORLD_SIZE 8, one
+    rendezvous on 127.0.0.1 (no device touched by the parent)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    specs = bench.rank_launch_specs(8, argv, 29555, base_env={"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert len(specs) == 8
+    for r, (cmd, env) in enumerate(specs):
+        assert cmd[0] == sys.executable and cmd[1] == os.path.join(ROOT, "bench.py") and cmd[2:] == argv
+        assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"]) == (str(r), str(r), "8")
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29555"
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """--gpus N with fewer visible GPUs (none here) fails non-zero instead of
+    benching fewer GPUs, unless FPF_BENCH_BACKEND=gloo asks for a rehearsal; a
+    launcher's WORLD_SIZE that disagrees with --gpus fails too."""
     import subprocess
     import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FPF_BENCH_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2", "--steps", "3",
-           "--warmup", "1", "--no-c4", "--no-cpu-baseline", "--in-batches", "1"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FPF_BENCH_BACKEND")}
+    env["HIP_VISIBLE_DEVICES"] = ""   # (no GPU in this container anyway; on a GPU box: none visible)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 2 and "visible" in r.stderr, r.stderr[-2000:]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, env=dict(env, WORLD_SIZE="4"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr, r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_share_one_gpu():
+    """`bench.py --gpus 2` exactly as the driver runs it (no launcher: bench.py
+    starts its two ranks itself), over gloo so the two ranks can share the box's
+    one GPU: n_gpus and the world each rank saw are 2, and the study aggregate
+    covers both ranks' shards."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FPF_BENCH_BACKEND"] = "gloo"
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-c4", "--no-cpu-baseline",
+           "--in-batches", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2
+    assert d["n_gpus"] == 2 and d["rccl_world"] == 2
     agg = d["aggregate"]
     assert agg["n_scen"] == 2 * 3 * 4096 and agg["n_conv"] == agg["n_scen"]

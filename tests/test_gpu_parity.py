@@ -310,6 +310,72 @@ def test_fast_mode_full_batches_against_oracle(kernel):
         np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
 
 
+def test_config4_wave_full_size():
+    """BASELINE config 4 at the size the bench runs it: one GPU's 131 072-scenario
+    shard of the hosting study (seed 2^20), scenario major, in one launch of the
+    wave kernel with light outputs (V + scalars) and the fused aggregate; every
+    scenario against the exact generic kernel on the same device inputs
+    (iteration counts and status identical, V 1e-10, loss 1e-8, Vmin/Vmax 1e-10,
+    the aggregate's counts equal) and a strided sample against the oracle
+    (DPF_return7.cpp:199-217: the sweep count is the reference's)."""
+    import torch
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = F.synthetic_feeder(123, 123)
+    B = 131072
+    dev = torch.device("cuda:0")
+    d_pq = torch.empty((B, 6, f.nl), dtype=torch.float64, device=dev)
+    for a in range(0, B, 16384):
+        d_pq[a:a + 16384] = torch.from_numpy(
+            F.hosting_loads(f, np.arange(a, a + 16384), seed=1 << 20).transpose(2, 0, 1).copy()).to(dev)
+
+    def run(pf):
+        nn = pf.nn
+        out = {"v_re": torch.empty((B, 3, nn), dtype=torch.float64, device=dev),
+               "v_im": torch.empty((B, 3, nn), dtype=torch.float64, device=dev),
+               "iters": torch.empty(B, dtype=torch.int32, device=dev),
+               "status": torch.empty(B, dtype=torch.int8, device=dev),
+               "loss": torch.empty(B, dtype=torch.float64, device=dev),
+               "vmin": torch.empty(B, dtype=torch.float64, device=dev),
+               "vmax": torch.empty(B, dtype=torch.float64, device=dev)}
+        agg = torch.zeros(8, dtype=torch.float64, device=dev)
+        pf.solve_device(d_pq, out, agg=agg)
+        torch.cuda.synchronize()
+        return out, agg.cpu().numpy()
+
+    fast = PowerFlow(f, device=0, layout=1)
+    assert fast.kernel == "wave"
+    w, wa = run(fast)
+    assert wa[7] == B and wa[3] + wa[4] == B
+    it = w["iters"].cpu().numpy()
+    assert len(set(it.tolist())) >= 2   # mixed sweep counts within wavefronts
+    idx = np.arange(0, B, 1021)
+    ti = torch.from_numpy(idx).to(dev)
+    pq_s = np.ascontiguousarray(d_pq[ti].cpu().numpy().transpose(1, 2, 0))
+    c = O.dpf_batch(f.Dl, f.Z, pq_s, nthreads=8)
+    assert (it[idx] == c["iters"]).all() and (w["status"][ti].cpu().numpy() == c["status"]).all()
+    vr = np.moveaxis(w["v_re"][ti].cpu().numpy(), 0, -1)
+    vi = np.moveaxis(w["v_im"][ti].cpu().numpy(), 0, -1)
+    assert _vrel(vr, vi, c["V_re"], c["V_im"]) <= 1e-10
+    _close(w["loss"][ti].cpu().numpy(), c["loss"], 1e-8)
+    np.testing.assert_allclose(w["vmin"][ti].cpu().numpy(), c["vmin"], rtol=1e-10)
+    np.testing.assert_allclose(w["vmax"][ti].cpu().numpy(), c["vmax"], rtol=1e-10)
+    exact = PowerFlow(f, device=0, exact=1, layout=1)
+    assert exact.kernel == "generic"
+    g, ga = run(exact)
+    assert torch.equal(w["iters"], g["iters"]) and torch.equal(w["status"], g["status"])
+    for c0 in range(0, B, 32768):   # (in chunks: complex V of the whole shard is 0.8 GB per kernel)
+        a = torch.complex(w["v_re"][c0:c0 + 32768], w["v_im"][c0:c0 + 32768])
+        b = torch.complex(g["v_re"][c0:c0 + 32768], g["v_im"][c0:c0 + 32768])
+        assert float(((a - b).abs() / b.abs()).max()) <= 1e-10
+        del a, b
+    assert float(((w["loss"] - g["loss"]).abs() / g["loss"].abs().max()).max()) <= 1e-8
+    assert float(((w["vmin"] - g["vmin"]).abs() / g["vmin"]).max()) <= 1e-10
+    assert float(((w["vmax"] - g["vmax"]).abs() / g["vmax"]).max()) <= 1e-10
+    np.testing.assert_array_equal(wa[3:], ga[3:])
+    np.testing.assert_allclose(wa[:3], ga[:3], rtol=1e-8)
+
+
 def test_device_api_on_torch_stream():
     import torch
     f = F.synthetic_feeder(123, 123)

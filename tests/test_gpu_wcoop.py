@@ -157,6 +157,39 @@ def _single_phase_subtrees(n, seed):
     return F.Feeder(Dl, Z, name=f"synthetic-{n}bus-single-phase-laterals")
 
 
+def _many_codes_feeder(n, seed, ncodes=70):
+    """Synthetic feeder whose branches (row 0 aside) use `ncodes` distinct
+    asymmetric line codes (code 1's 3x3 block with every entry perturbed by a
+    seeded factor in [0.8, 1.2]): the paired kernel's per-code Zl table in its
+    9-entry form, ncodes x 9 > 511 (the code field of its slot register holds the
+    code index, not code x 9)."""
+    f = F.synthetic_feeder(n, seed)
+    rng = np.random.default_rng(seed + 1)
+    z1 = f.Z[0:3]
+    extra = [z1 * (0.8 + 0.4 * rng.random((3, 3))) for _ in range(ncodes)]
+    Z = np.vstack([f.Z] + extra)
+    Dl = f.Dl.copy()
+    first = f.Z.shape[0] // 3 + 1
+    br = np.flatnonzero(Dl[:, 0] != 0)[1:]
+    Dl[br, 3] = first + (np.arange(br.size) % ncodes)
+    return F.Feeder(Dl, Z, name=f"synthetic-{n}bus-{ncodes}codes")
+
+
+def test_wcoop_many_asymmetric_codes():
+    """70 asymmetric line codes on a 3000-bus feeder (Zl table 70 x 9 entries):
+    the paired kernel against the oracle at the fast-mode bar."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = _many_codes_feeder(3000, 3000)
+    pq = F.scenario_loads(f, np.arange(16))
+    pf = PowerFlow(f)
+    assert pf.kernel == "wave" and pf.info["tile"] == 1
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    assert (c["status"] == 0).all()
+    _check_full(r, c)
+
+
 @pytest.mark.parametrize("n", [3000, 4096])
 def test_wcoop_zeroed_phases(n):
     """Zeroed phases on the paired kernel (single-phase laterals: a phase-B-only
@@ -275,3 +308,47 @@ def test_wcoop_small_and_ragged_batches(B):
     r = PowerFlow(f).solve(pq)
     c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
     _check_full(r, c)
+
+
+def test_wcoop_exchange_failure_reported(monkeypatch):
+    """A paired-kernel hand-off that gives up (forced: FPF_TEST_COOP_SPIN = 0 polls,
+    read at feeder creation) is its own outcome, never a non-convergence
+    (DPF_return7.cpp:199-217 defines that): every scenario reports status
+    FPF_EXCHANGE_FAILED (3), the aggregate counts none as converged or
+    non-converged, the host entry returns FPF_ERR_EXCHANGE, and the device entry
+    reports it through fpf_feeder_check and at the next call on the feeder."""
+    import torch
+    from freedm_amd import PowerFlow
+    from freedm_amd.engine import ExchangeError, FPF_EXCHANGE_FAILED
+    f = F.synthetic_feeder(2100, 2100)
+    monkeypatch.setenv("FPF_TEST_COOP_SPIN", "0")
+    pf = PowerFlow(f)
+    monkeypatch.delenv("FPF_TEST_COOP_SPIN")
+    assert pf.kernel == "wave"
+    B = 9
+    pq = F.scenario_loads(f, np.arange(B))
+    with pytest.raises(ExchangeError) as ei:
+        pf.solve(pq, full=False)
+    r = ei.value.results
+    assert ei.value.code == -6 and (r["status"] == FPF_EXCHANGE_FAILED).all()
+    a = r["aggregate"]
+    assert a["n_conv"] == 0 and a["n_nonconv"] == 0 and a["n_scen"] == B
+    dev = torch.device("cuda:0")
+    o = {"iters": torch.empty(B, dtype=torch.int32, device=dev), "status": torch.empty(B, dtype=torch.int8, device=dev),
+         "loss": torch.empty(B, dtype=torch.float64, device=dev)}
+    agg = torch.zeros(8, dtype=torch.float64, device=dev)
+    d_pq = torch.from_numpy(pq).to(dev)
+    pf.solve_device(d_pq, o, agg=agg)   # asynchronous: returns FPF_OK
+    with pytest.raises(ExchangeError):
+        pf.check()
+    pf.check()                          # reported once
+    assert (o["status"].cpu().numpy() == FPF_EXCHANGE_FAILED).all()
+    ag = agg.cpu().numpy()
+    assert ag[3] == 0 and ag[4] == 0 and ag[7] == B
+    pf.solve_device(d_pq, o)
+    torch.cuda.synchronize()
+    with pytest.raises(ExchangeError):  # the sticky word, at the next call on the feeder
+        pf.solve_device(d_pq, o)
+    # a feeder made without the override solves the same batch
+    ok = PowerFlow(f).solve(pq, full=False)
+    assert (ok["status"] == 0).all()

@@ -79,3 +79,15 @@ def test_paired_plan_zeroed_phases():
     p = _plan(_single_phase_subtrees(3000, 3000))
     assert p["ok"] == 1 and (p["spw"], p["C"], p["wpb"]) == (1, 4, 8) and p["lds"] <= 159 * 1024
     assert _plan(_masked_feeder(3000, 3000, restart=True))["ok"] == 0
+
+
+def test_paired_plan_line_codes():
+    """The paired kernel keeps a slot's line code in 9 bits of a register: 70
+    asymmetric codes (a 630-entry Zl table) are accepted, more than 512 codes
+    declined (the generic kernel runs them)."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_wcoop import _many_codes_feeder
+    p = _plan(_many_codes_feeder(3000, 3000))
+    assert p["ok"] == 1 and (p["spw"], p["C"], p["wpb"]) == (1, 4, 8) and p["lds"] <= 159 * 1024
+    assert _plan(_many_codes_feeder(2100, 2100, ncodes=520))["ok"] == 0
