@@ -1646,8 +1646,9 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     delete f;
 }
 
-// Order an aggregating launch on `st` after the previous one on this feeder
-// (they share d_partials / d_ticket); call agg_after() once it is enqueued.
+// Order a launch that uses state of the feeder (aggregate partials / ticket, the
+// guard's flag list, scratch, exchange areas, its own output buffers) on `st`
+// after the previous such launch; call agg_after() once it is enqueued.
 static hipError_t agg_before(fpf_feeder *f, hipStream_t st) {
     if (!f->agg_event) {
         hipError_t e = hipEventCreateWithFlags(&f->agg_event, hipEventDisableTiming);
@@ -1817,6 +1818,22 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     hipError_t e;
     bool agg_done = false;
     const int kern = kernel_for(f, n_scen);
+    // the convergence guard: the fast kernel flags, the exact fixup kernel re-solves
+    // (areas with per-scenario sources have no exact counterpart: no guard there);
+    // without an aggregate the wave kernel re-solves its flagged scenarios in its
+    // own LDS (local mode) where they fit
+    const bool guarded = kern == FPF_KERNEL_WAVE && f->guard && !d_vsrc && !d_s_in;
+    const bool local_fix = guarded && !d_agg && !f->wdev.wps &&
+                           (size_t)96 * (f->dev.nl + f->dev.nn) <= wave_lds_bytes(wave_dev_for(f, n_scen));
+    // launches that use state of the feeder -- the generic kernel's scratch, the
+    // layout copies, an aggregate's partials and ticket, the guard's flag list and
+    // fixup scratch, the paired kernel's exchange areas, the feeder's own
+    // per-scenario buffers (NULL outputs) -- are ordered across streams: each waits
+    // for the previous one (an event per feeder).  Wave-kernel solves that use none
+    // of it overlap freely.
+    const bool shared = kern != FPF_KERNEL_WAVE || d_agg || (guarded && !local_fix) || f->wdev.coop || !u.iters ||
+                        !u.status || !u.loss || !u.vmin || !u.vmax;
+    if (shared) HIPCHK(ctx, agg_before(f, st));
     // the generic and tiled kernels read and write [field][row][B] only: a
     // scenario-major batch goes through layout-0 copies (transposed in here,
     // the matrix outputs transposed back after the launch)
@@ -1864,13 +1881,9 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
         o.partials = f->d_partials;
         o.ticket = f->d_ticket;
         agg_done = true;
-        HIPCHK(ctx, agg_before(f, st));
     }
     if ((d_vsrc || d_s_in || d_skip || d_vinit_re) && kern != FPF_KERNEL_WAVE)
         return fail(ctx, FPF_ERR_UNSUPPORTED, "per-scenario source voltages need the wave kernel");
-    // the convergence guard: the fast kernel flags, the exact fixup kernel re-solves
-    // (areas with per-scenario sources have no exact counterpart: no guard there)
-    const bool guarded = kern == FPF_KERNEL_WAVE && f->guard && !d_vsrc && !d_s_in;
     if (guarded) {
         if (f->flag_cap < n_scen) {
             int rc = fpf_feeder_reserve(f, n_scen);
@@ -1879,8 +1892,7 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
         o.flag_count = f->d_flag_count;
         o.flag_ids = f->d_flag_ids;
         o.flag_out = agg_done ? d_flag_out : nullptr;
-        if (!agg_done && !d_agg && !f->wdev.wps &&
-            (size_t)96 * (f->dev.nl + f->dev.nn) <= wave_lds_bytes(wave_dev_for(f, n_scen))) {
+        if (local_fix) {
             // no aggregate to recompute: every wave-kernel workgroup re-solves the
             // scenarios it flagged itself, in its LDS (no second launch, nothing
             // global on the common path)
@@ -1917,12 +1929,12 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     if (transpose)
         for (const Tr &t : tr)
             if (t.user) HIPCHK(ctx, launch_transpose(*t.dev, t.user, t.rows, nB, st));   // [rows][B] -> [B][rows]
-    if (agg_done) HIPCHK(ctx, agg_after(f, st));
     if (d_agg && !agg_done) {
         e = launch_aggregate(n_scen, o.status, o.loss, o.vmin, o.vmax, f->dev.lb_v, f->dev.ub_v, d_agg, nullptr,
                              nullptr, st);
         if (e != hipSuccess) return fail(ctx, FPF_ERR_HIP, std::string("aggregate launch: ") + hipGetErrorString(e));
     }
+    if (shared) HIPCHK(ctx, agg_after(f, st));
     return FPF_OK;
 }
 

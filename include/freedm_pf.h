@@ -200,18 +200,17 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
 /* Device-memory batch: every pointer (pq, out fields, d_agg) is device memory;
  * enqueued on `stream` (a hipStream_t; NULL = the NULL/default stream, as in
  * every HIP API) and returns without synchronising.  d_agg (8 doubles, fpf_aggregate layout) may be NULL.
- * Launches that produce an aggregate (d_agg != NULL here, fpf_aggregate_device,
- * fpf_solve_batch) share the feeder's partials and arrival ticket; the library
- * serialises them across streams with an event per feeder (each waits for the
- * previous one), so they may be enqueued on different streams.  Other solves on
- * one feeder may overlap across streams only when they run the wave kernels
- * (fast mode, feeders of at most 2048 branches; the paired kernel of 2049..4096
- * branches exchanges through areas of the feeder, so its solves share one
- * stream), every per-scenario output they
- * use is the caller's (NULL outputs fall back to buffers of the feeder) and they
- * produce no aggregate; the generic and tiled kernels' scratch and layout
- * buffers and the guard's flag list belong to the feeder, so any other mix must
- * share one stream (or be serialised by the caller).
+ * Any mix of solves on one feeder may be enqueued on different streams: the
+ * library orders every launch that uses state of the feeder after the previous
+ * such launch (an event per feeder) -- launches that produce an aggregate
+ * (d_agg != NULL here, fpf_aggregate_device, fpf_solve_batch: the partials and
+ * ticket), the generic and tiled kernels (scratch, layout copies), the paired
+ * kernel (exchange areas), guarded solves whose flagged scenarios go to the
+ * feeder's flag list and fixup kernel, and solves with NULL per-scenario scalar
+ * outputs (they fall back to the feeder's buffers).  Solves on the wave kernels
+ * (feeders of at most 2048 branches) with every per-scenario scalar output the
+ * caller's, no aggregate and the guard resolved in the kernel's LDS (or
+ * no_guard) use none of it and overlap freely.
  * Returns FPF_OK or an error (the non-converged count is in d_agg / status).
  * Asynchronous faults: a paired-kernel launch whose exchange gave up sets a
  * sticky word of the feeder; the next fpf_solve_batch_device or

@@ -148,3 +148,51 @@ def test_guard_off_reports_fast_decisions():
     assert (np.abs(r["iters"][~same] - c["iters"][~same]) == 1).all()
     print(f"near-eps batch without the guard: {int((~same).sum())} of {pq.shape[2]} sweep counts differ "
           f"from the oracle")
+
+
+def test_two_streams_share_the_flag_list():
+    """Two guarded solves of one 2048-bus feeder (wave-block kernel: flagged
+    scenarios go to the feeder's flag list and dpf_fixup_kernel) enqueued on two
+    streams with no aggregate and caller-owned outputs: the library orders them
+    (fpf_solve_batch_device's contract), so each batch's near-eps scenarios are
+    re-solved with its own loads into its own outputs -- both equal the same
+    batches solved one at a time."""
+    import torch
+    from freedm_amd import PowerFlow
+    f, pq, _ = _near_eps(2048, n_pairs=4)
+    dev = torch.device("cuda:0")
+    pf = PowerFlow(f)
+    B = pq.shape[2]
+    # batch 1: the near-eps scenarios; batch 2: the same scenarios in reverse order
+    xs = [np.ascontiguousarray(pq), np.ascontiguousarray(pq[:, :, ::-1])]
+
+    def outs():
+        return {"v_re": torch.empty((3, pf.nn, B), dtype=torch.float64, device=dev),
+                "v_im": torch.empty((3, pf.nn, B), dtype=torch.float64, device=dev),
+                "iters": torch.empty(B, dtype=torch.int32, device=dev),
+                "status": torch.empty(B, dtype=torch.int8, device=dev),
+                "loss": torch.empty(B, dtype=torch.float64, device=dev),
+                "vmin": torch.empty(B, dtype=torch.float64, device=dev),
+                "vmax": torch.empty(B, dtype=torch.float64, device=dev),
+                "guard": torch.empty(B, dtype=torch.int8, device=dev)}
+    d = [torch.from_numpy(x).to(dev) for x in xs]
+    ref = []
+    for k in range(2):   # one at a time on one stream
+        r = outs()
+        pf.solve_device(d[k], r)
+        torch.cuda.synchronize()
+        ref.append({"iters": r["iters"].cpu().numpy(), "V_re": r["v_re"].cpu().numpy(),
+                    "V_im": r["v_im"].cpu().numpy(), "loss": r["loss"].cpu().numpy()})
+    o = [outs(), outs()]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        pf.solve_device(d[0], o[0], stream=s1)
+        pf.solve_device(d[1], o[1], stream=s2)
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert (o[k]["guard"].cpu().numpy() == 1).any()
+        np.testing.assert_array_equal(o[k]["iters"].cpu().numpy(), ref[k]["iters"])
+        np.testing.assert_array_equal(o[k]["v_re"].cpu().numpy(), ref[k]["V_re"])
+        np.testing.assert_array_equal(o[k]["v_im"].cpu().numpy(), ref[k]["V_im"])
+        np.testing.assert_array_equal(o[k]["loss"].cpu().numpy(), ref[k]["loss"])
