@@ -77,14 +77,16 @@ __host__ __device__ __forceinline__ int swz_row(int r) { return FPF_WAVE_SWZ ? r
 // 1 backward scan, 2 Ib, 3 convergence, 4 drops, 5 forward scan + stores,
 // 6 block offsets, 7 V), 120 after the loop, 121 V written out
 __device__ unsigned long long *fpf_wave_stamp_buf = nullptr;
+__device__ int fpf_wave_stamp_base = 0;   // the first recorded wave (global wave index)
 #define WSTAMP(idx)                                                                                   \
     do {                                                                                              \
-        const int gw_ = blockIdx.x * WPB + (threadIdx.x >> 6);                                         \
-        if (fpf_wave_stamp_buf && (threadIdx.x & 63) == 0 && gw_ < 64 && (idx) < 128)                  \
+        const int gw_ = blockIdx.x * WPB + (threadIdx.x >> 6) - fpf_wave_stamp_base;                   \
+        if (fpf_wave_stamp_buf && (threadIdx.x & 63) == 0 && gw_ >= 0 && gw_ < 64 && (idx) < 128)     \
             fpf_wave_stamp_buf[gw_ * 128 + (idx)] = __builtin_amdgcn_s_memtime();                       \
     } while (0)
-extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr) {
+extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr, int base) {
     unsigned long long *p = (unsigned long long *)dptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fpf_wave_stamp_base), &base, sizeof(base)) != hipSuccess) return -3;
     return hipMemcpyToSymbol(HIP_SYMBOL(fpf_wave_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
 }
 #else
