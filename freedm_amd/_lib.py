@@ -26,7 +26,7 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_multi_create", "fpf_multi_destroy", "fpf_multi_last_error", "fpf_multi_solve", "fpf_multi_get_feeder",
            "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_gradient_at", "fpf_vvc_round",
-           "fpf_vvc_gradient_batch", "fpf_feeder_check"]
+           "fpf_vvc_gradient_batch", "fpf_feeder_check", "fpf_vvc_round_batch"]
 
 
 class FpfOpts(C.Structure):
@@ -171,6 +171,11 @@ def load(path: str | None = None):
                                              C.c_double, C.c_int, _dp, _dp, C.POINTER(C.c_int), _dp,
                                              C.POINTER(C.c_int8)]
         L.fpf_vvc_gradient_batch.restype = C.c_int
+    if hasattr(L, "fpf_vvc_round_batch") or path == LIB_PATH:
+        L.fpf_vvc_round_batch.argtypes = [vp, _dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.c_int, _dp,
+                                          C.c_double, C.c_double, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int),
+                                          _dp, _dp, _dp, _dp, C.POINTER(C.c_int8)]
+        L.fpf_vvc_round_batch.restype = C.c_int
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
                  "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_check"):
         getattr(L, name).restype = C.c_int

@@ -66,6 +66,7 @@ struct fpf_feeder {
     // wave kernel (fast mode); wdev_big: the same tables launched with the
     // waves per workgroup of large batches
     void *d_wave = nullptr;
+    void *d_stage_tab = nullptr;   // the wave kernel's staging tables (both geometries)
     WaveDev wdev{}, wdev_big{};
     void *d_xch = nullptr, *d_xsync = nullptr, *d_xvm = nullptr;   // the paired wave-block kernel's exchange
     unsigned *h_xerr = nullptr;   // its sticky fault word (pinned, coherent; the kernel sets it at system scope)
@@ -1489,6 +1490,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         for (int i = 0; i < 6; ++i) w.V0[i] = d.V0[i];
         w.s3 = d.s3;
         w.eps = d.eps;
+        for (int p = 0; p < 3; ++p) w.rv0[p] = 1.0 / (d.V0[2 * p] * d.V0[2 * p] + d.V0[2 * p + 1] * d.V0[2 * p + 1]);
         w.lb_v = d.lb_v;
         w.ub_v = d.ub_v;
         w.slot_row = (const int32_t *)(wbase + o_row);
@@ -1569,6 +1571,42 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         }
         f->wdev_big = w;
         f->wdev_big.wpb = wh.wpb_big_batch;
+        if (!w.wps) {
+            // the table-driven staging of both launch geometries (fpf_wave.hip)
+            std::vector<int32_t> sm[2], l0[2], om[2], o0[2];
+            int U[2], UO[2];
+            WaveDev *wv[2] = {&f->wdev, &f->wdev_big};
+            std::vector<char> tb;
+            size_t off[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            for (int g = 0; g < 2; ++g) {
+                U[g] = wave_stage_tables(*wv[g], sm[g], l0[g]);
+                UO[g] = wave_out_tables(*wv[g], om[g], o0[g]);
+                if (U[g]) {
+                    off[g][0] = push_blob(tb, sm[g]);
+                    off[g][1] = push_blob(tb, l0[g]);
+                }
+                if (UO[g]) {
+                    off[g][2] = push_blob(tb, om[g]);
+                    off[g][3] = push_blob(tb, o0[g]);
+                }
+            }
+            if (!tb.empty()) {
+                e = hipMalloc(&f->d_stage_tab, tb.size());
+                if (e == hipSuccess) e = hipMemcpy(f->d_stage_tab, tb.data(), tb.size(), hipMemcpyHostToDevice);
+                if (e != hipSuccess) {
+                    fpf_feeder_destroy(f);
+                    return fail(ctx, FPF_ERR_HIP, std::string("staging tables: ") + hipGetErrorString(e));
+                }
+            }
+            for (int g = 0; g < 2; ++g) {
+                wv[g]->stage_u = U[g];
+                wv[g]->stage_smaj = U[g] ? (const int32_t *)((char *)f->d_stage_tab + off[g][0]) : nullptr;
+                wv[g]->stage_l0 = U[g] ? (const int32_t *)((char *)f->d_stage_tab + off[g][1]) : nullptr;
+                wv[g]->out_u = UO[g];
+                wv[g]->out_smaj = UO[g] ? (const int32_t *)((char *)f->d_stage_tab + off[g][2]) : nullptr;
+                wv[g]->out_l0 = UO[g] ? (const int32_t *)((char *)f->d_stage_tab + off[g][3]) : nullptr;
+            }
+        }
     }
     // auto: the interpreted tiled kernel only pays with several scenarios per
     // workgroup; below that (large feeders, e.g. 2048-bus at tile 1: 794 ms vs
@@ -1630,6 +1668,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_partials);
     (void)hipFree(f->d_ticket);
     (void)hipFree(f->d_wave);
+    (void)hipFree(f->d_stage_tab);
     (void)hipFree(f->d_xch);
     (void)hipFree(f->d_xsync);
     (void)hipFree(f->d_xvm);

@@ -149,6 +149,18 @@ struct WaveDev {
     const double *slot_temp;    // [9][C][L] complex: TEMP = lng*Z/Zb of the node's branch, row-major
                                 // (l, a); temp_sym: [4][C][L] (z_aa - zm for a = 0..2, zm)
     const int32_t *blk_pairs;   // [bdepth][2][nblk] (plus, minus) forward indices; pad = ncomp (zero)
+    // per-workgroup staging of a tile's loads (fpf_wave.hip, wave_stage_tables): for
+    // chunk c = u NT + t (16 bytes of pq) the STG double index of each of its two
+    // halves; scenario-major {dst0, dst1}, scenario-fastest {pq line, dst0}
+    // (dst1 = dst0 + 2); stage_u chunks per thread, 0: no tables (generic walk)
+    const int32_t *stage_smaj, *stage_l0;
+    int32_t stage_u;
+    // the V write-out, table-driven: element i = u NT + t of the tile's V block
+    // ([SPB][3][Nn] scenario major, [3 Nn][SPB] scenario fastest) at STG double2
+    // index out_*[i] (row 0: the scenario's V0S); out_u per thread, 0: none
+    const int32_t *out_smaj, *out_l0;
+    int32_t out_u;
+    double rv0[3];              // 1/|V0_p|^2 (the flat start's first load currents)
     // wave-block kernel (fpf_wblk.hip): one scenario per workgroup of wps
     // wavefronts (L = 64 wps lanes, C slots per lane) for feeders of 257..2048
     // branches; wps = 0: the per-wavefront kernel above.  TEMP = lng * Zl(code)
@@ -267,6 +279,11 @@ hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
                             double *d_agg, double *partials, unsigned *ticket, hipStream_t st);
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+// the staging tables of a wave-kernel geometry (WaveDev::stage_smaj / stage_l0,
+// [u][NT] int2 each); returns the chunks per thread, 0 if above the kernel's limit
+int wave_stage_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0);
+// the write-out tables (WaveDev::out_smaj / out_l0, [u][NT] int); 0 if above the limit
+int wave_out_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0);
 size_t wave_lds_bytes(const WaveDev &w);
 hipError_t launch_transpose(const double *in, double *out, size_t rows, size_t cols, hipStream_t st);
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);

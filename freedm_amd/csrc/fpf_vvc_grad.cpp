@@ -760,3 +760,148 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
     return bad;
 #undef GCHK
 }
+
+// ---------------------------------------------------------------------------
+// A whole VVC round per load scenario (VoltVarCtrl.cpp:1141-1762 for B scenarios
+// of one control table): the batched gradient, then every scenario's m_max + 1
+// step sizes as ONE device batch (B x (m_max + 1) solves), the reference's stop
+// rule per scenario, and one more batch for the scenarios whose search reverses.
+
+namespace {
+// the reference's stop rule over one search (VoltVarCtrl.cpp:1330-1540, as
+// fpf_vvc_line_search): keep c_m while c_{m+1} lowers the loss; the direction flag
+// drops when a kept loss exceeds Ploss_orig; the first candidate that does not
+// converge (the reference throws there)
+void stop_rule(const double *loss, const signed char *status, int m_max, double ploss_orig, int *stop, int *reverse,
+               int *first_nonconv) {
+    *first_nonconv = -1;
+    for (int m = 0; m <= m_max; ++m)
+        if (status[m] != FPF_CONVERGED) {
+            *first_nonconv = m;
+            break;
+        }
+    *stop = -1;
+    *reverse = 0;
+    for (int m = 0; m < m_max; ++m) {
+        if (loss[m + 1] > loss[m]) {
+            *stop = m;
+            break;
+        }
+        if (loss[m] > ploss_orig) *reverse = 1;
+    }
+}
+}  // namespace
+
+extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols, const double *z,
+                                   int z_rows, int z_cols, int n_scen, const double *pq, double beta0, double alpha,
+                                   int m_max, int ld, double *g, double *load_nodes, int *n_loads, double *loss_fwd,
+                                   double *loss_rev, double *pq_out, double *res, signed char *rstatus) {
+    if (!feeder || !ctrl_dl || n_scen < 0 || m_max < 1 || (n_scen > 0 && (!pq || !g || !pq_out || !res || !rstatus)))
+        return fpf::feeder_fail(feeder, FPF_ERR_ARG, "fpf_vvc_round_batch: bad arguments");
+    if (n_scen == 0) return 0;
+    const int B = n_scen, M = m_max + 1;
+    const size_t b = (size_t)B, nlz = (size_t)nl;
+    std::vector<double> stats(b * 8);
+    int rc = fpf_vvc_gradient_batch(feeder, ctrl_dl, nl, ncols, z, z_rows, z_cols, B, pq, beta0, ld, g, load_nodes,
+                                    n_loads, stats.data(), rstatus);
+    if (rc < 0) return rc;
+    const double bkva = fpf_feeder_bkva(feeder);
+    std::memcpy(pq_out, pq, sizeof(double) * 6 * nlz * b);
+    // the rows each load's Q update touches (rbus == load node, :1334-1372)
+    std::vector<std::vector<int>> rows[3];
+    for (int x = 0; x < 3; ++x) {
+        rows[x].resize(n_loads[x]);
+        for (int i = 0; i < n_loads[x]; ++i)
+            for (int r = 0; r < nl; ++r)
+                if (ctrl_dl[r + 2 * nlz] == load_nodes[(size_t)x * ld + i]) rows[x][i].push_back(r);
+    }
+    struct Sc {
+        int stop[2] = {-1, -1}, reversed = 0, sent = 0, nonconv = 0;
+        double after = 0.0;
+    };
+    std::vector<Sc> sc(b);
+    std::vector<int> todo;
+    for (int s = 0; s < B; ++s)
+        if (rstatus[s] == 0) todo.push_back(s);
+    for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
+        const int K = (int)todo.size();
+        const size_t Bc = (size_t)K * M;
+        // candidate (k, m) = column k M + m: scenario todo[k]'s loads with its Q
+        // set-points moved by -g (bkva/3) c_m, c_0 = c0 (:1323) or the reversed
+        // start -beta0/(bkva/3)/gabs_min (:1546), c_{m+1} = alpha c_m (:1420-1422)
+        std::vector<double> cand(6 * nlz * Bc);
+        for (size_t fr = 0; fr < 6 * nlz; ++fr)
+            for (int k = 0; k < K; ++k) {
+                const double v = pq[fr * b + todo[k]];
+                double *d = &cand[fr * Bc + (size_t)k * M];
+                for (int m = 0; m < M; ++m) d[m] = v;
+            }
+        for (int k = 0; k < K; ++k) {
+            const int s = todo[k];
+            const double *st8 = &stats[(size_t)s * 8];
+            double cvq = pass == 0 ? st8[3] : -beta0 / (bkva / 3) / st8[2];
+            for (int m = 0; m < M; ++m) {
+                for (int x = 0; x < 3; ++x) {
+                    const size_t fq = (size_t)(1 + 2 * x);   // Q of phase x = Dl column 7 + 2x
+                    for (int i = 0; i < n_loads[x]; ++i) {
+                        const double gupdate = g[((size_t)s * 3 + x) * ld + i] * (bkva / 3) * cvq;
+                        for (int r : rows[x][i])
+                            cand[(fq * nlz + r) * Bc + (size_t)k * M + m] = pq[(fq * nlz + r) * b + s] - gupdate;
+                    }
+                }
+                cvq = alpha * cvq;
+            }
+        }
+        std::vector<double> loss(Bc);
+        std::vector<signed char> status(Bc);
+        fpf_outputs out;
+        std::memset(&out, 0, sizeof(out));
+        out.loss = loss.data();
+        out.status = status.data();
+        rc = fpf::solve_batch_host(feeder, (int)Bc, cand.data(), &out, nullptr, FPF_LAYOUT_SCEN_FASTEST);
+        if (rc < 0) return rc;
+        std::vector<int> next;
+        for (int k = 0; k < K; ++k) {
+            const int s = todo[k];
+            Sc &q = sc[s];
+            const double *lk = &loss[(size_t)k * M];
+            double *lout = pass == 0 ? loss_fwd : loss_rev;
+            if (lout) std::memcpy(lout + (size_t)s * M, lk, sizeof(double) * M);
+            int stop, reverse, first_nonconv;
+            stop_rule(lk, &status[(size_t)k * M], m_max, stats[(size_t)s * 8 + 4], &stop, &reverse, &first_nonconv);
+            // the reference solves candidates 0 .. stop + 1 (two per step) and throws
+            // at the first that does not converge
+            const int last = stop >= 0 ? stop + 1 : m_max;
+            if (first_nonconv >= 0 && first_nonconv <= last) q.nonconv = 1;
+            q.stop[pass] = stop;
+            if (pass == 0) {
+                q.reversed = reverse;
+                if (reverse) next.push_back(s);
+            }
+            if (stop >= 0) {
+                q.after = lk[stop];
+                // Dl = Dl_osize (:1486/:1707): the kept candidate's Q set-points
+                for (int x = 0; x < 3; ++x) {
+                    const size_t fq = (size_t)(1 + 2 * x);
+                    for (int i = 0; i < n_loads[x]; ++i)
+                        for (int r : rows[x][i])
+                            pq_out[(fq * nlz + r) * b + s] = cand[(fq * nlz + r) * Bc + (size_t)k * M + stop];
+                }
+                if (lk[stop] < stats[(size_t)s * 8 + 4]) q.sent = 1;   // :1495
+            } else {
+                q.after = lk[m_max - 1];
+            }
+        }
+        todo.swap(next);
+    }
+    int bad = 0;
+    for (int s = 0; s < B; ++s) {
+        const double *st8 = &stats[(size_t)s * 8];
+        const Sc &q = sc[s];
+        const double v[13] = {st8[4], st8[5], st8[6], st8[3], (double)q.stop[0], (double)q.stop[1], (double)q.reversed,
+                              (double)q.sent, q.after, st8[0], st8[1], st8[2], (double)q.nonconv};
+        std::memcpy(res + (size_t)s * 13, v, sizeof(v));
+        if (rstatus[s] != 0 || q.nonconv) ++bad;
+    }
+    return bad;
+}

@@ -94,6 +94,7 @@ extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr, int base) {
 #endif
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
+constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging keeps in flight
 
 // experiments (tools/gpu_ab_trees.sh): IBO_LDS keeps the substation current of the
 // previous sweep (the convergence test's Ibo) in the scenario's LDS region instead
@@ -200,9 +201,73 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         };
         if ((int)threadIdx.x < 3 * SROW)   // the zero row of each phase plane
             stg[((int)threadIdx.x / SROW) * PSTR + swz_row(nl) * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
+        // the feeder tables (L2-resident): their loads issued first, in flight
+        // together with the tile's loads; stored to LDS after them
+        constexpr int UT = (9 * C * L + NT - 1) / NT;
+        double2 tt[TEMP_IN_LDS ? UT : 1];
+        if (TEMP_IN_LDS) {
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                const int i = u * NT + (int)threadIdx.x;
+                tt[u] = ld_global2(f.slot_temp, i < ntm * C * L ? i : 0);
+            }
+        }
+        const int np2 = 2 * bdepth * nblk;
+        const int pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
+        const int kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
-        if (o.smaj) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        constexpr int US = WAVE_STAGE_U;
+        const int SU = f.stage_u;
+        if (SU > 0 && (o.smaj || (B & 1) == 0)) {
+            // table-driven (wave_stage_tables): chunk c = u NT + t, 16 bytes each, every
+            // load of the thread in flight with its two STG destinations; scenario
+            // major: the tile is one contiguous block of nsb x 6 Nl doubles;
+            // scenario fastest: chunk c is scenarios (2 (t % H), + 1) of pq line tb.x
+            const int nchunk = DBG(256) ? 0 : nsb * 3 * nl;
+            constexpr int H = SPB / 2;
+            const int jj = 2 * ((int)threadIdx.x % H);
+            const int2 *tab = (const int2 *)(o.smaj ? f.stage_smaj : f.stage_l0);
+            const d2v *src = (const d2v *)(pq + (size_t)s0 * 6 * nl);
+            int2 tb[US];
+            d2v r[US];
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                if (u < SU) {
+                    const int c = u * NT + (int)threadIdx.x;
+                    tb[u] = tab[c];
+                    const bool ok = c < nchunk && (o.smaj || jj < nsb);
+                    if (o.smaj) {
+                        r[u] = __builtin_nontemporal_load(src + (ok ? c : 0));
+                    } else {
+                        const size_t ga = (size_t)tb[u].x * B + s0 + jj;
+                        r[u] = __builtin_nontemporal_load((const d2v *)(pq + (ok ? ga : 0)));
+                        r[u] = ok ? r[u] : d2v{0.0, 0.0};
+                    }
+                }
+            }
+#ifdef FPF_STAMPS
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            WSTAMP(3);
+#endif
+            double *const sd = (double *)stg;
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                const int c = u * NT + (int)threadIdx.x;
+                if (u < SU && c < 3 * nl * SPB && (o.smaj ? c < nchunk : true)) {
+                    sd[o.smaj ? tb[u].x : tb[u].y] = r[u].x * inv_s3;
+                    sd[o.smaj ? tb[u].y : tb[u].y + 2] = r[u].y * inv_s3;
+                }
+            }
+            if (o.smaj) {   // a partial last tile: zero loads in the columns of its missing scenarios
+                const int per = 6 * nl;
+                for (int i = threadIdx.x; i < (SPB - nsb) * per; i += NT) {
+                    const int j = nsb + i / per, fr = i % per;
+                    sd[spos(fr, j)] = 0.0;
+                }
+            }
+        } else if (o.smaj) {
             // scenario-major layout: the tile's nsb scenarios are one contiguous
             // block of nsb x 6 Nl doubles, read with 16-byte loads (6 Nl is even)
             typedef double d2v __attribute__((ext_vector_type(2)));
@@ -221,6 +286,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     const int i = i0 + u * NT + (int)threadIdx.x;
                     r[u] = __builtin_nontemporal_load(src + (i < total2 ? i : 0));
                 }
+#ifdef FPF_STAMPS
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (i0 == 0) WSTAMP(3);
+#endif
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + (int)threadIdx.x;
@@ -290,24 +359,13 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 if (i < total) sd[spos(i / SPB, i % SPB)] = r[u] * inv_s3;
             }
         }
-        // the feeder tables: all loads in flight before the LDS stores
         if (TEMP_IN_LDS) {
-            constexpr int UT = (9 * C * L + NT - 1) / NT;
-            double2 t[UT];
 #pragma unroll
             for (int u = 0; u < UT; ++u) {
                 const int i = u * NT + (int)threadIdx.x;
-                t[u] = ld_global2(f.slot_temp, i < ntm * C * L ? i : 0);
-            }
-#pragma unroll
-            for (int u = 0; u < UT; ++u) {
-                const int i = u * NT + (int)threadIdx.x;
-                if (i < ntm * C * L) tl[i] = t[u];
+                if (i < ntm * C * L) tl[i] = tt[u];
             }
         }
-        const int np2 = 2 * bdepth * nblk;
-        const int pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
-        const int kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
         if ((int)threadIdx.x < np2) pairs[threadIdx.x] = pv;
         for (int i = threadIdx.x + NT; i < np2; i += NT) pairs[i] = f.blk_pairs[i];
         if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
@@ -361,9 +419,13 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     // last scenario is done.
     cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     bool done = !live;
+    // flat start (V = V0 on every node, DPF_return7.cpp:92-96, the feeder's own
+    // source): the first sweep's load currents use the uniform 1/|V0_p|^2, and
+    // sum_k |S_k|_1 of the guard record is taken from that sweep's Sld reads
+    const bool flat = !o.vsrc && !o.vinit_re;
     // the guard record V0S[3] = (sum_k |S_k|_1, closest |err2 - eps^2| of a decision
     // in the coarse band, +inf: none) of the scenario, in LDS (fpf_api.cpp: guard_factor)
-    if (o.flag_count) {
+    if (o.flag_count && !flat) {
         double sabs = 0.0;
 #pragma unroll
         for (int c = 0; c < C; ++c)
@@ -398,7 +460,26 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
             for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(stg, p * PSTR + sb[c]), v[c][p]);
 #else
-        {
+        if (flat && it == 0) {
+            // IL = conj(S/V0) = conj(S) V0 / |V0|^2 (V0 != 0), every Sld read once
+            double sabs = 0.0;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                cx sl[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) sl[p] = ldx(stg, p * PSTR + sb[c]);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const double vr = f.V0[2 * p], vi = f.V0[2 * p + 1], r0 = f.rv0[p];
+                    il[c][p] = mk(fma(sl[p].re, vr, sl[p].im * vi) * r0, fma(sl[p].re, vi, -(sl[p].im * vr)) * r0);
+                    sabs += fabs(sl[p].re) + fabs(sl[p].im);
+                }
+            }
+            if (o.flag_count) {
+                sabs = seg_incl<L>(sabs);
+                if (li == L - 1) V0S[3] = make_double2(sabs, INFINITY);
+            }
+        } else {
             // a slot's three Sld reads issued together (FPF_WAVE_GROUP 2: the next
             // slot's before this slot's arithmetic); scheduling barriers keep the
             // groups, so the register allocator cannot fall back to one read in
@@ -697,12 +778,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         stx(stg, p * PSTR + swz_row(k - 1) * SROW + sc, v[c][p]);   // over the scenario's own Sld
-                        if (FULL) {
-                            emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
-                            const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
-                            mn = fmin(mn, m2);
-                            mx = fmax(mx, m2);
-                        }
+                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                        const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
+                        mn = fmin(mn, m2);
+                        mx = fmax(mx, m2);
                     }
                 }
             }
@@ -721,18 +800,12 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                         o.s_in[(size_t)(2 * p) * B + s] = sb.re;
                         o.s_in[(size_t)(2 * p + 1) * B + s] = sb.im;
                     }
-                    if (FULL) {
-                        const double m2 = fma(v0p.re, v0p.re, v0p.im * v0p.im);
-                        mn = fmin(mn, m2);
-                        mx = fmax(mx, m2);
-                    }
+                    const double m2 = fma(v0p.re, v0p.re, v0p.im * v0p.im);
+                    mn = fmin(mn, m2);
+                    mx = fmax(mx, m2);
                 }
             }
-            if (!FULL) {
-                // light outputs: V is in the region; the extremes are taken from there
-                // after the loop (fewer registers live across the sweep loop)
-                x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
-            } else if (!f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
+            if (!FULL || !f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
                 // every Lnum_p + 1 = Nn: V_abc_list keeps every row, so the extremes are
                 // plain min/max; loss = s3 sum Re(drop conj(Ib))
                 x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
@@ -785,12 +858,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 if (o.iters) o.iters[sf] = it + 1;
                 if (o.status) o.status[sf] = conv ? 0 : 1;
                 if (o.loss) o.loss[sf] = x;
-                if (FULL) {
-                    if (o.vmin) o.vmin[s] = mn;
-                    if (o.vmax) o.vmax[s] = mx;
-                    res[sc][1] = mn;
-                    res[sc][2] = mx;
-                }
+                if (o.vmin) o.vmin[sf] = mn;
+                if (o.vmax) o.vmax[sf] = mx;
+                res[sc][1] = mn;
+                res[sc][2] = mx;
                 res[sc][0] = x;
                 res[sc][3] = conv ? 0.0 : 1.0;
             }
@@ -799,29 +870,6 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         done = done || fin;
     }
     WSTAMP(120);
-    if (!FULL && live && !DBG(128)) {
-        // every Lnum_p + 1 = Nn (no zeroed phases): V_abc_list keeps every row, so
-        // Vmin/Vmax are the plain extremes of |V| over the scenario's V in its
-        // region (|V|^2 compared, one sqrt each: sqrt is monotonic)
-        double mn = INFINITY, mx = -INFINITY;
-        for (int k = li; k < nn; k += L) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
-                const double m2 = fma(vv.re, vv.re, vv.im * vv.im);
-                mn = fmin(mn, m2);
-                mx = fmax(mx, m2);
-            }
-        }
-        mn = sqrt(seg_reduce_min<L>(mn));
-        mx = sqrt(seg_reduce_max<L>(mx));
-        if (li == L - 1) {
-            if (o.vmin) o.vmin[s] = mn;
-            if (o.vmax) o.vmax[s] = mx;
-            res[sc][1] = mn;
-            res[sc][2] = mx;
-        }
-    }
 
     // ---- the guard band (fpf_api.cpp: guard_factor) for the scenarios with a decision
     // in the coarse band: errmx within tau = guard_k sum_k |IL_k|_1 of eps, where
@@ -860,7 +908,19 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     // workgroup; the last to arrive folds the partials in workgroup order
     // (deterministic) -- the hand-off of MI355X_MICROARCH.md "Valid forms".
     // Published before the V stores, so the ticket does not wait for them.
+    // the write-out table (wave_stage_tables; L2-resident), in flight across the barrier
+    constexpr int UO = WAVE_STAGE_U;
+    const int OU = (!FULL && (o.v_re || o.v_im) && !DBG(1024)) ? f.out_u : 0;
+    int otab[UO];
+    {
+        const int32_t *ot = o.smaj ? f.out_smaj : f.out_l0;
+#pragma unroll
+        for (int u = 0; u < UO; ++u)
+            if (u < OU) otab[u] = ot[u * NT + (int)threadIdx.x];
+    }
+    WSTAMP(122);
     __syncthreads();
+    WSTAMP(123);
     __shared__ int last_wg;
     const bool agg = o.agg && !DBG(2048);
     if (agg && threadIdx.x == 0) {
@@ -884,8 +944,34 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_wg = t == gridDim.x - 1;
     }
-    // ---- the workgroup's V, coalesced: consecutive scenarios of one (phase, node)
-    if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj) {
+    // ---- the workgroup's V, coalesced: consecutive scenarios of one (phase, node),
+    // or (scenario major) the tile's contiguous [nsb][3][Nn] block
+    if (OU > 0) {
+        // element i = u NT + t of the tile's block, read from STG at otab[u]
+        const int per = 3 * nn, ntot = SPB * per, nval = o.smaj ? nsb * per : ntot;
+        double2 vv[UO];
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int i = u * NT + (int)threadIdx.x;
+            if (u < OU && i < ntot) vv[u] = stg[otab[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int i = u * NT + (int)threadIdx.x;
+            if (u < OU && i < nval) {
+                size_t d;
+                if (o.smaj) {
+                    d = (size_t)s0 * per + i;
+                } else {
+                    const int j = i % SPB, r = i / SPB;   // (SPB a power of two)
+                    if (j >= nsb) continue;
+                    d = (size_t)r * B + s0 + j;
+                }
+                if (o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + d);
+                if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + d);
+            }
+        }
+    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj) {
         // scenario-major layout: the tile's V is one contiguous [nsb][3][Nn] block
         const int per = 3 * nn, total = nsb * per;
         // element i: scenario j = i / per, (phase p, node k) of i % per, walked NT apart
@@ -985,6 +1071,51 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             if (wv == 0) g3::g3_fixup_local(o.fix_dev, B, pq, (double *)lds, &osh, fix_ids, fix_n);
         }
     }
+}
+
+// STG double index of pq element (field fq, row r) of the workgroup's scenario j
+static int stg_double(int fq, int r, int j, int nl, int srow) {
+    return 2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(r)) * srow + j) + (fq & 1);
+}
+
+int wave_out_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0) {
+    const int spb = w.wpb * w.spw, nt = w.wpb * 64, nl = w.nl, nn = w.nn, srow = spb + 1;
+    const int ntot = spb * 3 * nn, U = (ntot + nt - 1) / nt;
+    if (U > WAVE_STAGE_U || (spb & (spb - 1))) return 0;
+    const int pstr = (swz_row(nl) + 1) * srow, xc = w.ncomp + 1, noff = w.off_in_x ? 0 : 3 * w.nblk;
+    const int rs = (3 * xc + noff + 4 + REGION_EXTRA) | 1;
+    auto at = [&](int j, int p, int k) { return k == 0 ? 3 * pstr + j * rs + 3 * xc + noff + p : p * pstr + swz_row(k - 1) * srow + j; };
+    smaj.assign((size_t)U * nt, 0);
+    l0.assign((size_t)U * nt, 0);
+    for (int i = 0; i < ntot; ++i) {
+        smaj[i] = at(i / (3 * nn), (i % (3 * nn)) / nn, i % nn);
+        l0[i] = at(i % spb, (i / spb) / nn, (i / spb) % nn);
+    }
+    return U;
+}
+
+int wave_stage_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0) {
+    const int spb = w.wpb * w.spw, nt = w.wpb * 64, nl = w.nl, srow = spb + 1;
+    const int nchunk = spb * 3 * nl, U = (nchunk + nt - 1) / nt;
+    if (U > WAVE_STAGE_U || spb % 2) return 0;
+    smaj.assign((size_t)2 * U * nt, 0);
+    l0.assign((size_t)2 * U * nt, 0);
+    const int H = spb / 2;
+    for (int u = 0; u < U; ++u)
+        for (int t = 0; t < nt; ++t) {
+            const int c = u * nt + t;
+            int32_t *a = &smaj[2 * (size_t)c], *b = &l0[2 * (size_t)c];
+            if (c >= nchunk) continue;
+            // scenario major: elements e = 2c, 2c + 1 of the tile's [spb][6][nl] block
+            const int e = 2 * c, j = e / (6 * nl), rem = e % (6 * nl), fq = rem / nl, r = rem % nl;
+            a[0] = stg_double(fq, r, j, nl, srow);
+            a[1] = r + 1 < nl ? stg_double(fq, r + 1, j, nl, srow) : stg_double(fq + 1, 0, j, nl, srow);
+            // scenario fastest: line fr of [6 nl][B], the scenario pair 2 (t % H), 2 (t % H) + 1
+            const int fr = t / H + u * (nt / H), jj = 2 * (t % H);
+            b[0] = fr;
+            b[1] = fr < 6 * nl ? stg_double(fr / nl, fr % nl, jj, nl, srow) : 0;
+        }
+    return U;
 }
 
 size_t wave_lds_bytes(const WaveDev &w) {

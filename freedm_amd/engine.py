@@ -342,6 +342,44 @@ class PowerFlow:
                 "gmin": st[:, 0], "gmax": st[:, 1], "gabs_min": st[:, 2], "c0": st[:, 3], "ploss_orig": st[:, 4],
                 "vmin_orig": st[:, 5], "vmax_orig": st[:, 6], "iters": st[:, 7].astype(int)}
 
+    def vvc_round_batch(self, ctrl_dl: np.ndarray, pq: np.ndarray, beta0: float = 0.1, alpha: float = 1.1,
+                        m_max: int = 100) -> dict:
+        """fpf_vvc_round_batch: a whole VVC round (VoltVarCtrl.cpp:1141-1762) for
+        every load scenario of pq ([6][Nl][B], the load columns 6..11 of ctrl_dl
+        per scenario): batched gradients, all scenarios' step sizes as one batch,
+        the reversed searches as another."""
+        L = _lib.load()
+        ctrl = np.asfortranarray(ctrl_dl, dtype=np.float64)
+        pq = np.ascontiguousarray(pq, dtype=np.float64)
+        if pq.ndim != 3 or pq.shape[:2] != (6, ctrl.shape[0]):
+            raise ValueError(f"pq must be [6][{ctrl.shape[0]}][B]")
+        B = pq.shape[2]
+        zbuf, zs = self._zbuf()
+        ld = ctrl.shape[0]
+        g, nodes = np.zeros((B, 3, ld)), np.zeros((3, ld))
+        n = (C.c_int * 3)()
+        lf, lr = np.full((B, m_max + 1), np.nan), np.full((B, m_max + 1), np.nan)
+        pq_out = np.zeros_like(pq)
+        res = np.zeros((B, 13))
+        rs = np.zeros(B, np.int8)
+        rc = L.fpf_vvc_round_batch(self.h, ctrl.ctypes.data_as(_lib._dp), ctrl.shape[0], ctrl.shape[1],
+                                   zbuf.ctypes.data_as(_lib._dp), zs[0], zs[1], B, pq.ctypes.data_as(_lib._dp),
+                                   float(beta0), float(alpha), int(m_max), ld, g.ctypes.data_as(_lib._dp),
+                                   nodes.ctypes.data_as(_lib._dp), n, lf.ctypes.data_as(_lib._dp),
+                                   lr.ctypes.data_as(_lib._dp), pq_out.ctypes.data_as(_lib._dp),
+                                   res.ctypes.data_as(_lib._dp), rs.ctypes.data_as(C.POINTER(C.c_int8)))
+        if rc < 0:
+            _raise(rc, self.ctx.err())
+        keys = ["ploss_orig", "vmin_orig", "vmax_orig", "c0", "stop_fwd", "stop_rev", "reversed", "sent",
+                "ploss_after", "gmin", "gmax", "gabs_min", "nonconv"]
+        r = {k: res[:, i].copy() for i, k in enumerate(keys)}
+        for k in ("stop_fwd", "stop_rev", "reversed", "sent", "nonconv"):
+            r[k] = r[k].astype(int)
+        r.update(g=[[g[s, x, :n[x]].copy() for x in range(3)] for s in range(B)],
+                 load_nodes=[nodes[x, :n[x]].copy() for x in range(3)], loss_fwd=lf, loss_rev=lr, pq=pq_out,
+                 rstatus=rs, n_bad=rc)
+        return r
+
     def vvc_round(self, ctrl_dl: np.ndarray, beta0: float = 0.1, alpha: float = 1.1, m_max: int = 100) -> dict:
         """fpf_vvc_round: one VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762) --
         gradient, batched step-size search, reversal -- and the control after it."""

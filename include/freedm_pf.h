@@ -399,6 +399,25 @@ int         fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, int
                           int m_max, int ld, double *g, double *load_nodes, int *n_loads,
                           double *loss_fwd, double *loss_rev, double *dl_out, double *res);
 
+/* One whole VVC round per load scenario (VoltVarCtrl.cpp:1141-1762 for a VVC
+ * Monte Carlo): scenario s is ctrl_dl with its load columns 6..11 replaced by
+ * pq[.][.][s] (host, [6][Nl][n_scen]).  The gradients as fpf_vvc_gradient_batch
+ * (same arguments and rules: every scenario's (int) load tests must be the
+ * control's); then every scenario's m_max + 1 step sizes as ONE device batch,
+ * the reference's stop rule per scenario, and one more batch for the scenarios
+ * whose search reverses (:1544-1762).  Per scenario: loss_fwd / loss_rev
+ * [n_scen][m_max + 1] (may be NULL; rows of scenarios that do not reverse are
+ * left as they are), pq_out [6][Nl][n_scen] the scenario's loads after the round
+ * (the kept candidate's Q set-points, Dl = Dl_osize), res [n_scen][13] as
+ * fpf_vvc_round's, rstatus [n_scen] the gradient's gstatus (0: the round ran).
+ * Returns the number of scenarios with rstatus != 0 or a non-converged candidate
+ * the reference would have solved (res[12]), or FPF_ERR_*. */
+int         fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
+                                const double *z, int z_rows, int z_cols, int n_scen, const double *pq,
+                                double beta0, double alpha, int m_max, int ld, double *g,
+                                double *load_nodes, int *n_loads, double *loss_fwd, double *loss_rev,
+                                double *pq_out, double *res, signed char *rstatus);
+
 /* Diagnostics: on-device check, over n seeded operand sets, that the
  * shared-reciprocal division the tiled kernel uses gives the same bits as the
  * compiler's a / b and as the libgcc __divdc3 complex division.  Returns the

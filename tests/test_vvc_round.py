@@ -200,3 +200,62 @@ def test_gradient_batch_against_oracle(which):
         assert all((h["g"][3][x] == 0).all() for x in range(3))
         for x in range(3):
             np.testing.assert_array_equal(h["g"][7][x], r["g"][7][x])
+
+
+def _round_scenarios(f, B, seed, lo=0.6, hi=1.4):
+    """B load scenarios of the control table that keep its (int) load tests (the
+    load lists are shared): entries whose test would flip keep the control's value."""
+    base = np.ascontiguousarray(f.Dl[:, 6:12].T)[:, :, None]
+    pq = base * np.random.default_rng(seed).uniform(lo, hi, size=(6, f.nl, B))
+    flip = (pq.astype(np.int64) != 0) != (base.astype(np.int64) != 0)
+    return np.ascontiguousarray(np.where(flip, base, pq))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["demo", "dlnew", "123bus"])
+def test_vvc_round_batch_against_oracle(which):
+    """fpf_vvc_round_batch (SURVEY 8(f) row 2's batched VVC Monte Carlo): B = 64
+    load scenarios, each a whole round -- gradient, all step sizes of all
+    scenarios as one device batch, the reversed searches as another -- against
+    ref_vvc.c's sequential vvc_main on that scenario's Dl (VoltVarCtrl.cpp:
+    1141-1762): stop indices, direction flag and whether S2 is sent identical;
+    c0 and the gradient 1e-10; the evaluated step losses 1e-10 (exact mode: the
+    oracle's roundings); the Q set-points after the round (S2 on the demo
+    feeder) 1e-9."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = {"demo": F.demo_feeder, "dlnew": F.dl_new_feeder, "123bus": lambda: F.synthetic_feeder(123, 123)}[which]()
+    B = 64
+    pq = _round_scenarios(f, B, 11)
+    pf = PowerFlow(f, exact=1)
+    r = pf.vvc_round_batch(f.Dl, pq)
+    assert r["n_bad"] == 0 and (r["rstatus"] == 0).all()
+    n_rev = 0
+    for s in range(B):
+        D = f.Dl.copy()
+        D[:, 6:12] = pq[:, :, s].T
+        o = O.vvc_main(D, f.Z)
+        assert o["rc"] == 0
+        for k in ("stop_fwd", "stop_rev", "reversed", "sent"):
+            assert r[k][s] == o[k], (k, s)
+        n_rev += int(o["reversed"])
+        assert r["ploss_orig"][s] == o["ploss_orig"]
+        for k in ("c0", "gmin", "gmax", "gabs_min", "ploss_after"):
+            assert r[k][s] == pytest.approx(o[k], rel=1e-10), (k, s)
+        for x in range(3):
+            np.testing.assert_allclose(r["g"][s][x], o["g"][x], rtol=1e-10, atol=0)
+        # the oracle keeps the loss at c_m for the steps it walked (0 .. stop)
+        st = o["stop_fwd"]
+        n_ev = st + 1 if st >= 0 else 100
+        np.testing.assert_allclose(r["loss_fwd"][s, :n_ev], o["loss_fwd"][:n_ev], rtol=1e-10)
+        if o["reversed"]:
+            sr = o["stop_rev"]
+            n_ev = sr + 1 if sr >= 0 else 100
+            np.testing.assert_allclose(r["loss_rev"][s, :n_ev], o["loss_rev"][:n_ev], rtol=1e-10)
+        after = r["pq"][:, :, s].T          # the load columns 6..11 after the round
+        np.testing.assert_allclose(after, o["Dl"][:, 6:12], rtol=1e-9, atol=1e-12)
+        if which == "demo":
+            Da = D.copy()
+            Da[:, 6:12] = after
+            np.testing.assert_allclose(vvc.s2_setpoints(Da), vvc.s2_setpoints(o["Dl"]), rtol=1e-9, atol=1e-12)
+    print(f"{which}: {n_rev} of {B} rounds reverse")

@@ -72,6 +72,12 @@ def main():
         n_sw = len(tops)
         d = {"staging": s[1] - s[0], "sld": s[2] - s[1], "sweeps": s[120] - s[2], "n_sweeps": n_sw,
              "v_out": s[121] - s[120], "total": s[121] - s[0]}
+        if s[3]:   # (scenario-major staging: the loads landed; stamps build waits for them there)
+            d["loads_landed"] = s[3] - s[0]
+        if s[122] and s[123]:   # after the post-loop extremes / guard, after the barrier
+            d["post_loop"] = s[122] - s[120]
+            d["barrier_wait"] = s[123] - s[122]
+            d["write_out"] = s[121] - s[123]
         d["per_sweep"] = d["sweeps"] / n_sw
         rows.append(d)
         for i, t in enumerate(tops):
@@ -81,6 +87,7 @@ def main():
     t0 = min(int(st[w][0]) for w in range(64) if st[w][0] != 0)
     entry = sorted(int(st[w][0]) - t0 for w in range(64) if st[w][0] != 0)
     keys = ["staging", "sld", "sweeps", "v_out", "total", "per_sweep", "n_sweeps"]
+    keys += [k for k in ("loads_landed", "post_loop", "barrier_wait", "write_out") if all(k in r for r in rows)]
     mean = {k: float(np.mean([r[k] for r in rows])) for k in keys}
     phm = np.mean(np.array(ph, dtype=np.float64), axis=0)
     print(json.dumps({"nn": nn, "B": B, "layout": layout, "base": base, "entry_spread": entry[::8],
