@@ -260,6 +260,55 @@ def config1_cpu(reps: int = 5):
     return out
 
 
+def round_scenarios(f, B: int, seed: int = 11, lo: float = 0.6, hi: float = 1.4) -> np.ndarray:
+    """B load scenarios ([6][Nl][B]) of a control table that keep its (int) load
+    tests (fpf_vvc_gradient_batch shares the load lists): entries whose test would
+    flip keep the control's value (tests/test_vvc_round.py)."""
+    base = np.ascontiguousarray(f.Dl[:, 6:12].T)[:, :, None]
+    pq = base * np.random.default_rng(seed).uniform(lo, hi, size=(6, f.nl, B))
+    flip = (pq.astype(np.int64) != 0) != (base.astype(np.int64) != 0)
+    return np.ascontiguousarray(np.where(flip, base, pq))
+
+
+def vvc_batch_leg(local: int, B: int = 64, cpu_sample: int = 8) -> dict:
+    """BASELINE config 1 as a Monte Carlo over loads: B whole VVC rounds
+    (fpf_vvc_round_batch: batched gradients, every scenario's 101 step sizes in
+    one batch, the reversed searches in another) per config-1 feeder, beside the
+    oracle's sequential vvc_main (VoltVarCtrl.cpp:1141-1762) on a sample of the
+    same scenarios, one core."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    out = {}
+    for name, f in config1_feeders():
+        pq = round_scenarios(f, B)
+        pf = PowerFlow(f, device=local)
+        r = pf.vvc_round_batch(f.Dl, pq)
+        tt = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = pf.vvc_round_batch(f.Dl, pq)
+            tt.append(time.perf_counter() - t0)
+        pf.close()
+        ts = []
+        agree = 0
+        for s in range(cpu_sample):
+            D = f.Dl.copy()
+            D[:, 6:12] = pq[:, :, s].T
+            t0 = time.perf_counter()
+            o = O.vvc_main(D, f.Z)
+            ts.append(time.perf_counter() - t0)
+            agree += int(all(int(r[k][s]) == int(o[k]) for k in ("stop_fwd", "stop_rev", "reversed", "sent")))
+        cpu_round_ms = float(np.median(ts)) * 1e3
+        out[name] = {"rounds": B, "gpu_ms": min(tt) * 1e3, "gpu_rounds_per_s": B / min(tt),
+                     "cpu_round_ms": cpu_round_ms, "cpu_rounds_per_s_one_core": 1e3 / cpu_round_ms,
+                     "speedup_vs_one_core": (B / min(tt)) / (1e3 / cpu_round_ms),
+                     "reversed": int(np.sum(r["reversed"])), "n_bad": int(r["n_bad"]),
+                     "decisions_equal_oracle": f"{agree}/{cpu_sample}"}
+    out["note"] = ("fpf_vvc_round_batch, host buffers, best of 3; CPU: oracle/ref_vvc.c vvc_main per scenario "
+                   "(median of a sample), one core; tests/test_vvc_round.py checks every scenario's decisions")
+    return out
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -529,6 +578,7 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-specialize", action="store_true")
     ap.add_argument("--exact", type=int, default=0, help="1: the reference's roundings (bit-identical mode)")
+    ap.add_argument("--no-guard", action="store_true", help="diagnostic: fast mode without the convergence guard")
     ap.add_argument("--layout", type=int, default=-1,
                     help="batch layout: 0 [6][Nl][B] (scenario fastest), 1 [B][6][Nl] (scenario major); "
                          "-1: the config's default (LAYOUT)")
@@ -577,7 +627,7 @@ def main():
     feeder = synthetic_feeder(n_nodes, f_seed)
     layout = LAYOUT[args.config] if args.layout < 0 else args.layout
     pf = PowerFlow(feeder, device=local, kernel=args.kernel, tile=args.tile, specialize=not args.no_specialize,
-                   exact=args.exact, layout=layout)
+                   exact=args.exact, layout=layout, no_guard=int(args.no_guard))
     B = args.scenarios or b_cfg
     pf.reserve(B)
     from freedm_amd import dist as D
@@ -858,6 +908,8 @@ def main():
             c1["note"] =("fpf_vvc_round (gradient + 101 step sizes in one batch + reversal), host-synchronous, "
                           "per config-1 feeder")
             res["config1_vvc_round"] = c1
+            if not args.no_cpu_baseline:
+                res["config1_vvc_round_batch"] = vvc_batch_leg(local)
         if world == 1 and args.config == 3 and not args.no_cpu_baseline and not args.nodes:
             # the 2048-bus feeder on the host: a bounded sample of 1024 scenarios
             cb = cpu_baseline(feeder, seconds=args.cpu_seconds, chunk=1024, config1=False,

@@ -83,7 +83,14 @@ struct fpf_areas {
     std::vector<int> order;      // solve order
     int cap = 0, vcap = 0;
     hipStream_t stream = nullptr;
-    double *d_pq = nullptr, *d_diff = nullptr;
+    // one stream and one "solved" event per area: within an outer iteration an
+    // area waits only for its parent (its source voltage), so siblings (and their
+    // subtrees) run concurrently; the check joins them all (FPF_AREAS_STREAMS=0:
+    // everything on `stream`)
+    std::vector<hipStream_t> astream;
+    std::vector<hipEvent_t> aev;
+    hipEvent_t ev_start = nullptr;
+    double *d_pq = nullptr, *d_diff = nullptr;   // d_diff: [area][B] boundary moves (each parent its own slice)
     // the whole-feeder results, one block so that one copy brings them back:
     // [ctl: done, outer, 2 pad (int32)][last move][loss B][vmin B][vmax B][status B (int8)]
     char *d_res = nullptr, *h_res = nullptr;   // h_res: pinned
@@ -141,6 +148,9 @@ extern "C" void fpf_areas_destroy(fpf_areas *a) {
     (void)hipHostFree(a->h_res);
     (void)hipFree(a->d_vre);
     (void)hipFree(a->d_vim);
+    for (hipEvent_t e : a->aev) (void)hipEventDestroy(e);
+    for (hipStream_t s : a->astream) (void)hipStreamDestroy(s);
+    if (a->ev_start) (void)hipEventDestroy(a->ev_start);
     if (a->stream) (void)hipStreamDestroy(a->stream);
     delete a;
 }
@@ -304,6 +314,21 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
         fpf_areas_destroy(a);
         return FPF_ERR_HIP;
     }
+    if (a->area.size() > 1 && !(getenv("FPF_AREAS_STREAMS") && atoi(getenv("FPF_AREAS_STREAMS")) == 0)) {
+        bool ok = hipEventCreateWithFlags(&a->ev_start, hipEventDisableTiming) == hipSuccess;
+        for (size_t i = 0; ok && i < a->area.size(); ++i) {
+            hipStream_t s = nullptr;
+            hipEvent_t e = nullptr;
+            ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+            if (ok) a->astream.push_back(s);
+            ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (ok) a->aev.push_back(e);
+        }
+        if (!ok) {
+            fpf_areas_destroy(a);
+            return FPF_ERR_HIP;
+        }
+    }
     o.kernel = FPF_KERNEL_WAVE;
     o.exact = 0;
     o.layout = FPF_LAYOUT_SCEN_FASTEST;   // fpf_areas_solve's arrays are [field][row][B] (include/freedm_pf.h)
@@ -348,7 +373,7 @@ static int areas_reserve(fpf_areas *a, int B, bool want_v) {
         a->d_res = a->h_res = nullptr;
         a->cap = 0;
         AHIP(a, hipMalloc(&a->d_pq, sizeof(double) * 6 * a->nl * b));
-        AHIP(a, hipMalloc(&a->d_diff, sizeof(double) * b));
+        AHIP(a, hipMalloc(&a->d_diff, sizeof(double) * b * a->area.size()));
         AHIP(a, hipMalloc(&a->d_res, res_bytes(b)));
         AHIP(a, hipHostMalloc((void **)&a->h_res, res_bytes(b), hipHostMallocDefault));
         for (Area &A : a->area) {
@@ -416,7 +441,8 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     int8_t *r_status = (int8_t *)(r_vmax + b);
     AHIP(a, hipMemcpyAsync(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice, st));
     AHIP(a, hipMemsetAsync(a->d_res, 0, RES_HEAD, st));
-    AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b, st));
+    AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b * a->area.size(), st));
+    const bool par = !a->astream.empty();
     // the area's loads and its working copy (the rows a child hangs off are
     // rewritten from the second iteration on: the first adds no child source power,
     // so neither the source powers nor the source voltages need clearing -- the
@@ -427,8 +453,11 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     // the previous one (a warm start: its sweeps then only follow the boundary's
     // move, instead of ~10 sweeps from the flat V0 to the inner tolerance)
     auto enqueue_iteration = [&](bool first, bool warm) -> int {
+        if (par) AHIP(a, hipEventRecord(a->ev_start, st));
         for (int ar : a->order) {
             Area &A = a->area[ar];
+            const hipStream_t sa = par ? a->astream[ar] : st;
+            if (par) AHIP(a, hipStreamWaitEvent(sa, A.parent >= 0 ? a->aev[A.parent] : a->ev_start, 0));
             // the boundary rows = their own load + the child's source power of the
             // previous iteration (every other row of d_work is the base, copied once);
             // all of an area's children in one launch (AREA_MAX_KIDS at a time)
@@ -438,7 +467,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
                     k.lrow[k.n] = A.kids[j].first;
                     k.ptr[k.n] = a->area[A.kids[j].second].d_sin;
                 }
-                AHIP(a, areas_add_rows(A.d_work, A.d_base, A.nl, B, k, ctl, st));
+                AHIP(a, areas_add_rows(A.d_work, A.d_base, A.nl, B, k, ctl, sa));
             }
             fpf_outputs o;
             std::memset(&o, 0, sizeof(o));
@@ -449,7 +478,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
             o.loss = A.d_loss;
             o.vmin = A.d_vmin;
             o.vmax = A.d_vmax;
-            const int r = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)st,
+            const int r = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)sa,
                                                 A.parent >= 0 ? A.d_vsrc : nullptr, A.d_sin, FPF_LAYOUT_SCEN_FASTEST,
                                                 nullptr, ctl, warm ? A.d_vre : nullptr, warm ? A.d_vim : nullptr);
             if (r < 0) return afail(a, r, std::string("area solve: ") + fpf_last_error(a->ctx));
@@ -462,10 +491,13 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
                     k.lrow[k.n] = Ch.lb;
                     k.ptr[k.n] = Ch.d_vsrc;
                 }
-                AHIP(a, areas_gather_vsrc_all(A.d_vre, A.d_vim, A.nn, B, k, a->d_diff, ctl, st));
+                AHIP(a, areas_gather_vsrc_all(A.d_vre, A.d_vim, A.nn, B, k, a->d_diff + (size_t)ar * b, ctl, sa));
             }
+            if (par) AHIP(a, hipEventRecord(a->aev[ar], sa));
         }
-        AHIP(a, areas_check(a->d_diff, B, tol, single, ctl, last, st));
+        if (par)
+            for (size_t ar = 0; ar < a->area.size(); ++ar) AHIP(a, hipStreamWaitEvent(st, a->aev[ar], 0));
+        AHIP(a, areas_check(a->d_diff, (int)(b * a->area.size()), tol, single, ctl, last, st));
         return FPF_OK;
     };
     // chunks of K iterations; the flag of chunk c is read after chunk c + 1 is enqueued

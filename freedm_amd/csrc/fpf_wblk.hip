@@ -185,9 +185,13 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     __syncthreads();
     if (WABL(4)) return;
 
+    // flat start (V = V0 on every node, DPF_return7.cpp:92-96, the feeder's own
+    // source): the first sweep's load currents use the uniform 1/|V0_p|^2 and take
+    // the guard record's sum from their Sld reads
+    const bool flat = !o.vsrc && !o.vinit_re;
     // the guard record: sum_k |S_k|_1 of the scenario (wtb[7], read after the loop;
     // Sld is overwritten by V in the last sweep)
-    if (GUARD_CODE && o.flag_count) {
+    if (GUARD_CODE && o.flag_count && !flat) {
         double a = 0.0;
 #pragma unroll
         for (int c = 0; c < C; ++c)
@@ -225,10 +229,28 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     for (;; ++it) {
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
+        if (flat && it == 0) {
+            // IL = conj(S/V0) = conj(S) V0 / |V0|^2 (V0 != 0)
+            double a = 0.0;
 #pragma unroll
-        for (int c = 0; c < C; ++c)
+            for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(stg, p * PS + sb[c]), v[c][p]);   // 0 on a zeroed phase
+                for (int p = 0; p < 3; ++p) {
+                    const cx x = ldx(stg, p * PS + sb[c]);
+                    const double vr = f.V0[2 * p], vi = f.V0[2 * p + 1], r0 = f.rv0[p];
+                    il[c][p] = mk(fma(x.re, vr, x.im * vi) * r0, fma(x.re, vi, -(x.im * vr)) * r0);
+                    a += fabs(x.re) + fabs(x.im);
+                }
+            if (GUARD_CODE && o.flag_count) {
+                a = seg_incl<64>(a);
+                if (lane == 63) wtb[8 * wv + 7] = a;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(stg, p * PS + sb[c]), v[c][p]);   // 0 on a zeroed phase
+        }
 
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of
         // IL: lane-local prefix, wavefront scan, the totals of the waves before
