@@ -95,6 +95,15 @@ extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr, int base) {
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
 constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging keeps in flight
+// the scenario-fastest batches' staging through the tables too (measured slower:
+// 44.1-44.5 vs 39.4-39.8 us on config 2, profiles/r04e); the feeder tables' loads
+// issued before the tile's (FPF_WAVE_EARLY_TABLES) or after its LDS stores
+#ifndef FPF_WAVE_L0_TABLE
+#define FPF_WAVE_L0_TABLE 0
+#endif
+#ifndef FPF_WAVE_EARLY_TABLES
+#define FPF_WAVE_EARLY_TABLES 1
+#endif
 
 // experiments (tools/gpu_ab_trees.sh): IBO_LDS keeps the substation current of the
 // previous sweep (the convergence test's Ibo) in the scenario's LDS region instead
@@ -205,27 +214,33 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         // together with the tile's loads; stored to LDS after them
         constexpr int UT = (9 * C * L + NT - 1) / NT;
         double2 tt[TEMP_IN_LDS ? UT : 1];
-        if (TEMP_IN_LDS) {
-#pragma unroll
-            for (int u = 0; u < UT; ++u) {
-                const int i = u * NT + (int)threadIdx.x;
-                tt[u] = ld_global2(f.slot_temp, i < ntm * C * L ? i : 0);
-            }
-        }
         const int np2 = 2 * bdepth * nblk;
-        const int pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
-        const int kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
+        int pv = 0, kv = 0;
+        auto table_loads = [&]() {
+            if (TEMP_IN_LDS) {
+#pragma unroll
+                for (int u = 0; u < UT; ++u) {
+                    const int i = u * NT + (int)threadIdx.x;
+                    tt[u] = ld_global2(f.slot_temp, i < ntm * C * L ? i : 0);
+                }
+            }
+            pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
+            kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
+        };
+        if (FPF_WAVE_EARLY_TABLES) table_loads();
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
         typedef double d2v __attribute__((ext_vector_type(2)));
         constexpr int US = WAVE_STAGE_U;
         const int SU = f.stage_u;
-        if (SU > 0 && (o.smaj || (B & 1) == 0)) {
+        if (SU > 0 && (o.smaj || (FPF_WAVE_L0_TABLE && (B & 1) == 0))) {
             // table-driven (wave_stage_tables): chunk c = u NT + t, 16 bytes each, every
             // load of the thread in flight with its two STG destinations; scenario
             // major: the tile is one contiguous block of nsb x 6 Nl doubles;
             // scenario fastest: chunk c is scenarios (2 (t % H), + 1) of pq line tb.x
-            const int nchunk = DBG(256) ? 0 : nsb * 3 * nl;
+            // valid chunks: scenario major, the first nsb scenarios' (contiguous);
+            // scenario fastest, every line of the pairs below nsb
+            const int nchunk = DBG(256) ? 0 : (o.smaj ? nsb : SPB) * 3 * nl;
             constexpr int H = SPB / 2;
             const int jj = 2 * ((int)threadIdx.x % H);
             const int2 *tab = (const int2 *)(o.smaj ? f.stage_smaj : f.stage_l0);
@@ -241,7 +256,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     if (o.smaj) {
                         r[u] = __builtin_nontemporal_load(src + (ok ? c : 0));
                     } else {
-                        const size_t ga = (size_t)tb[u].x * B + s0 + jj;
+                        // (the line of chunk c is t / H + u NT / H: the load does not
+                        // wait for the table entry)
+                        const int fr = (int)threadIdx.x / H + u * (NT / H);
+                        const size_t ga = (size_t)fr * B + s0 + jj;
                         r[u] = __builtin_nontemporal_load((const d2v *)(pq + (ok ? ga : 0)));
                         r[u] = ok ? r[u] : d2v{0.0, 0.0};
                     }
@@ -359,6 +377,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 if (i < total) sd[spos(i / SPB, i % SPB)] = r[u] * inv_s3;
             }
         }
+        if (!FPF_WAVE_EARLY_TABLES) table_loads();
         if (TEMP_IN_LDS) {
 #pragma unroll
             for (int u = 0; u < UT; ++u) {

@@ -229,13 +229,18 @@ def test_vvc_round_batch_against_oracle(which):
     pq = _round_scenarios(f, B, 11)
     pf = PowerFlow(f, exact=1)
     r = pf.vvc_round_batch(f.Dl, pq)
-    assert r["n_bad"] == 0 and (r["rstatus"] == 0).all()
-    n_rev = 0
+    assert (r["rstatus"] == 0).all(), r["rstatus"]
+    n_rev = n_throw = 0
     for s in range(B):
         D = f.Dl.copy()
         D[:, 6:12] = pq[:, :, s].T
         o = O.vvc_main(D, f.Z)
-        assert o["rc"] == 0
+        # a step the reference solves does not converge: it throws (rc != 0), the
+        # batch flags the scenario (res[12]); nothing after that point is compared
+        assert r["nonconv"][s] == (1 if o["rc"] != 0 else 0), (s, o["rc"])
+        if o["rc"] != 0:
+            n_throw += 1
+            continue
         for k in ("stop_fwd", "stop_rev", "reversed", "sent"):
             assert r[k][s] == o[k], (k, s)
         n_rev += int(o["reversed"])
@@ -252,10 +257,14 @@ def test_vvc_round_batch_against_oracle(which):
             sr = o["stop_rev"]
             n_ev = sr + 1 if sr >= 0 else 100
             np.testing.assert_allclose(r["loss_rev"][s, :n_ev], o["loss_rev"][:n_ev], rtol=1e-10)
-        after = r["pq"][:, :, s].T          # the load columns 6..11 after the round
-        np.testing.assert_allclose(after, o["Dl"][:, 6:12], rtol=1e-9, atol=1e-12)
+        # the load columns 6..11 after the round: Q - g (bkva/3) c_stop cancels where
+        # the set-point moves close to zero, so the bar is 1e-9 of the column's scale
+        after = r["pq"][:, :, s].T
+        ref = o["Dl"][:, 6:12]
+        np.testing.assert_allclose(after, ref, rtol=1e-9, atol=1e-9 * float(np.abs(ref).max()))
         if which == "demo":
             Da = D.copy()
             Da[:, 6:12] = after
             np.testing.assert_allclose(vvc.s2_setpoints(Da), vvc.s2_setpoints(o["Dl"]), rtol=1e-9, atol=1e-12)
-    print(f"{which}: {n_rev} of {B} rounds reverse")
+    assert r["n_bad"] == n_throw
+    print(f"{which}: {n_rev} of {B} rounds reverse, {n_throw} would throw")
