@@ -48,8 +48,9 @@ CONFIGS = {2: (123, 123, 4096, 4096, "scenario"),
            4: (123, 123, 131072, 1 << 20, "hosting")}
 # batch layout each config is benched in (fpf_opts.layout; --layout overrides)
 # (measured, profiles/r02e_layout: config 3 17.5 -> 9.9 ms per launch and
-# config 4 1.14 -> 1.06 ms with [B][6][Nl]; config 2 39.4 vs 41.0 us)
-LAYOUT = {2: 0, 3: 1, 4: 1}
+# config 4 1.14 -> 1.06 ms with [B][6][Nl]; config 2 39.4 vs 41.0 us then; since the
+# table-driven scenario-major staging, profiles/r04f: config 2 38.6-39.1 vs 40.6-41.1 us)
+LAYOUT = {2: 1, 3: 1, 4: 1}
 
 
 def bytes_alg_per_scenario(nb: int, nn: int) -> int:

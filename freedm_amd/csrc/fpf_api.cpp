@@ -1831,9 +1831,17 @@ extern "C" int fpf_solve_batch_device(fpf_feeder *f, int n_scen, const double *d
                                       f ? f->opts.layout : 0);
 }
 
+bool fpf::wave_hooks_supported(fpf_feeder *f, int n_scen) {
+    if (kernel_for(f, n_scen) != FPF_KERNEL_WAVE || f->wdev.wps || f->wdev.coop) return false;
+    const WaveDev w = wave_dev_for(f, n_scen);
+    return !w.wps && !w.coop;
+}
+
 int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                                void *stream, const double *d_vsrc, double *d_s_in, int layout, unsigned *d_flag_out,
-                               const int32_t *d_skip, const double *d_vinit_re, const double *d_vinit_im) {
+                               const int32_t *d_skip, const double *d_vinit_re, const double *d_vinit_im,
+                               const AreaHook *d_hook, unsigned long long *d_move, const double *d_eps,
+                               const AreaLink *d_check, unsigned *d_check_ticket) {
     if (!f || n_scen < 0 || (n_scen > 0 && !d_pq)) return fail(f ? f->ctx : nullptr, FPF_ERR_ARG, "bad arguments");
     fpf_ctx *ctx = f->ctx;
     if (n_scen == 0) return FPF_OK;
@@ -1852,6 +1860,14 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     o.skip = d_skip;
     o.vinit_re = d_vinit_re;
     o.vinit_im = d_vinit_im;
+    o.hook = d_hook;
+    o.move = d_move;
+    o.eps_dev = d_eps;
+    o.check = d_check;
+    o.check_ticket = d_check_ticket;
+    if ((d_hook || d_eps || d_check) && (!d_move || !d_skip || (d_check && !d_check_ticket) ||
+                                         !wave_hooks_supported(f, n_scen)))
+        return fail(ctx, FPF_ERR_UNSUPPORTED, "area hooks: the plain wave kernel only, with a move slot");
     if ((d_vinit_re != nullptr) != (d_vinit_im != nullptr) || (d_vinit_re && o.smaj))
         return fail(ctx, FPF_ERR_ARG, "warm start: both planes, scenario-fastest batches only");
     hipError_t e;

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -36,18 +37,14 @@
 #include "fpf_internal.h"
 
 namespace fpf {
-hipError_t areas_gather_rows(const double *src, int nl_src, const int32_t *row, int nl, int B, double *dst,
-                             double *dst2, hipStream_t st);
-hipError_t areas_add_rows(double *work, const double *base, int nl, int B, const AreaKids &k, const int32_t *ctl,
-                          hipStream_t st);
-hipError_t areas_gather_vsrc_all(const double *v_re, const double *v_im, int nn, int B, const AreaKids &k, double *diff,
-                                 const int32_t *ctl, hipStream_t st);
+hipError_t areas_gather_rows(const double *src, const int32_t *map, int rows, int B, double *dst, hipStream_t st);
+hipError_t areas_link(const AreaLink &L, int B, int32_t *ctl, hipStream_t st);
+hipError_t areas_subtree_sums(const double *pq, int nl, int B, int n_areas, const int32_t *sub_off,
+                              const int32_t *sub_rows, double *s_in, double *eps_dev, double eps_first, hipStream_t st);
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
                                hipStream_t st);
-hipError_t areas_fold_results(int B, const double *loss, const double *vmin, const double *vmax, const int8_t *status,
-                              int first, double *o_loss, double *o_vmin, double *o_vmax, int8_t *o_status,
-                              hipStream_t st);
-hipError_t areas_check(double *diff, int n, double tol, int single, int32_t *ctl, double *last, hipStream_t st);
+hipError_t areas_fold_results(int B, const AreaFold &F, double *o_loss, double *o_vmin, double *o_vmax,
+                              int8_t *o_status, hipStream_t st);
 }  // namespace fpf
 
 using namespace fpf;
@@ -63,10 +60,14 @@ struct Area {
     std::vector<int32_t> mono;           // local node -> monolithic node (local 0 -> bus)
     std::vector<int> local_of;           // monolithic node -> local node (-1: not here)
     std::vector<std::pair<int, int>> kids;   // (local row carrying the bus's load, child area)
+    std::vector<int32_t> sub_rows;       // monolithic rows of the area's whole subtree (its own and its descendants')
     fpf_feeder *feeder = nullptr;
     // device buffers
-    int32_t *d_rows = nullptr, *d_mono = nullptr;
-    double *d_base = nullptr, *d_work = nullptr, *d_vsrc = nullptr, *d_sin = nullptr;
+    int32_t *d_mono = nullptr;
+    size_t roff = 0;             // the area's first line in fpf_areas::d_base / d_work
+    double *d_base = nullptr, *d_work = nullptr;   // [6][nl][B] in fpf_areas::d_base / d_work (not owned)
+    double *d_vsrc = nullptr;
+    double *d_sin = nullptr;   // [6][B] in fpf_areas::d_sin (not owned)
     double *d_vre = nullptr, *d_vim = nullptr, *d_loss = nullptr, *d_vmin = nullptr, *d_vmax = nullptr;
     int32_t *d_iters = nullptr;
     int8_t *d_status = nullptr;
@@ -77,20 +78,49 @@ struct fpf_areas {
     fpf_ctx *ctx = nullptr;
     int nl = 0, ncols = 0, nn = 0;
     double lb_v = 0.96, ub_v = 1.05;   // the hosting counters of the aggregate (fpf_opts)
+    double eps = 1e-4;                 // the areas' inner eps (fpf_opts)
+    // inexact outer iterations (with hooks, more than one area): the first
+    // iteration's solves run to eps_first, each later one to inexact x the
+    // previous boundary move, never looser than eps_first nor tighter than eps --
+    // the early iterations' areas stop sweeping once they are as accurate as
+    // their boundary is; the loop stops only after an iteration solved to eps.
+    // FPF_AREAS_INEXACT (0: off) / FPF_AREAS_EPS_FIRST
+    double inexact = 1e-2, eps_first = 1e-6;
     bool warm = true;                  // warm-started area solves (FPF_AREAS_WARM=0: flat V0 each time)
     int last_outer = 0;                // the previous solve's outer iterations (the first chunk's size)
     std::vector<Area> area;      // index = area id, parents before children
     std::vector<int> order;      // solve order
     int cap = 0, vcap = 0;
     hipStream_t stream = nullptr;
-    // one stream and one "solved" event per area: within an outer iteration an
-    // area waits only for its parent (its source voltage), so siblings (and their
-    // subtrees) run concurrently; the check joins them all (FPF_AREAS_STREAMS=0:
-    // everything on `stream`)
+    // when some area has more than one child area: one stream and one "solved"
+    // event per area -- within an outer iteration an area waits only for its
+    // parent (its source voltage), so siblings (and their subtrees) run
+    // concurrently; the check joins them all.  Otherwise (a chain of areas, where
+    // nothing can overlap) everything on `stream`: the cross-stream waits cost
+    // about 11 us each (profiles/r04h_c5).  FPF_AREAS_STREAMS=0 / 1 forces either.
     std::vector<hipStream_t> astream;
     std::vector<hipEvent_t> aev;
     hipEvent_t ev_start = nullptr;
-    double *d_pq = nullptr, *d_diff = nullptr;   // d_diff: [area][B] boundary moves (each parent its own slice)
+    double *d_pq = nullptr;
+    double *d_sin = nullptr;                       // [area][6][B] children's source powers
+    unsigned long long *d_move = nullptr;          // [2] the iteration's boundary move (by parity, link_kernel)
+    int32_t *d_sub_off = nullptr, *d_sub_rows = nullptr;   // Area::sub_rows of every area, CSR
+    // the links folded into the area solves (AreaHook, one per area; the plain wave
+    // kernel for every area, at most AREA_MAX_KIDS children each): an outer
+    // iteration is then its n_areas solves and one stop-test launch.
+    // FPF_AREAS_HOOKS=0: separate link launches (A/B)
+    AreaHook *d_hook = nullptr;
+    bool hooks_env = true;
+    // every area's loads, one block: [sum of 6 nl][B] (gathered from the feeder's
+    // batch by d_gmap in one launch), and the working copy of the link launches
+    double *d_base = nullptr, *d_work = nullptr;
+    int32_t *d_gmap = nullptr;
+    int n_gmap = 0;
+    // the stop test fused into the last area's solve (OutDev::check): its
+    // arguments by iteration parity, and the workgroups' ticket
+    AreaLink h_check[2];
+    AreaLink *d_check = nullptr;
+    unsigned *d_ticket = nullptr;
     // the whole-feeder results, one block so that one copy brings them back:
     // [ctl: done, outer, 2 pad (int32)][last move][loss B][vmin B][vmax B][status B (int8)]
     char *d_res = nullptr, *h_res = nullptr;   // h_res: pinned
@@ -99,7 +129,7 @@ struct fpf_areas {
 };
 
 namespace {
-constexpr size_t RES_HEAD = 32;   // ctl (16 bytes) + the last boundary move (8) + pad
+constexpr size_t RES_HEAD = 32;   // ctl (16 bytes) + the last boundary move (8) + the inexact inner eps (8)
 size_t res_bytes(size_t B) { return RES_HEAD + 24 * B + ((B + 7) & ~(size_t)7); }
 }  // namespace
 
@@ -115,10 +145,7 @@ int afail(fpf_areas *a, int code, const std::string &msg) {
     } while (0)
 
 void free_area_buffers(Area &ar) {
-    (void)hipFree(ar.d_base);
-    (void)hipFree(ar.d_work);
     (void)hipFree(ar.d_vsrc);
-    (void)hipFree(ar.d_sin);
     (void)hipFree(ar.d_vre);
     (void)hipFree(ar.d_vim);
     (void)hipFree(ar.d_loss);
@@ -138,12 +165,20 @@ extern "C" void fpf_areas_destroy(fpf_areas *a) {
     if (a->ctx) (void)hipSetDevice(ctx_device(a->ctx));
     for (Area &ar : a->area) {
         free_area_buffers(ar);
-        (void)hipFree(ar.d_rows);
         (void)hipFree(ar.d_mono);
         fpf_feeder_destroy(ar.feeder);
     }
     (void)hipFree(a->d_pq);
-    (void)hipFree(a->d_diff);
+    (void)hipFree(a->d_sin);
+    (void)hipFree(a->d_move);
+    (void)hipFree(a->d_hook);
+    (void)hipFree(a->d_base);
+    (void)hipFree(a->d_work);
+    (void)hipFree(a->d_gmap);
+    (void)hipFree(a->d_check);
+    (void)hipFree(a->d_ticket);
+    (void)hipFree(a->d_sub_off);
+    (void)hipFree(a->d_sub_rows);
     (void)hipFree(a->d_res);
     (void)hipHostFree(a->h_res);
     (void)hipFree(a->d_vre);
@@ -292,6 +327,11 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
         }
         P.kids.push_back({lrow, ar});
     }
+    // every non-root area's subtree rows (the first iteration's source-power estimate)
+    for (int ar = 0; ar < n_areas; ++ar)
+        for (int d = ar; d >= 0 && a->area[d].parent >= 0; d = a->area[d].parent)
+            for (int32_t m : a->area[ar].row_of_local)
+                if (m >= 0) a->area[d].sub_rows.push_back(m);
     // solve order: parents first
     std::vector<int> depth(n_areas, 0);
     for (int ar = 0; ar < n_areas; ++ar)
@@ -308,13 +348,20 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
     if (opts) o = *opts;
     else fpf_opts_default(&o);
     a->lb_v = o.lb_v;
+    a->eps = o.eps;
+    if (const char *e = getenv("FPF_AREAS_INEXACT")) a->inexact = atof(e);
+    if (const char *e = getenv("FPF_AREAS_EPS_FIRST")) a->eps_first = atof(e);
     a->ub_v = o.ub_v;
     if (const char *e = getenv("FPF_AREAS_WARM")) a->warm = atoi(e) != 0;   // (A/B, tests)
+    if (const char *e = getenv("FPF_AREAS_HOOKS")) a->hooks_env = atoi(e) != 0;
     if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
         fpf_areas_destroy(a);
         return FPF_ERR_HIP;
     }
-    if (a->area.size() > 1 && !(getenv("FPF_AREAS_STREAMS") && atoi(getenv("FPF_AREAS_STREAMS")) == 0)) {
+    bool branching = false;
+    for (const Area &A : a->area) branching = branching || A.kids.size() > 1;
+    if (const char *e = getenv("FPF_AREAS_STREAMS")) branching = atoi(e) != 0;
+    if (a->area.size() > 1 && branching) {
         bool ok = hipEventCreateWithFlags(&a->ev_start, hipEventDisableTiming) == hipSuccess;
         for (size_t i = 0; ok && i < a->area.size(); ++i) {
             hipStream_t s = nullptr;
@@ -332,6 +379,42 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
     o.kernel = FPF_KERNEL_WAVE;
     o.exact = 0;
     o.layout = FPF_LAYOUT_SCEN_FASTEST;   // fpf_areas_solve's arrays are [field][row][B] (include/freedm_pf.h)
+    {
+        // the areas' lines of the feeder's batch: area after area, [field][local row]
+        std::vector<int32_t> gmap;
+        for (Area &A : a->area) {
+            A.roff = gmap.size();
+            for (int f = 0; f < 6; ++f)
+                for (int r = 0; r < A.nl; ++r)
+                    gmap.push_back(A.row_of_local[r] < 0 ? -1 : f * nl + A.row_of_local[r]);
+        }
+        a->n_gmap = (int)gmap.size();
+        if (hipMalloc(&a->d_gmap, sizeof(int32_t) * gmap.size()) != hipSuccess ||
+            hipMalloc(&a->d_check, 2 * sizeof(AreaLink)) != hipSuccess ||
+            hipMalloc(&a->d_ticket, sizeof(unsigned)) != hipSuccess ||
+            hipMemset(a->d_ticket, 0, sizeof(unsigned)) != hipSuccess ||
+            hipMemcpy(a->d_gmap, gmap.data(), sizeof(int32_t) * gmap.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            fpf_areas_destroy(a);
+            return FPF_ERR_HIP;
+        }
+    }
+    {
+        std::vector<int32_t> off(1, 0), rows;
+        for (const Area &A : a->area) {
+            rows.insert(rows.end(), A.sub_rows.begin(), A.sub_rows.end());
+            off.push_back((int32_t)rows.size());
+        }
+        if (rows.empty()) rows.push_back(0);
+        if (hipMalloc(&a->d_sub_off, sizeof(int32_t) * off.size()) != hipSuccess ||
+            hipMalloc(&a->d_sub_rows, sizeof(int32_t) * rows.size()) != hipSuccess ||
+            hipMalloc(&a->d_move, 2 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc(&a->d_hook, sizeof(AreaHook) * a->area.size()) != hipSuccess ||
+            hipMemcpy(a->d_sub_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(a->d_sub_rows, rows.data(), sizeof(int32_t) * rows.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            fpf_areas_destroy(a);
+            return FPF_ERR_HIP;
+        }
+    }
     for (Area &A : a->area) {
         const int rc = fpf_feeder_create(ctx, A.dl.data(), A.nl, ncols, z, z_rows, z_cols, &o, &A.feeder);
         if (rc != FPF_OK) {
@@ -339,9 +422,7 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
             fpf_areas_destroy(a);
             return rc;
         }
-        if (hipMalloc(&A.d_rows, sizeof(int32_t) * A.nl) != hipSuccess ||
-            hipMalloc(&A.d_mono, sizeof(int32_t) * A.nn) != hipSuccess ||
-            hipMemcpy(A.d_rows, A.row_of_local.data(), sizeof(int32_t) * A.nl, hipMemcpyHostToDevice) != hipSuccess ||
+        if (hipMalloc(&A.d_mono, sizeof(int32_t) * A.nn) != hipSuccess ||
             hipMemcpy(A.d_mono, A.mono.data(), sizeof(int32_t) * A.nn, hipMemcpyHostToDevice) != hipSuccess) {
             fpf_areas_destroy(a);
             return FPF_ERR_HIP;
@@ -366,21 +447,28 @@ static int areas_reserve(fpf_areas *a, int B, bool want_v) {
     if (B > a->cap) {
         for (Area &A : a->area) free_area_buffers(A);
         (void)hipFree(a->d_pq);
-        (void)hipFree(a->d_diff);
+        (void)hipFree(a->d_sin);
+        (void)hipFree(a->d_base);
+        (void)hipFree(a->d_work);
         (void)hipFree(a->d_res);
         (void)hipHostFree(a->h_res);
-        a->d_pq = a->d_diff = nullptr;
+        a->d_pq = a->d_sin = a->d_base = a->d_work = nullptr;
         a->d_res = a->h_res = nullptr;
         a->cap = 0;
         AHIP(a, hipMalloc(&a->d_pq, sizeof(double) * 6 * a->nl * b));
-        AHIP(a, hipMalloc(&a->d_diff, sizeof(double) * b * a->area.size()));
+        AHIP(a, hipMalloc(&a->d_sin, sizeof(double) * 6 * b * a->area.size()));
         AHIP(a, hipMalloc(&a->d_res, res_bytes(b)));
-        AHIP(a, hipHostMalloc((void **)&a->h_res, res_bytes(b), hipHostMallocDefault));
+        AHIP(a, hipHostMalloc((void **)&a->h_res, res_bytes(b) + 16, hipHostMallocDefault));   // + the flag slots
+        AHIP(a, hipMalloc(&a->d_base, sizeof(double) * a->n_gmap * b));
+        AHIP(a, hipMalloc(&a->d_work, sizeof(double) * a->n_gmap * b));
+        for (size_t ar = 0; ar < a->area.size(); ++ar) {
+            Area &A = a->area[ar];
+            A.d_sin = a->d_sin + ar * 6 * b;
+            A.d_base = a->d_base + A.roff * b;
+            A.d_work = a->d_work + A.roff * b;
+        }
         for (Area &A : a->area) {
-            AHIP(a, hipMalloc(&A.d_base, sizeof(double) * 6 * A.nl * b));
-            AHIP(a, hipMalloc(&A.d_work, sizeof(double) * 6 * A.nl * b));
             AHIP(a, hipMalloc(&A.d_vsrc, sizeof(double) * 6 * b));
-            AHIP(a, hipMalloc(&A.d_sin, sizeof(double) * 6 * b));
             AHIP(a, hipMalloc(&A.d_vre, sizeof(double) * 3 * A.nn * b));
             AHIP(a, hipMalloc(&A.d_vim, sizeof(double) * 3 * A.nn * b));
             AHIP(a, hipMalloc(&A.d_loss, sizeof(double) * b));
@@ -389,6 +477,22 @@ static int areas_reserve(fpf_areas *a, int B, bool want_v) {
             AHIP(a, hipMalloc(&A.d_iters, sizeof(int32_t) * b));
             AHIP(a, hipMalloc(&A.d_status, sizeof(int8_t) * b));
         }
+        // the hooks point at the buffers just allocated
+        std::vector<AreaHook> hk(a->area.size());
+        for (size_t ar = 0; ar < a->area.size(); ++ar) {
+            const Area &A = a->area[ar];
+            AreaHook &h = hk[ar];
+            std::memset(&h, 0, sizeof(h));
+            for (size_t j = 0; j < A.kids.size() && j < (size_t)AREA_MAX_KIDS; ++j) {
+                const Area &Ch = a->area[A.kids[j].second];
+                h.pre_lrow[j] = A.kids[j].first;
+                h.pre_sin[j] = Ch.d_sin;
+                h.post_lb[j] = Ch.lb;
+                h.post_vsrc[j] = Ch.d_vsrc;
+            }
+            h.pre_n = h.post_n = (int)std::min(A.kids.size(), (size_t)AREA_MAX_KIDS);
+        }
+        AHIP(a, hipMemcpy(a->d_hook, hk.data(), sizeof(AreaHook) * hk.size(), hipMemcpyHostToDevice));
         a->cap = B;
     }
     if (want_v && B > a->vcap) {
@@ -408,8 +512,8 @@ static int areas_reserve(fpf_areas *a, int B, bool want_v) {
 // area; FPF_NONCONVERGED also when the outer loop did not reach tol), loss
 // (sum over areas), vmin / vmax (over areas).  vpolar / pqb / pql must be NULL.
 //
-// Schedule: every launch on the object's stream, no host round trip inside the
-// outer loop.  The convergence test is a device flag (check_kernel: ctl[0]);
+// Schedule: no host round trip inside the outer loop.  The convergence test is a
+// device flag (link_kernel's stop test: ctl[0]);
 // every kernel of an iteration enqueued after it is set does nothing.  The host
 // enqueues iterations in chunks and looks at the flag of chunk c (an 8-byte
 // copy into pinned memory) only after chunk c + 1 is enqueued, so the GPU never
@@ -441,68 +545,186 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     int8_t *r_status = (int8_t *)(r_vmax + b);
     AHIP(a, hipMemcpyAsync(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice, st));
     AHIP(a, hipMemsetAsync(a->d_res, 0, RES_HEAD, st));
-    AHIP(a, hipMemsetAsync(a->d_diff, 0, sizeof(double) * b * a->area.size(), st));
+    AHIP(a, hipMemsetAsync(a->d_move, 0, 2 * sizeof(unsigned long long), st));
     const bool par = !a->astream.empty();
-    // the area's loads and its working copy (the rows a child hangs off are
-    // rewritten from the second iteration on: the first adds no child source power,
-    // so neither the source powers nor the source voltages need clearing -- the
-    // first check never stops the loop)
-    for (Area &A : a->area) AHIP(a, areas_gather_rows(a->d_pq, a->nl, A.d_rows, A.nl, B, A.d_base, A.d_work, st));
     const int single = a->area.size() == 1 ? 1 : 0;
+    // the areas' loads and their working copies (the rows a child hangs off are
+    // rewritten every iteration, every other row of d_work is the base, copied
+    // once), and the first iteration's source powers: each child's subtree load
+    bool hooks = a->hooks_env;
+    for (Area &A : a->area) hooks = hooks && A.kids.size() <= (size_t)AREA_MAX_KIDS && wave_hooks_supported(A.feeder, B);
+    AHIP(a, areas_gather_rows(a->d_pq, a->d_gmap, a->n_gmap, B, a->d_base, st));
+    if (!hooks)
+        AHIP(a, hipMemcpyAsync(a->d_work, a->d_base, sizeof(double) * a->n_gmap * b, hipMemcpyDeviceToDevice, st));
+    // (the inexact iterations' inner eps, RES_HEAD's last 8 bytes, set by that launch)
+    const bool inexact = hooks && !single && a->inexact > 0 && a->eps_first > a->eps;
+    double *eps_dev = inexact ? (double *)(a->d_res + 24) : nullptr;
+    AHIP(a, areas_subtree_sums(a->d_pq, a->nl, B, (int)a->area.size(), a->d_sub_off, a->d_sub_rows, a->d_sin, eps_dev,
+                               a->eps_first, st));
+    // the stop test's arguments for iteration `it`
+    auto fill_check = [&](AreaLink &L, int it) {
+        L.move_acc = a->d_move + (it & 1);
+        L.move_chk = a->d_move + (it & 1);
+        L.move_clr = a->d_move + ((it + 1) & 1);
+        L.last = last;
+        L.tol = tol;
+        L.single = single;
+        L.eps_dev = eps_dev;
+        L.eps = a->eps;
+        L.eps_first = a->eps_first;
+        L.inexact = a->inexact;
+    };
+    // one stream with hooks: the stop test runs in the last area's solve
+    const bool fused_check = hooks && !par;
+    if (fused_check) {
+        for (int p = 0; p < 2; ++p) {
+            std::memset(&a->h_check[p], 0, sizeof(AreaLink));
+            fill_check(a->h_check[p], p);
+            a->h_check[p].check = 1;
+        }
+        AHIP(a, hipMemcpyAsync(a->d_check, a->h_check, sizeof(a->h_check), hipMemcpyHostToDevice, st));
+    }
+    // one link launch (link_kernel): the children's source voltages after `post`'s
+    // solve, the child rows of `pre` before its solve, the stop test of iteration
+    // `it` (AREA_MAX_KIDS children of each at a time)
+    auto link = [&](const Area *post, const Area *pre, bool check, int it, hipStream_t s) -> int {
+        const size_t np = post ? post->kids.size() : 0, nq = pre ? pre->kids.size() : 0;
+        const size_t n = std::max<size_t>(std::max((np + AREA_MAX_KIDS - 1) / AREA_MAX_KIDS,
+                                                   (nq + AREA_MAX_KIDS - 1) / AREA_MAX_KIDS), check ? 1 : 0);
+        for (size_t c = 0; c < n; ++c) {
+            AreaLink L{};
+            if (post) {
+                L.v_re = post->d_vre;
+                L.v_im = post->d_vim;
+                L.nn = post->nn;
+                for (size_t j = c * AREA_MAX_KIDS; j < np && L.post.n < AREA_MAX_KIDS; ++j, ++L.post.n) {
+                    const Area &Ch = a->area[post->kids[j].second];
+                    L.post.lrow[L.post.n] = Ch.lb;
+                    L.post.ptr[L.post.n] = Ch.d_vsrc;
+                }
+            }
+            if (pre) {
+                L.work = pre->d_work;
+                L.base = pre->d_base;
+                L.nl = pre->nl;
+                for (size_t j = c * AREA_MAX_KIDS; j < nq && L.pre.n < AREA_MAX_KIDS; ++j, ++L.pre.n) {
+                    L.pre.lrow[L.pre.n] = pre->kids[j].first;
+                    L.pre.ptr[L.pre.n] = a->area[pre->kids[j].second].d_sin;
+                }
+            }
+            fill_check(L, it);
+            // the stop test reads the move once every post of the iteration is done:
+            // in its own launch after them (the last area in the order has no children)
+            L.check = check && c + 1 == n ? 1 : 0;
+            if (L.check && L.post.n > 0) return afail(a, FPF_ERR_TOPOLOGY, "areas: stop test fused with a post link");
+            AHIP(a, areas_link(L, B, ctl, s));
+        }
+        return FPF_OK;
+    };
+    auto solve_area = [&](Area &A, bool warm, int it, hipStream_t s, bool check) -> int {
+        fpf_outputs o;
+        std::memset(&o, 0, sizeof(o));
+        o.v_re = A.d_vre;
+        o.v_im = A.d_vim;
+        o.iters = A.d_iters;
+        o.status = (signed char *)A.d_status;
+        o.loss = A.d_loss;
+        o.vmin = A.d_vmin;
+        o.vmax = A.d_vmax;
+        const size_t ai = (size_t)(&A - a->area.data());
+        const int r = solve_batch_device_ex(A.feeder, B, hooks ? A.d_base : A.d_work, &o, nullptr, (void *)s,
+                                            A.parent >= 0 ? A.d_vsrc : nullptr, A.d_sin, FPF_LAYOUT_SCEN_FASTEST,
+                                            nullptr, ctl, warm ? A.d_vre : nullptr, warm ? A.d_vim : nullptr,
+                                            hooks ? a->d_hook + ai : nullptr, hooks ? a->d_move + (it & 1) : nullptr,
+                                            eps_dev, check ? a->d_check + (it & 1) : nullptr,
+                                            check ? a->d_ticket : nullptr);
+        if (r < 0) return afail(a, r, std::string("area solve: ") + fpf_last_error(a->ctx));
+        static const bool dbg = getenv("FPF_AREAS_DEBUG") && atoi(getenv("FPF_AREAS_DEBUG")) != 0;
+        if (dbg) {   // (diagnostics: every area solve's sweeps; synchronises)
+            std::vector<int32_t> h(b);
+            AHIP(a, hipMemcpyAsync(h.data(), A.d_iters, sizeof(int32_t) * b, hipMemcpyDeviceToHost, s));
+            AHIP(a, hipStreamSynchronize(s));
+            long sum = 0;
+            int mx = 0;
+            for (int32_t x : h) sum += x, mx = std::max(mx, (int)x);
+            fprintf(stderr, "areas it %d area %d: sweeps mean %.2f max %d\n", it, (int)ai, (double)sum / B, mx);
+        }
+        return FPF_OK;
+    };
     // from the second outer iteration on, every area solve starts from its own V of
     // the previous one (a warm start: its sweeps then only follow the boundary's
-    // move, instead of ~10 sweeps from the flat V0 to the inner tolerance)
-    auto enqueue_iteration = [&](bool first, bool warm) -> int {
-        if (par) AHIP(a, hipEventRecord(a->ev_start, st));
+    // move, instead of ~10 sweeps from the flat V0 to the inner tolerance).
+    // With hooks: the solves (each its links folded in), then the stop test --
+    // on one stream, or each area on its stream after its parent's.  Without:
+    // one stream: solve, link(post this, pre next), ..., the last link also the
+    // stop test and the root's rows of the next iteration -- n_areas solves and
+    // n_areas links per iteration; per-area streams: each area's pre link, solve
+    // and post link on its stream after its parent's; the stop test joins them.
+    auto enqueue_iteration = [&](int it, bool warm) -> int {
+        int r = FPF_OK;
+        if (fused_check) {
+            for (size_t i = 0; !r && i < a->order.size(); ++i)
+                r = solve_area(a->area[a->order[i]], warm, it, st, i + 1 == a->order.size());
+            return r;
+        }
+        if (!par) {
+            if (it == 0) r = link(nullptr, &a->area[a->order[0]], false, it, st);
+            for (size_t i = 0; !r && i < a->order.size(); ++i) {
+                Area &A = a->area[a->order[i]];
+                r = solve_area(A, warm, it, st, false);
+                const bool last_area = i + 1 == a->order.size();
+                if (!r) r = link(&A, &a->area[a->order[last_area ? 0 : i + 1]], last_area, it, st);
+            }
+            return r;
+        }
+        AHIP(a, hipEventRecord(a->ev_start, st));
         for (int ar : a->order) {
             Area &A = a->area[ar];
-            const hipStream_t sa = par ? a->astream[ar] : st;
-            if (par) AHIP(a, hipStreamWaitEvent(sa, A.parent >= 0 ? a->aev[A.parent] : a->ev_start, 0));
-            // the boundary rows = their own load + the child's source power of the
-            // previous iteration (every other row of d_work is the base, copied once);
-            // all of an area's children in one launch (AREA_MAX_KIDS at a time)
-            for (size_t j0 = 0; !first && j0 < A.kids.size(); j0 += AREA_MAX_KIDS) {
-                AreaKids k{};
-                for (size_t j = j0; j < A.kids.size() && k.n < AREA_MAX_KIDS; ++j, ++k.n) {
-                    k.lrow[k.n] = A.kids[j].first;
-                    k.ptr[k.n] = a->area[A.kids[j].second].d_sin;
-                }
-                AHIP(a, areas_add_rows(A.d_work, A.d_base, A.nl, B, k, ctl, sa));
-            }
-            fpf_outputs o;
-            std::memset(&o, 0, sizeof(o));
-            o.v_re = A.d_vre;
-            o.v_im = A.d_vim;
-            o.iters = A.d_iters;
-            o.status = (signed char *)A.d_status;
-            o.loss = A.d_loss;
-            o.vmin = A.d_vmin;
-            o.vmax = A.d_vmax;
-            const int r = solve_batch_device_ex(A.feeder, B, A.d_work, &o, nullptr, (void *)sa,
-                                                A.parent >= 0 ? A.d_vsrc : nullptr, A.d_sin, FPF_LAYOUT_SCEN_FASTEST,
-                                                nullptr, ctl, warm ? A.d_vre : nullptr, warm ? A.d_vim : nullptr);
-            if (r < 0) return afail(a, r, std::string("area solve: ") + fpf_last_error(a->ctx));
-            // this area's V at every child's boundary bus: the children's source
-            // voltages of this iteration (solved next, in order), one launch
-            for (size_t j0 = 0; j0 < A.kids.size(); j0 += AREA_MAX_KIDS) {
-                AreaKids k{};
-                for (size_t j = j0; j < A.kids.size() && k.n < AREA_MAX_KIDS; ++j, ++k.n) {
-                    const Area &Ch = a->area[A.kids[j].second];
-                    k.lrow[k.n] = Ch.lb;
-                    k.ptr[k.n] = Ch.d_vsrc;
-                }
-                AHIP(a, areas_gather_vsrc_all(A.d_vre, A.d_vim, A.nn, B, k, a->d_diff + (size_t)ar * b, ctl, sa));
-            }
-            if (par) AHIP(a, hipEventRecord(a->aev[ar], sa));
+            const hipStream_t sa = a->astream[ar];
+            AHIP(a, hipStreamWaitEvent(sa, A.parent >= 0 ? a->aev[A.parent] : a->ev_start, 0));
+            if (!hooks && !A.kids.empty()) r = link(nullptr, &A, false, it, sa);
+            if (!r) r = solve_area(A, warm, it, sa, false);
+            if (!r && !hooks && !A.kids.empty()) r = link(&A, nullptr, false, it, sa);
+            if (r) return r;
+            AHIP(a, hipEventRecord(a->aev[ar], sa));
         }
-        if (par)
-            for (size_t ar = 0; ar < a->area.size(); ++ar) AHIP(a, hipStreamWaitEvent(st, a->aev[ar], 0));
-        AHIP(a, areas_check(a->d_diff, (int)(b * a->area.size()), tol, single, ctl, last, st));
+        for (size_t ar = 0; ar < a->area.size(); ++ar) AHIP(a, hipStreamWaitEvent(st, a->aev[ar], 0));
+        return link(nullptr, nullptr, true, it, st);
+    };
+    // results in the feeder's numbering; whole-feeder loss / extremes / status.
+    // Without V they are enqueued after every chunk (before its flag is looked
+    // at): the chunk that ends the loop then needs no further launch
+    auto enqueue_results = [&](bool with_v) -> int {
+        AreaFold F{};
+        F.first = 1;
+        for (size_t i = 0; i < a->order.size(); ++i) {
+            const Area &A = a->area[a->order[i]];
+            F.loss[F.n] = A.d_loss;
+            F.vmin[F.n] = A.d_vmin;
+            F.vmax[F.n] = A.d_vmax;
+            F.status[F.n] = A.d_status;
+            if (++F.n == AREA_MAX_FOLD || i + 1 == a->order.size()) {
+                AHIP(a, areas_fold_results(B, F, r_loss, r_vmin, r_vmax, r_status, st));
+                F.n = 0;
+                F.first = 0;
+            }
+        }
+        for (int ar : a->order) {
+            Area &A = a->area[ar];
+            if (with_v) {
+                // the root area's local node 0 is the substation (monolithic node 0)
+                const int k0 = A.parent < 0 ? 0 : 1;
+                AHIP(a, areas_scatter_nodes(A.d_vre, A.nn, k0, A.d_mono, a->nn, B, a->d_vre, st));
+                AHIP(a, areas_scatter_nodes(A.d_vim, A.nn, k0, A.d_mono, a->nn, B, a->d_vim, st));
+            }
+        }
+        AHIP(a, hipMemcpyAsync(a->h_res, a->d_res, res_bytes(b), hipMemcpyDeviceToHost, st));
         return FPF_OK;
     };
     // chunks of K iterations; the flag of chunk c is read after chunk c + 1 is enqueued
     const int K = 2;
-    int32_t *h_ctl[2] = {(int32_t *)a->h_res, (int32_t *)a->h_res + 2};   // two 8-byte slots in the pinned head
+    int32_t *const h_flag = (int32_t *)(a->h_res + res_bytes(b));
+    int32_t *h_ctl[2] = {h_flag, h_flag + 2};   // two 8-byte slots after the pinned results
     hipEvent_t ev[2] = {nullptr, nullptr};
     AHIP(a, hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
     AHIP(a, hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
@@ -515,11 +737,15 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     while (!stop && enq < max_outer) {
         const int n_it = chunk == 0 && first_chunk ? first_chunk : K;
         for (int i = 0; i < n_it && enq < max_outer; ++i, ++enq) {
-            rc = enqueue_iteration(enq == 0, enq > 0 && a->warm);
+            rc = enqueue_iteration(enq, enq > 0 && a->warm);
             if (rc) break;
         }
         if (rc) break;
         AHIP(a, hipMemcpyAsync(h_ctl[chunk & 1], ctl, 8, hipMemcpyDeviceToHost, st));
+        if (!want_v) {
+            rc = enqueue_results(false);
+            if (rc) break;
+        }
         AHIP(a, hipEventRecord(ev[chunk & 1], st));
         if (chunk == 0 && first_chunk) {
             AHIP(a, hipEventSynchronize(ev[0]));
@@ -536,21 +762,10 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
         (void)hipStreamSynchronize(st);
         return rc;
     }
-    // results in the feeder's numbering; whole-feeder loss / extremes / status
-    bool first = true;
-    for (int ar : a->order) {
-        Area &A = a->area[ar];
-        AHIP(a, areas_fold_results(B, A.d_loss, A.d_vmin, A.d_vmax, A.d_status, first ? 1 : 0, r_loss, r_vmin, r_vmax,
-                                   r_status, st));
-        first = false;
-        if (want_v) {
-            // the root area's local node 0 is the substation (monolithic node 0)
-            const int k0 = A.parent < 0 ? 0 : 1;
-            AHIP(a, areas_scatter_nodes(A.d_vre, A.nn, k0, A.d_mono, a->nn, B, a->d_vre, st));
-            AHIP(a, areas_scatter_nodes(A.d_vim, A.nn, k0, A.d_mono, a->nn, B, a->d_vim, st));
-        }
+    if (want_v) {
+        rc = enqueue_results(true);
+        if (rc) return rc;
     }
-    AHIP(a, hipMemcpyAsync(a->h_res, a->d_res, res_bytes(b), hipMemcpyDeviceToHost, st));
     if (u.v_re) AHIP(a, hipMemcpyAsync(u.v_re, a->d_vre, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost, st));
     if (u.v_im) AHIP(a, hipMemcpyAsync(u.v_im, a->d_vim, sizeof(double) * 3 * a->nn * b, hipMemcpyDeviceToHost, st));
     AHIP(a, hipStreamSynchronize(st));

@@ -237,6 +237,19 @@ struct OutDev {
     // iteration's V of the area) instead of the flat V0 of DPF_return7.cpp:92-96.
     // NULL: the reference's flat start
     const double *vinit_re, *vinit_im;
+    // the multi-area solve's links folded into the solve (plain wave kernel only,
+    // fpf_areas.cpp): device memory, NULL: none.  move: the outer iteration's
+    // boundary-move slot (an atomic max of the double's bits)
+    const struct AreaHook *hook;
+    unsigned long long *move;
+    // the convergence test's eps for this launch (device memory; wave kernel, no
+    // guard); NULL: fpf_opts.eps
+    const double *eps_dev;
+    // the multi-area solve's stop test fused into the last area's solve: the
+    // workgroup that takes the last ticket runs areas_stop_test(*check, ctl)
+    // (ctl = the skip flag's array).  NULL: none
+    const struct AreaLink *check;
+    unsigned *check_ticket;
 };
 
 // The exact re-solve of flagged scenarios (fpf_generic.hip: dpf_fixup_kernel):
@@ -255,7 +268,10 @@ int ctx_device(const fpf_ctx *ctx);   // the HIP device of a context
 int solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                           void *stream, const double *d_vsrc, double *d_s_in, int layout,
                           unsigned *d_flag_out = nullptr, const int32_t *d_skip = nullptr,
-                          const double *d_vinit_re = nullptr, const double *d_vinit_im = nullptr);
+                          const double *d_vinit_re = nullptr, const double *d_vinit_im = nullptr,
+                          const AreaHook *d_hook = nullptr, unsigned long long *d_move = nullptr,
+                          const double *d_eps = nullptr, const AreaLink *d_check = nullptr,
+                          unsigned *d_check_ticket = nullptr);
 // the exact re-solve of the scenarios a deferred (d_flag_out) guarded solve flagged
 int fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                        void *stream, int layout);
@@ -300,6 +316,61 @@ struct AreaKids {
     int lrow[AREA_MAX_KIDS];
     double *ptr[AREA_MAX_KIDS];
 };
+// the links of one area folded into its wave-kernel solve (OutDev::hook): after
+// the loads are staged, the rows its children hang off get the children's source
+// powers added (pre: base + s_in, scaled like the loads); after the sweeps, each
+// child's boundary bus voltage (local node post_lb >= 1) becomes its source
+// voltage and the largest move joins *OutDev::move
+struct AreaHook {
+    int pre_n, post_n;
+    int pre_lrow[AREA_MAX_KIDS], post_lb[AREA_MAX_KIDS];
+    const double *pre_sin[AREA_MAX_KIDS];
+    double *post_vsrc[AREA_MAX_KIDS];
+};
+// the per-scenario results of up to AREA_MAX_FOLD areas, folded in one launch
+constexpr int AREA_MAX_FOLD = 8;
+struct AreaFold {
+    int n, first;
+    const double *loss[AREA_MAX_FOLD], *vmin[AREA_MAX_FOLD], *vmax[AREA_MAX_FOLD];
+    const int8_t *status[AREA_MAX_FOLD];
+};
+// whether an area solve of n scenarios runs the plain wave kernel (hooks apply)
+bool wave_hooks_supported(fpf_feeder *f, int n_scen);
+// one launch between two area solves of an outer iteration (fpf_areas.cpp): the
+// solved area's children's source voltages (post; V [3][nn][B]), the next area's
+// child rows (pre; work / base [6][nl][B]), the iteration's stop test (check)
+struct AreaLink {
+    const double *v_re, *v_im;
+    int nn, nl;
+    AreaKids post, pre;
+    double *work;
+    const double *base;
+    unsigned long long *move_acc, *move_chk, *move_clr;   // the iteration's move (two slots, by parity)
+    double *last;
+    double tol;
+    int check, single;
+    // inexact outer iterations (check): the next iteration's inner eps
+    // *eps_dev = clamp(inexact * move, eps, eps_first); stop only after an
+    // iteration solved to eps itself.  eps_dev NULL: every solve to eps
+    double *eps_dev;
+    double eps, eps_first, inexact;
+};
+// the end of an outer iteration (link_kernel, or the last workgroup of the last
+// area's solve: OutDev::check), once every boundary move of the iteration is in:
+// the outer count, the move, the next iteration's inner eps, the stop flag ctl[0]
+__device__ inline void areas_stop_test(const AreaLink &L, int32_t *ctl) {
+    const double m = __longlong_as_double((long long)*L.move_chk);
+    const int outer = ctl[1] + 1;
+    ctl[1] = outer;
+    *L.last = m;
+    *L.move_clr = 0ull;
+    bool exact = true;   // this iteration's solves ran to eps
+    if (L.eps_dev) {
+        exact = *L.eps_dev <= L.eps;
+        *L.eps_dev = fmax(L.eps, fmin(L.eps_first, L.inexact * m));
+    }
+    if (L.single || (outer > 1 && m <= L.tol && exact)) ctl[0] = 1;
+}
 constexpr int COOP_NSLOT = 1024;   // exchange areas of the paired kernel (scenarios in flight <= 256)
 inline size_t wave_any_lds_bytes(const WaveDev &w) {
     return w.coop ? wcoop_lds_bytes(w) : (w.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w));

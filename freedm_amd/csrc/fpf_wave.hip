@@ -97,12 +97,13 @@ constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deepe
 constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging keeps in flight
 // the scenario-fastest batches' staging through the tables too (measured slower:
 // 44.1-44.5 vs 39.4-39.8 us on config 2, profiles/r04e); the feeder tables' loads
-// issued before the tile's (FPF_WAVE_EARLY_TABLES) or after its LDS stores
+// issued before the tile's (FPF_WAVE_EARLY_TABLES) or after its LDS stores (the
+// default: config 4 0.942-0.945 vs 0.953-0.958 ms, config 2 equal, profiles/r04f)
 #ifndef FPF_WAVE_L0_TABLE
 #define FPF_WAVE_L0_TABLE 0
 #endif
 #ifndef FPF_WAVE_EARLY_TABLES
-#define FPF_WAVE_EARLY_TABLES 1
+#define FPF_WAVE_EARLY_TABLES 0
 #endif
 
 // experiments (tools/gpu_ab_trees.sh): IBO_LDS keeps the substation current of the
@@ -389,6 +390,19 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         for (int i = threadIdx.x + NT; i < np2; i += NT) pairs[i] = f.blk_pairs[i];
         if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
     }
+    if (o.hook && o.hook->pre_n > 0) {
+        // the multi-area solve (OutDev::hook): the rows children hang off carry
+        // their source powers too, scaled like the loads
+        __syncthreads();
+        const AreaHook *const h = o.hook;
+        double *const sd = (double *)stg;
+        for (int i = threadIdx.x; i < h->pre_n * 6 * SPB; i += NT) {
+            const int j = i % SPB, q = i / SPB, kid = q / 6, fq = q % 6;
+            if (j < nsb)
+                sd[2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(h->pre_lrow[kid])) * SROW + j) + (fq & 1)] +=
+                    h->pre_sin[kid][(size_t)fq * B + s0 + j] * inv_s3;
+        }
+    }
     __syncthreads();
     WSTAMP(1);
     if (DBG(8192)) return;
@@ -442,6 +456,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     // source): the first sweep's load currents use the uniform 1/|V0_p|^2, and
     // sum_k |S_k|_1 of the guard record is taken from that sweep's Sld reads
     const bool flat = !o.vsrc && !o.vinit_re;
+    // the convergence test's eps^2 (the multi-area solve's inexact outer
+    // iterations pass their own, OutDev::eps_dev)
+    const double eps2 = o.eps_dev ? *o.eps_dev * *o.eps_dev : f.eps * f.eps;
     // the guard record V0S[3] = (sum_k |S_k|_1, closest |err2 - eps^2| of a decision
     // in the coarse band, +inf: none) of the scenario, in LDS (fpf_api.cpp: guard_factor)
     if (o.flag_count && !flat) {
@@ -586,7 +603,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             for (int p = 0; p < 3; ++p) stx(IBO, p, tot[p]);
         }
         // decided in the segment's last lane, broadcast by ballot
-        const unsigned long long cbits = __ballot(li == L - 1 && err2 < f.eps * f.eps);
+        const unsigned long long cbits = __ballot(li == L - 1 && err2 < eps2);
         const bool conv = (cbits >> (seg * L + L - 1)) & 1;
         const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
         if (o.flag_count) {
@@ -940,6 +957,24 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     WSTAMP(122);
     __syncthreads();
     WSTAMP(123);
+    if (o.hook && o.hook->post_n > 0) {
+        // the multi-area solve (OutDev::hook): each child's source voltage = V at
+        // its boundary bus, the largest move into the iteration's slot
+        const AreaHook *const h = o.hook;
+        double d = 0.0;
+        for (int i = threadIdx.x; i < h->post_n * 3 * SPB; i += NT) {
+            const int j = i % SPB, q = i / SPB, kid = q / 3, p = q % 3;
+            if (j < nsb) {
+                const double2 vv = stg[p * PSTR + swz_row(h->post_lb[kid] - 1) * SROW + j];
+                double *const vs = h->post_vsrc[kid] + (size_t)(2 * p) * B + s0 + j;
+                d = fmax(d, fmax(fabs(vv.x - vs[0]), fabs(vv.y - vs[B])));
+                vs[0] = vv.x;
+                vs[B] = vv.y;
+            }
+        }
+        for (int w = 32; w > 0; w >>= 1) d = fmax(d, __shfl_xor(d, w));
+        if (lane == 0 && d > 0.0) atomicMax(o.move, (unsigned long long)__double_as_longlong(d));
+    }
     __shared__ int last_wg;
     const bool agg = o.agg && !DBG(2048);
     if (agg && threadIdx.x == 0) {
@@ -1072,6 +1107,15 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // (every workgroup's flags were appended before its ticket)
             if (threadIdx.x == 0 && o.flag_out)
                 *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (o.check && threadIdx.x == 0) {
+        // the multi-area solve's stop test (OutDev::check): the last workgroup to
+        // finish (every workgroup has passed the skip test by then)
+        const unsigned t = __hip_atomic_fetch_add(o.check_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            areas_stop_test(*o.check, (int32_t *)o.skip);
+            __hip_atomic_store(o.check_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     if (o.fix_dev) {

@@ -266,7 +266,8 @@ void        fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate 
  * connected subtree, the area of bus 1 is the root.  Every area is solved as
  * its own feeder fed from its boundary bus (fast mode, wave kernel, the
  * opts' eps / mxitr), parents first, children's source power added to their
- * boundary bus as a load, until no boundary voltage moves by more than tol
+ * boundary bus as a load (the first outer iteration: the child subtree's total
+ * load), until no boundary voltage moves by more than tol
  * (p.u.) or max_outer outer iterations.  This algorithm has no reference
  * counterpart: at its fixed point V is the monolithic solution (to the
  * solver tolerances).  out (host): v_re / v_im in the feeder's numbering,

@@ -32,9 +32,19 @@ def _tight_monolithic(f, pq):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["auto", "streams0", "streams1", "links"])
 @pytest.mark.parametrize("case", ["demo_sst", "123bus_3areas", "123bus_nested"])
-def test_areas_equal_monolithic(case):
+def test_areas_equal_monolithic(case, mode, monkeypatch):
+    """Every schedule (fpf_areas.cpp): the links folded into the area solves
+    (AreaHook, the default) or launched between them (FPF_AREAS_HOOKS=0), on one
+    stream (the default for a chain of areas) or one stream per area (the
+    default when an area has several child areas; FPF_AREAS_STREAMS=0 / 1
+    forces either)."""
     from freedm_amd import AreaPowerFlow
+    if mode.startswith("streams"):
+        monkeypatch.setenv("FPF_AREAS_STREAMS", mode[-1])
+    if mode == "links":
+        monkeypatch.setenv("FPF_AREAS_HOOKS", "0")
     if case == "demo_sst":
         f = F.demo_feeder()
         node_area = F.sst_node_areas(f)
