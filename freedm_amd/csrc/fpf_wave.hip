@@ -102,6 +102,9 @@ constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging
 #ifndef FPF_WAVE_L0_TABLE
 #define FPF_WAVE_L0_TABLE 0
 #endif
+#ifndef FPF_WAVE_LATE_VINIT   // the warm start's loads after the staging barrier (A/B)
+#define FPF_WAVE_LATE_VINIT 0
+#endif
 #ifndef FPF_WAVE_EARLY_TABLES
 #define FPF_WAVE_EARLY_TABLES 0
 #endif
@@ -194,6 +197,22 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         bk[c] = f.slot_blk[c * L + li];
     }
     const double inv_s3 = 1.0 / f.s3;
+
+    // the multi-area solve's warm start (OutDev::vinit_re / _im): node k of each
+    // slot from the given V, loaded before the tile's loads so that their
+    // latencies overlap (the slot's node from the global table: LDS is not staged)
+    cx v[C][3];
+    const bool warm = o.vinit_re && live && !FPF_WAVE_LATE_VINIT;
+    if (warm) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (si_valid(si[c])) {
+                const int k = f.slot_node[c * L + li];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    v[c][p] = mk(o.vinit_re[((size_t)p * nn + k) * B + s], o.vinit_im[((size_t)p * nn + k) * B + s]);
+            }
+    }
 
     // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced (16 scenarios = one
     // 128-byte line per row), all of a thread's loads in flight, into STG scaled
@@ -422,7 +441,6 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 
     // the source voltage: V0 (DPF_return7.cpp:84-89), or this scenario's when the
     // caller supplies one (an area of the multi-area solve, fed from its boundary bus)
-    cx v[C][3];
     {
         cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
         if (o.vsrc && live) {
@@ -432,9 +450,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         if (li < 3) stx(V0S, li, li == 0 ? v0[0] : (li == 1 ? v0[1] : v0[2]));
 #pragma unroll
         for (int c = 0; c < C; ++c)
+            if (!warm || !si_valid(si[c]))
 #pragma unroll
-            for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
-        if (o.vinit_re && live) {
+                for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
+        if (o.vinit_re && live && FPF_WAVE_LATE_VINIT) {
             // the multi-area solve's warm start: node k of each slot from the given V
 #pragma unroll
             for (int c = 0; c < C; ++c)
