@@ -85,7 +85,7 @@ struct fpf_areas {
     // the early iterations' areas stop sweeping once they are as accurate as
     // their boundary is; the loop stops only after an iteration solved to eps.
     // FPF_AREAS_INEXACT (0: off) / FPF_AREAS_EPS_FIRST
-    double inexact = 1e-2, eps_first = 1e-6;
+    double inexact = 1e-4, eps_first = 1e-6;
     bool warm = true;                  // warm-started area solves (FPF_AREAS_WARM=0: flat V0 each time)
     int last_outer = 0;                // the previous solve's outer iterations (the first chunk's size)
     std::vector<Area> area;      // index = area id, parents before children
@@ -118,7 +118,7 @@ struct fpf_areas {
     int n_gmap = 0;
     // the stop test fused into the last area's solve (OutDev::check): its
     // arguments by iteration parity, and the workgroups' ticket
-    AreaLink h_check[2];
+    AreaLink h_check[2] = {};
     AreaLink *d_check = nullptr;
     unsigned *d_ticket = nullptr;
     // the whole-feeder results, one block so that one copy brings them back:
@@ -354,6 +354,7 @@ extern "C" int fpf_areas_create(fpf_ctx *ctx, const double *dl, int nl, int ncol
     a->ub_v = o.ub_v;
     if (const char *e = getenv("FPF_AREAS_WARM")) a->warm = atoi(e) != 0;   // (A/B, tests)
     if (const char *e = getenv("FPF_AREAS_HOOKS")) a->hooks_env = atoi(e) != 0;
+
     if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
         fpf_areas_destroy(a);
         return FPF_ERR_HIP;
@@ -577,12 +578,16 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     // one stream with hooks: the stop test runs in the last area's solve
     const bool fused_check = hooks && !par;
     if (fused_check) {
+        AreaLink hc[2];
         for (int p = 0; p < 2; ++p) {
-            std::memset(&a->h_check[p], 0, sizeof(AreaLink));
-            fill_check(a->h_check[p], p);
-            a->h_check[p].check = 1;
+            std::memset(&hc[p], 0, sizeof(AreaLink));
+            fill_check(hc[p], p);
+            hc[p].check = 1;
         }
-        AHIP(a, hipMemcpyAsync(a->d_check, a->h_check, sizeof(a->h_check), hipMemcpyHostToDevice, st));
+        if (std::memcmp(hc, a->h_check, sizeof(hc)) != 0) {   // (the same as the previous solve's: no copy)
+            std::memcpy(a->h_check, hc, sizeof(hc));
+            AHIP(a, hipMemcpyAsync(a->d_check, a->h_check, sizeof(a->h_check), hipMemcpyHostToDevice, st));
+        }
     }
     // one link launch (link_kernel): the children's source voltages after `post`'s
     // solve, the child rows of `pre` before its solve, the stop test of iteration
@@ -647,7 +652,10 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
             long sum = 0;
             int mx = 0;
             for (int32_t x : h) sum += x, mx = std::max(mx, (int)x);
-            fprintf(stderr, "areas it %d area %d: sweeps mean %.2f max %d\n", it, (int)ai, (double)sum / B, mx);
+            double mv = 0.0;
+            if (check) AHIP(a, hipMemcpy(&mv, last, 8, hipMemcpyDeviceToHost));
+            fprintf(stderr, "areas it %d area %d: sweeps mean %.2f max %d%s%.3e\n", it, (int)ai, (double)sum / B, mx,
+                    check ? ", boundary move " : "", check ? mv : 0.0);
         }
         return FPF_OK;
     };

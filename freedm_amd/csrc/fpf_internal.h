@@ -365,11 +365,12 @@ __device__ inline void areas_stop_test(const AreaLink &L, int32_t *ctl) {
     *L.last = m;
     *L.move_clr = 0ull;
     bool exact = true;   // this iteration's solves ran to eps
-    if (L.eps_dev) {
-        exact = *L.eps_dev <= L.eps;
-        *L.eps_dev = fmax(L.eps, fmin(L.eps_first, L.inexact * m));
-    }
-    if (L.single || (outer > 1 && m <= L.tol && exact)) ctl[0] = 1;
+    if (L.eps_dev) exact = *L.eps_dev <= L.eps;
+    const bool done = L.single || (outer > 1 && m <= L.tol && exact);
+    // (the first iteration's move compares with the previous solve's source
+    // voltages: it does not set the next eps)
+    if (L.eps_dev) *L.eps_dev = outer == 1 ? L.eps_first : fmax(L.eps, fmin(L.eps_first, L.inexact * m));
+    if (done) ctl[0] = 1;
 }
 constexpr int COOP_NSLOT = 1024;   // exchange areas of the paired kernel (scenarios in flight <= 256)
 inline size_t wave_any_lds_bytes(const WaveDev &w) {

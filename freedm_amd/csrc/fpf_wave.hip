@@ -127,6 +127,11 @@ struct WaveGeom {
     // waves per SIMD the registers allow (light outputs; the full-output variants of
     // the larger geometries keep 2 and their registers)
     static constexpr int MINW = SPW * C <= 2 ? 4 : (C <= 2 ? 3 : 2);
+    // what a workgroup of WPB waves can use of it: whole workgroups per CU (4
+    // SIMDs) -- 3 waves per SIMD with 8-wave workgroups is still one workgroup per
+    // CU, so those take the registers of 2 (config 5's 36-bus area: 37 scratch
+    // loads per sweep at the 168-VGPR cap, none at 256)
+    template <int WPB> static constexpr int eff_minw() { return (MINW * 4 / WPB) * WPB / 4; }
 };
 
 // the TEMP blocks are staged in LDS once per workgroup (a diagnostic build
@@ -139,7 +144,7 @@ constexpr bool TEMP_IN_LDS = true;
 #endif
 
 template <int SPW, int C, bool FULL, int WPB>
-__global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, C>::MINW)) void dpf_wave_kernel(
+__global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, C>::template eff_minw<WPB>())) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
     constexpr int L = WaveGeom<SPW, C>::L, SPB = WPB * SPW;
     constexpr int NT = WPB * 64;
