@@ -101,3 +101,26 @@ def test_areas_schedule_and_aggregate():
     assert ag["n_under"] == int((r["vmin"] < 0.96).sum()) and ag["n_over"] == int((r["vmax"] > 1.05).sum())
     assert ag["n_under"] + ag["n_over"] > 0 or (r["vmin"] >= 0.96).all()
     ap.close()
+
+
+@pytest.mark.gpu
+def test_areas_wave_block_root_uses_link_launches():
+    """An area too large for the per-wavefront kernel (a 600-bus feeder's root
+    area: the wave-block kernel, which has no area hooks) runs the link-launch
+    schedule (fpf_areas.cpp: hooks only when every area solves on the wave
+    kernel) and still meets the monolithic solve to 1e-10."""
+    from freedm_amd import AreaPowerFlow
+    f = F.synthetic_feeder(600, 600)
+    node_area = F.subtree_node_areas(f, [450])
+    ap = AreaPowerFlow(f, node_area)
+    assert len(ap.area_nodes) == 2 and max(ap.area_nodes) > 257
+    pq = F.scenario_loads(f, np.arange(32))
+    r = ap.solve(pq, tol=1e-13, max_outer=100)
+    c = _tight_monolithic(f, pq)
+    assert (c["status"] == 0).all() and (r["status"] == 0).all(), r["note"]
+    v = r["V_re"] + 1j * r["V_im"]
+    vc = c["V_re"] + 1j * c["V_im"]
+    rel = float(np.max(np.abs(v - vc) / np.abs(vc)))
+    assert rel <= 1e-10, (rel, r["note"])
+    np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-8)
+    ap.close()
