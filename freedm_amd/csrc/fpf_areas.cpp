@@ -37,10 +37,10 @@
 #include "fpf_internal.h"
 
 namespace fpf {
-hipError_t areas_gather_rows(const double *src, const int32_t *map, int rows, int B, double *dst, hipStream_t st);
+hipError_t areas_setup(const double *src, int nl, const int32_t *map, int rows, int B, double *dst, int n_areas,
+                       const int32_t *sub_off, const int32_t *sub_rows, double *s_in, int32_t *ctl, double *last,
+                       unsigned long long *move, double *eps_dev, double eps_first, hipStream_t st);
 hipError_t areas_link(const AreaLink &L, int B, int32_t *ctl, hipStream_t st);
-hipError_t areas_subtree_sums(const double *pq, int nl, int B, int n_areas, const int32_t *sub_off,
-                              const int32_t *sub_rows, double *s_in, double *eps_dev, double eps_first, hipStream_t st);
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
                                hipStream_t st);
 hipError_t areas_fold_results(int B, const AreaFold &F, double *o_loss, double *o_vmin, double *o_vmax,
@@ -545,8 +545,6 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     double *r_loss = (double *)(a->d_res + RES_HEAD), *r_vmin = r_loss + b, *r_vmax = r_vmin + b;
     int8_t *r_status = (int8_t *)(r_vmax + b);
     AHIP(a, hipMemcpyAsync(a->d_pq, pq, sizeof(double) * 6 * a->nl * b, hipMemcpyHostToDevice, st));
-    AHIP(a, hipMemsetAsync(a->d_res, 0, RES_HEAD, st));
-    AHIP(a, hipMemsetAsync(a->d_move, 0, 2 * sizeof(unsigned long long), st));
     const bool par = !a->astream.empty();
     const int single = a->area.size() == 1 ? 1 : 0;
     // the areas' loads and their working copies (the rows a child hangs off are
@@ -554,14 +552,14 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
     // once), and the first iteration's source powers: each child's subtree load
     bool hooks = a->hooks_env;
     for (Area &A : a->area) hooks = hooks && A.kids.size() <= (size_t)AREA_MAX_KIDS && wave_hooks_supported(A.feeder, B);
-    AHIP(a, areas_gather_rows(a->d_pq, a->d_gmap, a->n_gmap, B, a->d_base, st));
-    if (!hooks)
-        AHIP(a, hipMemcpyAsync(a->d_work, a->d_base, sizeof(double) * a->n_gmap * b, hipMemcpyDeviceToDevice, st));
     // (the inexact iterations' inner eps, RES_HEAD's last 8 bytes, set by that launch)
     const bool inexact = hooks && !single && a->inexact > 0 && a->eps_first > a->eps;
     double *eps_dev = inexact ? (double *)(a->d_res + 24) : nullptr;
-    AHIP(a, areas_subtree_sums(a->d_pq, a->nl, B, (int)a->area.size(), a->d_sub_off, a->d_sub_rows, a->d_sin, eps_dev,
-                               a->eps_first, st));
+    // (also the loop's state in the result head and the move slots)
+    AHIP(a, areas_setup(a->d_pq, a->nl, a->d_gmap, a->n_gmap, B, a->d_base, (int)a->area.size(), a->d_sub_off,
+                        a->d_sub_rows, a->d_sin, ctl, last, a->d_move, eps_dev, a->eps_first, st));
+    if (!hooks)
+        AHIP(a, hipMemcpyAsync(a->d_work, a->d_base, sizeof(double) * a->n_gmap * b, hipMemcpyDeviceToDevice, st));
     // the stop test's arguments for iteration `it`
     auto fill_check = [&](AreaLink &L, int it) {
         L.move_acc = a->d_move + (it & 1);
@@ -749,7 +747,10 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
             if (rc) break;
         }
         if (rc) break;
-        AHIP(a, hipMemcpyAsync(h_ctl[chunk & 1], ctl, 8, hipMemcpyDeviceToHost, st));
+        // (the first chunk's flag, read at once, comes back with the results when
+        // those are enqueued after every chunk: no copy of its own)
+        const bool flag_in_res = chunk == 0 && first_chunk && !want_v;
+        if (!flag_in_res) AHIP(a, hipMemcpyAsync(h_ctl[chunk & 1], ctl, 8, hipMemcpyDeviceToHost, st));
         if (!want_v) {
             rc = enqueue_results(false);
             if (rc) break;
@@ -757,7 +758,7 @@ extern "C" int fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, doubl
         AHIP(a, hipEventRecord(ev[chunk & 1], st));
         if (chunk == 0 && first_chunk) {
             AHIP(a, hipEventSynchronize(ev[0]));
-            stop = h_ctl[0][0] != 0;
+            stop = (flag_in_res ? ((const int32_t *)a->h_res)[0] : h_ctl[0][0]) != 0;
         } else if (chunk > 0) {
             AHIP(a, hipEventSynchronize(ev[(chunk - 1) & 1]));
             stop = stop || h_ctl[(chunk - 1) & 1][0] != 0;

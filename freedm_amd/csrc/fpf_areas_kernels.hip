@@ -12,14 +12,37 @@
 namespace fpf {
 namespace {
 
-// dst[y][s] = src[map[y]][s] (map[y] < 0: a separator row, 0) -- every area's
-// [field][row] lines of the feeder's batch in one launch
-__global__ void gather_rows_kernel(const double *__restrict__ src, const int32_t *__restrict__ map, int B,
-                                   double *__restrict__ dst) {
+// The set-up of a solve, one launch: rows y < rows gather every area's
+// [field][row] lines of the feeder's batch, dst[y][s] = src[map[y]][s] (map[y] <
+// 0: a separator row, 0); the rows after them are the first outer iteration's
+// source powers of every non-root area: the loads of its whole subtree (rows
+// sub_rows[sub_off[a] .. sub_off[a+1]) of the batch) -- short of the subtree's
+// losses only, so that the first solve of the parent already sees nearly all of
+// its children's demand -- and the loop's state: ctl (done, outer), the last
+// move, the first iteration's inner eps, the two move slots
+__global__ void setup_kernel(const double *__restrict__ src, int nl, const int32_t *__restrict__ map, int rows, int B,
+                             double *__restrict__ dst, const int32_t *__restrict__ sub_off,
+                             const int32_t *__restrict__ sub_rows, double *__restrict__ s_in,
+                             int32_t *__restrict__ ctl, double *__restrict__ last, unsigned long long *__restrict__ move,
+                             double *__restrict__ eps_dev, double eps_first) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y, m = map[y];
+    const int y = blockIdx.y;
+    if (s == 0 && y == 0) {
+        for (int i = 0; i < 4; ++i) ctl[i] = 0;
+        *last = 0.0;
+        move[0] = move[1] = 0ull;
+        if (eps_dev) *eps_dev = eps_first;
+    }
     if (s >= B) return;
-    dst[(size_t)y * B + s] = m < 0 ? 0.0 : src[(size_t)m * B + s];
+    if (y < rows) {
+        const int m = map[y];
+        dst[(size_t)y * B + s] = m < 0 ? 0.0 : src[(size_t)m * B + s];
+        return;
+    }
+    const int a = (y - rows) / 6, f = (y - rows) % 6;
+    double x = 0.0;
+    for (int i = sub_off[a]; i < sub_off[a + 1]; ++i) x += src[((size_t)f * nl + sub_rows[i]) * B + s];
+    s_in[((size_t)a * 6 + f) * B + s] = x;
 }
 
 // The kernels of one outer iteration do nothing once the loop has converged
@@ -63,22 +86,6 @@ __global__ void link_kernel(AreaLink L, int B, int32_t *__restrict__ ctl) {
     if (L.check && blockIdx.x == 0 && threadIdx.x == 0) areas_stop_test(L, ctl);
 }
 
-// the first outer iteration's source powers of every non-root area: the loads of
-// its whole subtree (rows sub_rows[sub_off[a] .. sub_off[a+1]) of the feeder's
-// batch) -- short of the subtree's losses only, so that the first solve of the
-// parent already sees nearly all of its children's demand
-__global__ void subtree_sum_kernel(const double *__restrict__ pq, int nl, int B, const int32_t *__restrict__ sub_off,
-                                   const int32_t *__restrict__ sub_rows, double *__restrict__ s_in,
-                                   double *__restrict__ eps_dev, double eps_first) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    const int a = blockIdx.y / 6, f = blockIdx.y % 6;
-    if (eps_dev && s == 0 && blockIdx.y == 0) *eps_dev = eps_first;   // the first iteration's inner eps
-    if (s >= B) return;
-    double x = 0.0;
-    for (int i = sub_off[a]; i < sub_off[a + 1]; ++i) x += pq[((size_t)f * nl + sub_rows[i]) * B + s];
-    s_in[((size_t)a * 6 + f) * B + s] = x;
-}
-
 // dst[p][mono[k]][s] = src[p][k][s] for k = k0 .. nn-1
 __global__ void scatter_nodes_kernel(const double *__restrict__ src, int nn, int k0, const int32_t *__restrict__ mono,
                                      int nn_dst, int B, double *__restrict__ dst) {
@@ -112,18 +119,15 @@ __global__ void fold_results_kernel(int B, AreaFold F, double *__restrict__ o_lo
 inline dim3 grid(int B, int y) { return dim3((unsigned)((B + 255) / 256), (unsigned)y); }
 }  // namespace
 
-hipError_t areas_gather_rows(const double *src, const int32_t *map, int rows, int B, double *dst, hipStream_t st) {
-    hipLaunchKernelGGL(gather_rows_kernel, grid(B, rows), dim3(256), 0, st, src, map, B, dst);
+hipError_t areas_setup(const double *src, int nl, const int32_t *map, int rows, int B, double *dst, int n_areas,
+                       const int32_t *sub_off, const int32_t *sub_rows, double *s_in, int32_t *ctl, double *last,
+                       unsigned long long *move, double *eps_dev, double eps_first, hipStream_t st) {
+    hipLaunchKernelGGL(setup_kernel, grid(B, rows + 6 * n_areas), dim3(256), 0, st, src, nl, map, rows, B, dst, sub_off,
+                       sub_rows, s_in, ctl, last, move, eps_dev, eps_first);
     return hipGetLastError();
 }
 hipError_t areas_link(const AreaLink &L, int B, int32_t *ctl, hipStream_t st) {
     hipLaunchKernelGGL(link_kernel, grid(B, 1), dim3(256), 0, st, L, B, ctl);
-    return hipGetLastError();
-}
-hipError_t areas_subtree_sums(const double *pq, int nl, int B, int n_areas, const int32_t *sub_off,
-                              const int32_t *sub_rows, double *s_in, double *eps_dev, double eps_first, hipStream_t st) {
-    hipLaunchKernelGGL(subtree_sum_kernel, grid(B, 6 * n_areas), dim3(256), 0, st, pq, nl, B, sub_off, sub_rows, s_in,
-                       eps_dev, eps_first);
     return hipGetLastError();
 }
 hipError_t areas_scatter_nodes(const double *src, int nn, int k0, const int32_t *mono, int nn_dst, int B, double *dst,
