@@ -41,4 +41,14 @@ bool gradb_lu_fits(int nf);
 hipError_t launch_gradb_lu(int nf, int nb, double *A, double *rhs, int8_t *sing, hipStream_t st);
 hipError_t launch_gradb_g(const GradPhaseDev &P, int c0, int nb, const double *sol, int ld, double *g, hipStream_t st);
 
+// The step-size search's candidate batch of fpf_vvc_round_batch on the device:
+// candidate column k M + m of cand [6 nl][K M] is scenario todo[k]'s loads of pq
+// [6 nl][B] with, at every (phase x, load i, row r) of the triples [T][3], the Q
+// set-point moved: pq - g[(s 3 + x) ld + i] * scale * c_m, c_0 = cstart[k],
+// c_{m+1} = alpha c_m (VoltVarCtrl.cpp:1323, 1420-1422, 1546) -- the host loop's
+// operations in its order, so the candidates are bit-identical to it
+hipError_t launch_vvc_candidates(const double *pq, int nl, int B, const int32_t *todo, int K, int M,
+                                 const int32_t *triples, int T, const double *g, int ld, double scale, double alpha,
+                                 const double *cstart, double *cand, hipStream_t st);
+
 }  // namespace fpf

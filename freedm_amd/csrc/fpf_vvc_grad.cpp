@@ -823,43 +823,65 @@ extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, in
     std::vector<int> todo;
     for (int s = 0; s < B; ++s)
         if (rstatus[s] == 0) todo.push_back(s);
+#define RCHK(expr)                                                                                      \
+    do {                                                                                                \
+        const hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                           \
+            return fpf::feeder_fail(feeder, FPF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+    // the candidate batches are formed on the device (launch_vvc_candidates): the
+    // scenarios' loads, g and the (phase, load, row) triples of the Q updates go
+    // up once; per pass only the scenario list and the first step sizes
+    const double scale = bkva / 3;
+    std::vector<int32_t> tri;
+    for (int x = 0; x < 3; ++x)
+        for (int i = 0; i < n_loads[x]; ++i)
+            for (int r : rows[x][i]) tri.insert(tri.end(), {x, i, r});
+    const int T = (int)(tri.size() / 3);
+    const size_t Bmax = (size_t)todo.size() * M;
+    DevBuf d_pq, d_g, d_tri, d_todo, d_cst, d_cand, d_loss, d_stat;
+    if (!todo.empty()) {
+        RCHK(hipMalloc(&d_pq.p, sizeof(double) * 6 * nlz * b));
+        RCHK(hipMalloc(&d_g.p, sizeof(double) * b * 3 * ld));
+        RCHK(hipMalloc(&d_tri.p, sizeof(int32_t) * std::max<size_t>(tri.size(), 1)));
+        RCHK(hipMalloc(&d_todo.p, sizeof(int32_t) * b));
+        RCHK(hipMalloc(&d_cst.p, sizeof(double) * b));
+        RCHK(hipMalloc(&d_cand.p, sizeof(double) * 6 * nlz * Bmax));
+        RCHK(hipMalloc(&d_loss.p, sizeof(double) * Bmax));
+        RCHK(hipMalloc(&d_stat.p, Bmax));
+        RCHK(hipMemcpy(d_pq.p, pq, sizeof(double) * 6 * nlz * b, hipMemcpyHostToDevice));
+        RCHK(hipMemcpy(d_g.p, g, sizeof(double) * b * 3 * ld, hipMemcpyHostToDevice));
+        if (!tri.empty()) RCHK(hipMemcpy(d_tri.p, tri.data(), sizeof(int32_t) * tri.size(), hipMemcpyHostToDevice));
+    }
     for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
         const int K = (int)todo.size();
         const size_t Bc = (size_t)K * M;
         // candidate (k, m) = column k M + m: scenario todo[k]'s loads with its Q
         // set-points moved by -g (bkva/3) c_m, c_0 = c0 (:1323) or the reversed
         // start -beta0/(bkva/3)/gabs_min (:1546), c_{m+1} = alpha c_m (:1420-1422)
-        std::vector<double> cand(6 * nlz * Bc);
-        for (size_t fr = 0; fr < 6 * nlz; ++fr)
-            for (int k = 0; k < K; ++k) {
-                const double v = pq[fr * b + todo[k]];
-                double *d = &cand[fr * Bc + (size_t)k * M];
-                for (int m = 0; m < M; ++m) d[m] = v;
-            }
+        std::vector<double> cstart(K);
         for (int k = 0; k < K; ++k) {
-            const int s = todo[k];
-            const double *st8 = &stats[(size_t)s * 8];
-            double cvq = pass == 0 ? st8[3] : -beta0 / (bkva / 3) / st8[2];
-            for (int m = 0; m < M; ++m) {
-                for (int x = 0; x < 3; ++x) {
-                    const size_t fq = (size_t)(1 + 2 * x);   // Q of phase x = Dl column 7 + 2x
-                    for (int i = 0; i < n_loads[x]; ++i) {
-                        const double gupdate = g[((size_t)s * 3 + x) * ld + i] * (bkva / 3) * cvq;
-                        for (int r : rows[x][i])
-                            cand[(fq * nlz + r) * Bc + (size_t)k * M + m] = pq[(fq * nlz + r) * b + s] - gupdate;
-                    }
-                }
-                cvq = alpha * cvq;
-            }
+            const double *st8 = &stats[(size_t)todo[k] * 8];
+            cstart[k] = pass == 0 ? st8[3] : -beta0 / (bkva / 3) / st8[2];
         }
-        std::vector<double> loss(Bc);
-        std::vector<signed char> status(Bc);
+        RCHK(hipMemcpy(d_todo.p, todo.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice));
+        RCHK(hipMemcpy(d_cst.p, cstart.data(), sizeof(double) * K, hipMemcpyHostToDevice));
+        RCHK(fpf::launch_vvc_candidates((const double *)d_pq.p, nl, B, (const int32_t *)d_todo.p, K, M,
+                                        (const int32_t *)d_tri.p, T, (const double *)d_g.p, ld, scale, alpha,
+                                        (const double *)d_cst.p, (double *)d_cand.p, nullptr));
         fpf_outputs out;
         std::memset(&out, 0, sizeof(out));
-        out.loss = loss.data();
-        out.status = status.data();
-        rc = fpf::solve_batch_host(feeder, (int)Bc, cand.data(), &out, nullptr, FPF_LAYOUT_SCEN_FASTEST);
+        out.loss = (double *)d_loss.p;
+        out.status = (signed char *)d_stat.p;
+        rc = fpf::solve_batch_device_ex(feeder, (int)Bc, (const double *)d_cand.p, &out, nullptr, nullptr, nullptr,
+                                        nullptr, FPF_LAYOUT_SCEN_FASTEST);
         if (rc < 0) return rc;
+        std::vector<double> loss(Bc);
+        std::vector<signed char> status(Bc);
+        RCHK(hipMemcpy(loss.data(), d_loss.p, sizeof(double) * Bc, hipMemcpyDeviceToHost));
+        RCHK(hipMemcpy(status.data(), d_stat.p, Bc, hipMemcpyDeviceToHost));
+        rc = fpf::take_exchange_fault(feeder);   // (the copies above synchronised the device)
+        if (rc) return rc;
         std::vector<int> next;
         for (int k = 0; k < K; ++k) {
             const int s = todo[k];
@@ -880,12 +902,16 @@ extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, in
             }
             if (stop >= 0) {
                 q.after = lk[stop];
-                // Dl = Dl_osize (:1486/:1707): the kept candidate's Q set-points
+                // Dl = Dl_osize (:1486/:1707): the kept candidate's Q set-points, formed
+                // as the device formed them
+                double cvq = cstart[k];
+                for (int j = 0; j < stop; ++j) cvq = alpha * cvq;
                 for (int x = 0; x < 3; ++x) {
                     const size_t fq = (size_t)(1 + 2 * x);
-                    for (int i = 0; i < n_loads[x]; ++i)
-                        for (int r : rows[x][i])
-                            pq_out[(fq * nlz + r) * b + s] = cand[(fq * nlz + r) * Bc + (size_t)k * M + stop];
+                    for (int i = 0; i < n_loads[x]; ++i) {
+                        const double gupdate = g[((size_t)s * 3 + x) * ld + i] * scale * cvq;
+                        for (int r : rows[x][i]) pq_out[(fq * nlz + r) * b + s] = pq[(fq * nlz + r) * b + s] - gupdate;
+                    }
                 }
                 if (lk[stop] < stats[(size_t)s * 8 + 4]) q.sent = 1;   // :1495
             } else {
@@ -894,6 +920,7 @@ extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, in
         }
         todo.swap(next);
     }
+#undef RCHK
     int bad = 0;
     for (int s = 0; s < B; ++s) {
         const double *st8 = &stats[(size_t)s * 8];

@@ -285,4 +285,46 @@ hipError_t launch_gradb_g(const GradPhaseDev &P, int c0, int nb, const double *s
     return hipGetLastError();
 }
 
+namespace {
+// the broadcast: cand[fr][k M + m] = pq[fr][todo[k]]
+__global__ void vvc_cand_bcast_kernel(const double *__restrict__ pq, int B, const int32_t *__restrict__ todo, int K,
+                                      int M, double *__restrict__ cand) {
+    const size_t Bc = (size_t)K * M;
+    const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int fr = blockIdx.y;
+    if (col >= Bc) return;
+    cand[fr * Bc + col] = pq[(size_t)fr * B + todo[col / M]];
+}
+// the Q set-points: one thread per (candidate, triple)
+__global__ void vvc_cand_q_kernel(const double *__restrict__ pq, int nl, int B, const int32_t *__restrict__ todo, int K,
+                                  int M, const int32_t *__restrict__ triples, int T, const double *__restrict__ g,
+                                  int ld, double scale, double alpha, const double *__restrict__ cstart,
+                                  double *__restrict__ cand) {
+    const size_t Bc = (size_t)K * M;
+    const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y;
+    if (col >= Bc) return;
+    const int k = (int)(col / M), m = (int)(col % M), s = todo[k];
+    const int x = triples[3 * t], i = triples[3 * t + 1], r = triples[3 * t + 2];
+    double cvq = cstart[k];
+    for (int j = 0; j < m; ++j) cvq = alpha * cvq;
+    const double gupdate = g[((size_t)s * 3 + x) * ld + i] * scale * cvq;
+    const size_t row = (size_t)(1 + 2 * x) * nl + r;   // Q of phase x = Dl column 7 + 2x
+    cand[row * Bc + col] = pq[row * B + s] - gupdate;
+}
+}  // namespace
+
+hipError_t launch_vvc_candidates(const double *pq, int nl, int B, const int32_t *todo, int K, int M,
+                                 const int32_t *triples, int T, const double *g, int ld, double scale, double alpha,
+                                 const double *cstart, double *cand, hipStream_t st) {
+    const size_t Bc = (size_t)K * M;
+    if (Bc == 0) return hipSuccess;
+    const unsigned gx = (unsigned)((Bc + 255) / 256);
+    hipLaunchKernelGGL(vvc_cand_bcast_kernel, dim3(gx, 6 * nl), dim3(256), 0, st, pq, B, todo, K, M, cand);
+    if (T > 0)
+        hipLaunchKernelGGL(vvc_cand_q_kernel, dim3(gx, T), dim3(256), 0, st, pq, nl, B, todo, K, M, triples, T, g, ld,
+                           scale, alpha, cstart, cand);
+    return hipGetLastError();
+}
+
 }  // namespace fpf
