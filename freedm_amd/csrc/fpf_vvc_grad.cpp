@@ -20,9 +20,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -619,6 +622,33 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
     DevBuf d_g;
     GCHK(hipMalloc(&d_g.p, sizeof(double) * b * 3 * ld));
     GCHK(hipMemset(d_g.p, 0, sizeof(double) * b * 3 * ld));
+    // the three phases' set-up / LU / g on three streams: independent matrices (one
+    // workgroup each), so their launches overlap; their buffers live until the end.
+    // The streams are the device's, created once (creating three per call cost
+    // more than the overlap saves on small feeders)
+    struct {
+        hipStream_t s[3];
+    } ps;
+    {
+        static std::mutex mu;
+        static std::map<int, std::array<hipStream_t, 3>> cache;
+        int dev = 0;
+        GCHK(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(dev);
+        if (it == cache.end()) {
+            std::array<hipStream_t, 3> a{};
+            for (int x = 0; x < 3; ++x) GCHK(hipStreamCreateWithFlags(&a[x], hipStreamNonBlocking));
+            it = cache.emplace(dev, a).first;
+        }
+        for (int x = 0; x < 3; ++x) ps.s[x] = it->second[x];
+    }
+    struct PhaseWork {
+        PhaseBufs pb;
+        DevBuf A, rhs, sing;
+        bool used = false;
+    };
+    PhaseWork work[3];
     for (int x = 0; x < 3; ++x) {
         const PhaseNet &P = plan.ph[x];
         const int L = P.lnum, n = L + 1, m1 = n - 1, nf = 2 * m1;
@@ -664,7 +694,7 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
                 if (P.node[ia + 1] == plan.loads[x][j]) ld_ia.push_back(ia);
             ld_ptr.push_back((int32_t)ld_ia.size());
         }
-        PhaseBufs pb;
+        PhaseBufs &pb = work[x].pb;
         GCHK(pb.vrow.up(P.vrow));
         GCHK(pb.vmask.up(vmask));
         GCHK(pb.bs.up(P.s));
@@ -707,22 +737,28 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
         // the dense J^T of a chunk of scenarios at a time (nf^2 doubles each, within ~2 GB)
         const size_t per = (size_t)nf * nf * sizeof(double);
         const int chunk = (int)std::max<size_t>(1, std::min<size_t>(b, ((size_t)2 << 30) / per));
-        DevBuf d_A, d_rhs, d_sing;
-        GCHK(hipMalloc(&d_A.p, per * chunk));
-        GCHK(hipMalloc(&d_rhs.p, sizeof(double) * nf * chunk));
-        GCHK(hipMalloc(&d_sing.p, chunk));
-        std::vector<int8_t> sing(chunk);
+        PhaseWork &w = work[x];
+        GCHK(hipMalloc(&w.A.p, per * chunk));
+        GCHK(hipMalloc(&w.rhs.p, sizeof(double) * nf * chunk));
+        GCHK(hipMalloc(&w.sing.p, b));
+        w.used = true;
+        const hipStream_t sx = ps.s[x];
         for (int c0 = 0; c0 < B; c0 += chunk) {
             const int nb = std::min(chunk, B - c0);
-            double *A = (double *)d_A.p, *rhs = (double *)d_rhs.p;
-            GCHK(fpf::launch_gradb_setup(D, B, c0, nb, (const double *)d_vp.p, A, rhs, (int8_t *)d_gst.p, st));
+            double *A = (double *)w.A.p, *rhs = (double *)w.rhs.p;
+            GCHK(fpf::launch_gradb_setup(D, B, c0, nb, (const double *)d_vp.p, A, rhs, (int8_t *)d_gst.p, sx));
             // lambda = -inv(J^T) Fx: one LU with partial pivoting and one solve per matrix
-            GCHK(fpf::launch_gradb_lu(nf, nb, A, rhs, (int8_t *)d_sing.p, st));
-            GCHK(fpf::launch_gradb_g(D, c0, nb, rhs, ld, (double *)d_g.p, st));
-            GCHK(hipMemcpy(sing.data(), d_sing.p, nb, hipMemcpyDeviceToHost));
-            for (int k = 0; k < nb; ++k)
-                if (sing[k] != 0 && h_gst[c0 + k] == fpf::FPF_GRAD_OK) h_gst[c0 + k] = fpf::FPF_GRAD_SINGULAR;
+            GCHK(fpf::launch_gradb_lu(nf, nb, A, rhs, (int8_t *)w.sing.p + c0, sx));
+            GCHK(fpf::launch_gradb_g(D, c0, nb, rhs, ld, (double *)d_g.p, sx));
         }
+    }
+    std::vector<int8_t> sing(b);
+    for (int x = 0; x < 3; ++x) {
+        GCHK(hipStreamSynchronize(ps.s[x]));
+        if (!work[x].used) continue;
+        GCHK(hipMemcpy(sing.data(), work[x].sing.p, b, hipMemcpyDeviceToHost));
+        for (int s = 0; s < B; ++s)
+            if (sing[s] != 0 && h_gst[s] == fpf::FPF_GRAD_OK) h_gst[s] = fpf::FPF_GRAD_SINGULAR;
     }
     // per-scenario results: the device's pattern flags merged with the host's
     std::vector<int8_t> d_flags(b);
