@@ -136,10 +136,6 @@ struct WaveDev {
     int32_t wpb;             // wavefronts per workgroup (16, 8 or 4; fpf_api.cpp: analyse_wave)
     int32_t off_in_x;        // 1: block offsets stored over X's first nblk entries (nblk <= L, depth <= 4)
     int32_t stag_lo, stag_hi, stag_n;   // workgroups [lo, hi) start stag_n x 8 k cycles late (diagnostic)
-    // (wave-block kernel, scenario-major batches) the workgroup that runs pf_ahead
-    // launches later on this XCD: its loads are touched during this staging so
-    // that they come from L2 / the Infinity Cache; 0: none
-    int32_t pf_ahead;
     int32_t temp_sym;        // 1: every branch's TEMP has one common off-diagonal zm (transposed
                              //    line / transformer): slot_temp holds (z_aa - zm) x 3, zm per slot
     double V0[6], s3, eps, lb_v, ub_v;

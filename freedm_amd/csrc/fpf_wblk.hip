@@ -106,7 +106,6 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             // element e = 2 i: (field, row) walked 2 NT elements per load
             RowWalk w;
             w.init(2 * tid, 2 * NT, nl);
-            double pf0 = 0.0, pf1 = 0.0;
             for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
                 d2v r[U2];
                 int q0[U2], q1[U2];
@@ -119,14 +118,6 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     q1[u] = 2 * ((f1 >> 1) * PS + r1) + (f1 & 1);
                     w.next();
                 }
-                // the block pf_ahead launches on: one double of each 128-byte line of
-                // its scenario, in flight with this tile's loads (WaveDev::pf_ahead)
-                if (i0 == 0 && f.pf_ahead > 0 && (int)blockIdx.x + f.pf_ahead < (int)gridDim.x) {
-                    const double *np = pq + (size_t)xcd_tile((int)blockIdx.x + f.pf_ahead, gridDim.x) * total;
-                    const int e0 = 16 * tid, e1 = 16 * (tid + NT);
-                    pf0 = e0 < total ? np[e0] : 0.0;
-                    pf1 = e1 < total ? np[e1] : 0.0;
-                }
 #pragma unroll
                 for (int u = 0; u < U2; ++u) {
                     const int i = i0 + u * NT + tid;
@@ -136,7 +127,6 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     }
                 }
             }
-            __asm__ volatile("" ::"v"(pf0), "v"(pf1));   // (the touches are kept)
         } else {
             RowWalk w;   // (field, row) of element i, walked NT per load
             w.init(tid, NT, nl);
@@ -848,17 +838,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
             attr_done.insert(key);
         }
     }
-    WaveDev wl = w;
-    wl.pf_ahead = 0;
-    static const int pf_env = getenv("FPF_WBLK_PREFETCH") ? atoi(getenv("FPF_WBLK_PREFETCH")) : 1;
-    if (pf_env && o.smaj) {
-        // the workgroups resident at once: CUs x workgroups per CU (LDS-bound)
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 0;
-        const int per_cu = std::max(1, (int)((160 * 1024) / std::max<size_t>(1, wblk_lds_bytes(w))));
-        wl.pf_ahead = ncu * per_cu;
-    }
-    hipLaunchKernelGGL(k, dim3((unsigned)n_scen), dim3(64 * w.wps), wblk_lds_bytes(w), st, wl, n_scen, pq, o);
+    hipLaunchKernelGGL(k, dim3((unsigned)n_scen), dim3(64 * w.wps), wblk_lds_bytes(w), st, w, n_scen, pq, o);
     return hipGetLastError();
 }
 
