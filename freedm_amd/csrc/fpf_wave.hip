@@ -1275,6 +1275,10 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     }
     WaveDev wl = w;
     wl.stag_lo = wl.stag_hi = wl.stag_n = 0;
+    if (getenv("FPF_PRINT_WAVEDEV"))   // (diagnostic: the uniform plan values of a launch)
+        fprintf(stderr, "wavedev spw %d C %d wpb %d nl %d nn %d nblk %d bdepth %d ncomp %d temp_sym %d off_in_x %d "
+                "stage_u %d out_u %d has_mask %d has_rel %d mxitr %d\n", w.spw, w.C, w.wpb, w.nl, w.nn, w.nblk, w.bdepth,
+                w.ncomp, (int)w.temp_sym, (int)w.off_in_x, w.stage_u, w.out_u, (int)w.has_mask, (int)w.has_rel, w.mxitr);
     if (const char *e = getenv("FPF_WAVE_WG_STAGGER")) {   // experiments: "lo,hi,n"
         if (sscanf(e, "%d,%d,%d", &wl.stag_lo, &wl.stag_hi, &wl.stag_n) != 3) wl.stag_lo = wl.stag_hi = wl.stag_n = 0;
     }
