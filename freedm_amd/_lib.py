@@ -26,7 +26,8 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_multi_create", "fpf_multi_destroy", "fpf_multi_last_error", "fpf_multi_solve", "fpf_multi_get_feeder",
            "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_gradient_at", "fpf_vvc_round",
-           "fpf_vvc_gradient_batch", "fpf_feeder_check", "fpf_vvc_round_batch"]
+           "fpf_vvc_gradient_batch", "fpf_feeder_check", "fpf_vvc_round_batch", "fpf_feeder_wave_rtc_source",
+           "fpf_wave_rtc_builds"]
 
 
 class FpfOpts(C.Structure):
@@ -116,6 +117,10 @@ def load(path: str | None = None):
     L.fpf_feeder_rtc_source.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
                                         C.c_char_p, C.c_size_t]
     L.fpf_feeder_rtc_source.restype = C.c_long
+    if hasattr(L, "fpf_feeder_wave_rtc_source"):   # (older diagnostic builds lack it)
+        L.fpf_feeder_wave_rtc_source.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
+                                                 C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+        L.fpf_feeder_wave_rtc_source.restype = C.c_long
     L.fpf_vvc_line_search.argtypes = [vp, _dp, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int), C.c_int, C.c_double,
                                       C.c_double, C.c_int, C.c_double, C.POINTER(FpfLineSearch)]
     L.fpf_vvc_line_search.restype = C.c_int

@@ -1485,6 +1485,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.off_in_x = wh.off_in_x;
         w.temp_sym = wh.temp_sym;
         w.dbg = getenv("FPF_WAVE_DBG") ? atoi(getenv("FPF_WAVE_DBG")) : 0;
+        w.spec = o.specialize ? 1 : 0;
         w.mxitr = o.mxitr;
         for (int p = 0; p < 3; ++p) w.K[p] = d.K[p];
         for (int i = 0; i < 6; ++i) w.V0[i] = d.V0[i];
@@ -2196,4 +2197,50 @@ extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const d
     const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, lds, wh.ncomp, wh.nblk, wh.bdepth};
     std::memcpy(out, v, sizeof(v));
     return FPF_OK;
+}
+
+extern "C" long fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols, const double *z, int z_rows,
+                                           int z_cols, const fpf_opts *opts, int big_batch, int full, char *buf,
+                                           size_t buf_size) {
+    if (!dl || nl < 1 || ncols < 12 || z_rows < 0 || (z_rows > 0 && !z)) return FPF_ERR_ARG;
+    fpf_opts o;
+    if (opts) o = *opts;
+    else fpf_opts_default(&o);
+    HostFeeder h;
+    h.nl = nl;
+    h.ncols = ncols;
+    h.dl.assign(dl, dl + (size_t)nl * ncols);
+    std::string why = build_ops(h, z, z_rows, z_cols, o);
+    if (why.empty()) why = build_lnum(h, z, z_rows, o);
+    if (!why.empty()) return FPF_ERR_TOPOLOGY;
+    analyse_tiled(h);
+    WaveHost wh;
+    analyse_wave(h, wh);
+    if (!wh.ok || wh.wps || wh.coop) return FPF_ERR_UNSUPPORTED;
+    // the plan values fpf_feeder_create puts in the launch's WaveDev
+    WaveDev w{};
+    w.nn = h.nn;
+    w.nl = nl;
+    w.spw = wh.spw;
+    w.C = wh.C;
+    w.nblk = wh.nblk;
+    w.bdepth = wh.bdepth;
+    w.ncomp = wh.ncomp;
+    w.has_rel = wh.has_rel;
+    w.has_mask = wh.has_mask;
+    w.wpb = big_batch ? wh.wpb_big_batch : wh.wpb;
+    w.off_in_x = wh.off_in_x;
+    w.temp_sym = wh.temp_sym;
+    w.mxitr = o.mxitr;
+    std::vector<int32_t> a, b;
+    w.stage_u = wave_stage_tables(w, a, b);
+    w.out_u = wave_out_tables(w, a, b);
+    std::string name;
+    const std::string src = wave_rtc_source(w, full != 0, &name);
+    if (buf && buf_size > 0) {
+        const size_t n = std::min(buf_size - 1, src.size());
+        std::memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return (long)src.size() + 1;
 }

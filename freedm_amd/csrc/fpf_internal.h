@@ -10,6 +10,10 @@ using __hip_internal::int32_t;
 using __hip_internal::uint16_t;
 using __hip_internal::uint32_t;
 #define INFINITY __builtin_huge_val()
+// the per-scenario status values of include/freedm_pf.h
+#define FPF_CONVERGED 0
+#define FPF_NONCONVERGED 1
+#define FPF_EXCHANGE_FAILED 3
 #else
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -138,6 +142,8 @@ struct WaveDev {
     int32_t stag_lo, stag_hi, stag_n;   // workgroups [lo, hi) start stag_n x 8 k cycles late (diagnostic)
     int32_t temp_sym;        // 1: every branch's TEMP has one common off-diagonal zm (transposed
                              //    line / transformer): slot_temp holds (z_aa - zm) x 3, zm per slot
+    int32_t spec;            // 1: large launches run the per-feeder hipRTC build (fpf_opts.specialize;
+                             //    fpf_rtc.cpp: wave_rtc_function), 0: the static kernel only
     double V0[6], s3, eps, lb_v, ub_v;
     const int32_t *slot_row;    // [C][L] Dl row of the slot's node (-1: empty slot)
     const int32_t *slot_node;   // [C][L] node id
@@ -258,6 +264,72 @@ struct OutDev {
 // the count is reset to 0 for the next launch.
 constexpr int FIXUP_BLOCKS = 1;   // one workgroup: 4 x 21 scenarios per pass
 
+// (device-visible: also compiled by hipRTC, fpf_rtc.cpp)
+// the multi-area solve's fused exchange kernels (fpf_areas_kernels.hip): up to
+// AREA_MAX_KIDS children of one area per launch -- the local row of a child's
+// bus and its source power (add_rows), or the child's boundary bus and its
+// source-voltage array (gather_vsrc_all)
+constexpr int AREA_MAX_KIDS = 8;
+struct AreaKids {
+    int n;
+    int lrow[AREA_MAX_KIDS];
+    double *ptr[AREA_MAX_KIDS];
+};
+// the links of one area folded into its wave-kernel solve (OutDev::hook): after
+// the loads are staged, the rows its children hang off get the children's source
+// powers added (pre: base + s_in, scaled like the loads); after the sweeps, each
+// child's boundary bus voltage (local node post_lb >= 1) becomes its source
+// voltage and the largest move joins *OutDev::move
+struct AreaHook {
+    int pre_n, post_n;
+    int pre_lrow[AREA_MAX_KIDS], post_lb[AREA_MAX_KIDS];
+    const double *pre_sin[AREA_MAX_KIDS];
+    double *post_vsrc[AREA_MAX_KIDS];
+};
+// the per-scenario results of up to AREA_MAX_FOLD areas, folded in one launch
+constexpr int AREA_MAX_FOLD = 8;
+struct AreaFold {
+    int n, first;
+    const double *loss[AREA_MAX_FOLD], *vmin[AREA_MAX_FOLD], *vmax[AREA_MAX_FOLD];
+    const int8_t *status[AREA_MAX_FOLD];
+};
+// one launch between two area solves of an outer iteration (fpf_areas.cpp): the
+// solved area's children's source voltages (post; V [3][nn][B]), the next area's
+// child rows (pre; work / base [6][nl][B]), the iteration's stop test (check)
+struct AreaLink {
+    const double *v_re, *v_im;
+    int nn, nl;
+    AreaKids post, pre;
+    double *work;
+    const double *base;
+    unsigned long long *move_acc, *move_chk, *move_clr;   // the iteration's move (two slots, by parity)
+    double *last;
+    double tol;
+    int check, single;
+    // inexact outer iterations (check): the next iteration's inner eps
+    // *eps_dev = clamp(inexact * move, eps, eps_first); stop only after an
+    // iteration solved to eps itself.  eps_dev NULL: every solve to eps
+    double *eps_dev;
+    double eps, eps_first, inexact;
+};
+// the end of an outer iteration (link_kernel, or the last workgroup of the last
+// area's solve: OutDev::check), once every boundary move of the iteration is in:
+// the outer count, the move, the next iteration's inner eps, the stop flag ctl[0]
+__device__ inline void areas_stop_test(const AreaLink &L, int32_t *ctl) {
+    const double m = __longlong_as_double((long long)*L.move_chk);
+    const int outer = ctl[1] + 1;
+    ctl[1] = outer;
+    *L.last = m;
+    *L.move_clr = 0ull;
+    bool exact = true;   // this iteration's solves ran to eps
+    if (L.eps_dev) exact = *L.eps_dev <= L.eps;
+    const bool done = L.single || (outer > 1 && m <= L.tol && exact);
+    // (the first iteration's move compares with the previous solve's source
+    // voltages: it does not set the next eps)
+    if (L.eps_dev) *L.eps_dev = outer == 1 ? L.eps_first : fmax(L.eps, fmin(L.eps_first, L.inexact * m));
+    if (done) ctl[0] = 1;
+}
+
 #ifndef __HIPCC_RTC__
 }  // namespace fpf
 struct fpf_feeder;
@@ -306,72 +378,8 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
 size_t wblk_lds_bytes(const WaveDev &w);
 hipError_t launch_wcoop(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 size_t wcoop_lds_bytes(const WaveDev &w);
-// the multi-area solve's fused exchange kernels (fpf_areas_kernels.hip): up to
-// AREA_MAX_KIDS children of one area per launch -- the local row of a child's
-// bus and its source power (add_rows), or the child's boundary bus and its
-// source-voltage array (gather_vsrc_all)
-constexpr int AREA_MAX_KIDS = 8;
-struct AreaKids {
-    int n;
-    int lrow[AREA_MAX_KIDS];
-    double *ptr[AREA_MAX_KIDS];
-};
-// the links of one area folded into its wave-kernel solve (OutDev::hook): after
-// the loads are staged, the rows its children hang off get the children's source
-// powers added (pre: base + s_in, scaled like the loads); after the sweeps, each
-// child's boundary bus voltage (local node post_lb >= 1) becomes its source
-// voltage and the largest move joins *OutDev::move
-struct AreaHook {
-    int pre_n, post_n;
-    int pre_lrow[AREA_MAX_KIDS], post_lb[AREA_MAX_KIDS];
-    const double *pre_sin[AREA_MAX_KIDS];
-    double *post_vsrc[AREA_MAX_KIDS];
-};
-// the per-scenario results of up to AREA_MAX_FOLD areas, folded in one launch
-constexpr int AREA_MAX_FOLD = 8;
-struct AreaFold {
-    int n, first;
-    const double *loss[AREA_MAX_FOLD], *vmin[AREA_MAX_FOLD], *vmax[AREA_MAX_FOLD];
-    const int8_t *status[AREA_MAX_FOLD];
-};
 // whether an area solve of n scenarios runs the plain wave kernel (hooks apply)
 bool wave_hooks_supported(fpf_feeder *f, int n_scen);
-// one launch between two area solves of an outer iteration (fpf_areas.cpp): the
-// solved area's children's source voltages (post; V [3][nn][B]), the next area's
-// child rows (pre; work / base [6][nl][B]), the iteration's stop test (check)
-struct AreaLink {
-    const double *v_re, *v_im;
-    int nn, nl;
-    AreaKids post, pre;
-    double *work;
-    const double *base;
-    unsigned long long *move_acc, *move_chk, *move_clr;   // the iteration's move (two slots, by parity)
-    double *last;
-    double tol;
-    int check, single;
-    // inexact outer iterations (check): the next iteration's inner eps
-    // *eps_dev = clamp(inexact * move, eps, eps_first); stop only after an
-    // iteration solved to eps itself.  eps_dev NULL: every solve to eps
-    double *eps_dev;
-    double eps, eps_first, inexact;
-};
-// the end of an outer iteration (link_kernel, or the last workgroup of the last
-// area's solve: OutDev::check), once every boundary move of the iteration is in:
-// the outer count, the move, the next iteration's inner eps, the stop flag ctl[0]
-__device__ inline void areas_stop_test(const AreaLink &L, int32_t *ctl) {
-    const double m = __longlong_as_double((long long)*L.move_chk);
-    const int outer = ctl[1] + 1;
-    ctl[1] = outer;
-    *L.last = m;
-    *L.move_clr = 0ull;
-    bool exact = true;   // this iteration's solves ran to eps
-    if (L.eps_dev) exact = *L.eps_dev <= L.eps;
-    const bool done = L.single || (outer > 1 && m <= L.tol && exact);
-    // (the first iteration's move compares with the previous solve's source
-    // voltages: it does not set the next eps)
-    if (L.eps_dev) *L.eps_dev = outer == 1 ? L.eps_first : fmax(L.eps, fmin(L.eps_first, L.inexact * m));
-    if (done) ctl[0] = 1;
-}
 constexpr int COOP_NSLOT = 1024;   // exchange areas of the paired kernel (scenarios in flight <= 256)
 inline size_t wave_any_lds_bytes(const WaveDev &w) {
     return w.coop ? wcoop_lds_bytes(w) : (w.wps ? wblk_lds_bytes(w) : wave_lds_bytes(w));
@@ -433,6 +441,11 @@ int rtc_build(int device, const RtcSpec &spec, RtcKernel *out, std::string *err)
 void rtc_release(const RtcKernel &k);   // drop one reference; the last unloads the code object
 hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
                       hipStream_t st);
+// the wave kernel compiled for one plan (its uniform values as constants,
+// fpf_wave_body.h: FPF_WSPEC) and variant; built on first use, kept for the
+// process.  NULL if the build failed (the static kernel runs)
+hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full);
+std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name);
 #endif
 
 }  // namespace fpf

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <vector>
 
 #include "fpf_internal.h"
 
@@ -237,6 +238,60 @@ std::string rtc_source(const RtcSpec &sp) {
     return src;
 }
 
+namespace {
+// compile src for gfx950 and load it on the current device: the kernel fname,
+// or, given name_expr (a template instantiation), its lowered name
+int compile_load(const std::string &src, const char *file, const char *fname, const char *name_expr,
+                 std::vector<const char *> opts, RtcKernel *k, std::string *err) {
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), file, 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        *err = "hiprtcCreateProgram failed";
+        return -1;
+    }
+    if (name_expr && hiprtcAddNameExpression(prog, name_expr) != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        *err = "hiprtcAddNameExpression failed";
+        return -1;
+    }
+    opts.insert(opts.begin(), {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"});
+    hiprtcResult rr = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
+    if (rr != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        *err = std::string("hipRTC compile failed: ") + hiprtcGetErrorString(rr) + "\n" + log.substr(0, 4000);
+        hiprtcDestroyProgram(&prog);
+        return -1;
+    }
+    std::string lowered = fname;
+    if (name_expr) {
+        const char *low = nullptr;
+        if (hiprtcGetLoweredName(prog, name_expr, &low) != HIPRTC_SUCCESS || !low) {
+            hiprtcDestroyProgram(&prog);
+            *err = "hiprtcGetLoweredName failed";
+            return -1;
+        }
+        lowered = low;
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    std::string code(n, '\0');
+    hiprtcGetCode(prog, &code[0]);
+    hiprtcDestroyProgram(&prog);
+    if (hipModuleLoadData(&k->mod, code.data()) != hipSuccess) {
+        *err = "hipModuleLoadData failed";
+        return -1;
+    }
+    if (hipModuleGetFunction(&k->fn, k->mod, lowered.c_str()) != hipSuccess) {
+        (void)hipModuleUnload(k->mod);
+        *err = "hipModuleGetFunction failed";
+        return -1;
+    }
+    return 0;
+}
+}  // namespace
+
 int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
     const std::string src = rtc_source(sp);
     std::lock_guard<std::mutex> lk(g_mu);
@@ -247,48 +302,74 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
         *out = it->second.k;
         return 0;
     }
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "fpf_rtc_tiled.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-        *err = "hiprtcCreateProgram failed";
-        return -1;
-    }
-#ifdef FPF_STAMPS
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-DFPF_STAMPS"};
-    hiprtcResult rr = hiprtcCompileProgram(prog, 5, opts);
-#else
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
-    hiprtcResult rr = hiprtcCompileProgram(prog, 4, opts);
-#endif
-    if (rr != HIPRTC_SUCCESS) {
-        size_t n = 0;
-        hiprtcGetProgramLogSize(prog, &n);
-        std::string log(n, '\0');
-        if (n) hiprtcGetProgramLog(prog, &log[0]);
-        *err = std::string("hipRTC compile failed: ") + hiprtcGetErrorString(rr) + "\n" + log.substr(0, 4000);
-        hiprtcDestroyProgram(&prog);
-        return -1;
-    }
-    size_t n = 0;
-    hiprtcGetCodeSize(prog, &n);
-    std::string code(n, '\0');
-    hiprtcGetCode(prog, &code[0]);
-    hiprtcDestroyProgram(&prog);
     RtcKernel k{};
-    if (hipModuleLoadData(&k.mod, code.data()) != hipSuccess) {
-        *err = "hipModuleLoadData failed";
-        return -1;
-    }
-    if (hipModuleGetFunction(&k.fn, k.mod, "fpf_rtc_tiled") != hipSuccess) {
-        (void)hipModuleUnload(k.mod);
-        *err = "hipModuleGetFunction failed";
-        return -1;
-    }
+#ifdef FPF_STAMPS
+    if (compile_load(src, "fpf_rtc_tiled.hip", "fpf_rtc_tiled", nullptr, {"-DFPF_STAMPS"}, &k, err) != 0) return -1;
+#else
+    if (compile_load(src, "fpf_rtc_tiled.hip", "fpf_rtc_tiled", nullptr, {}, &k, err) != 0) return -1;
+#endif
     k.nt = sp.nt;
     // dynamic LDS above the default 64 KiB (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     g_cache[key] = RtcEntry{k, 1};
     *out = k;
     return 0;
+}
+
+// ---- the wave kernel per plan (fpf_wave_body.h, FPF_WSPEC): the same source as
+// the static build with the plan's uniform values defined as constants, so the
+// arithmetic -- and every result -- is the static kernel's.  Measured -4 to -5 %
+// kernel time on the 123-bus feeder (profiles/r04sp, r04rtc).
+std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
+    std::ostringstream s;
+    s << "#define FPF_WSPEC 1\n"
+      << "#define FPF_WSPEC_NN " << w.nn << "\n#define FPF_WSPEC_NL " << w.nl << "\n#define FPF_WSPEC_NBLK " << w.nblk
+      << "\n#define FPF_WSPEC_BDEPTH " << w.bdepth << "\n#define FPF_WSPEC_NCOMP " << w.ncomp
+      << "\n#define FPF_WSPEC_TEMP_SYM " << w.temp_sym << "\n#define FPF_WSPEC_OFF_IN_X " << w.off_in_x
+      << "\n#define FPF_WSPEC_STAGE_U " << w.stage_u << "\n#define FPF_WSPEC_OUT_U " << w.out_u
+      << "\n#define FPF_WSPEC_HAS_MASK " << w.has_mask << "\n#define FPF_WSPEC_HAS_REL " << w.has_rel
+      << "\n#define FPF_WSPEC_MXITR " << w.mxitr << "\n";
+    for (const char *part : kRtcWaveSources) s << part;
+    char nm[96];
+    snprintf(nm, sizeof nm, "fpf::dpf_wave_kernel<%d, %d, %s, %d>", w.spw, w.C, full ? "true" : "false", w.wpb);
+    s << "\ntemplate __global__ void " << nm << "(fpf::WaveDev, int, const double *, fpf::OutDev);\n";
+    *name = nm;
+    return s.str();
+}
+
+int g_wave_rtc_builds = 0;   // successful builds in this process (fpf_wave_rtc_builds)
+
+hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
+    std::string name;
+    const std::string src = wave_rtc_source(w, full, &name);
+    static std::map<std::pair<int, std::string>, hipFunction_t> built;   // NULL: the build failed
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_pair(device, src);
+    auto it = built.find(key);
+    if (it != built.end()) return it->second;
+    RtcKernel k{};
+    std::string err;
+    // the static build's ILP-first scheduler (Makefile: fpf_wave.o)
+    hipFunction_t fn = nullptr;
+    if (compile_load(src, "fpf_rtc_wave.hip", nullptr, name.c_str(),
+                     {"-mllvm", "-amdgpu-sched-strategy=iterative-ilp"}, &k, &err) == 0) {
+        int stat = 0;
+        if (hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.fn) == hipSuccess &&
+            hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - stat) ==
+                hipSuccess)
+            fn = k.fn;
+        else
+            err = "hipFuncSetAttribute failed";
+    }
+    if (!fn && getenv("FPF_DEBUG")) fprintf(stderr, "wave_rtc_function: %s (the static kernel runs)\n", err.c_str());
+    if (fn) ++g_wave_rtc_builds;
+    built[key] = fn;   // (the module stays loaded for the process)
+    return fn;
+}
+
+extern "C" int fpf_wave_rtc_builds(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_wave_rtc_builds;
 }
 
 void rtc_release(const RtcKernel &k) {

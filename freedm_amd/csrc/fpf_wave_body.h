@@ -1,0 +1,1140 @@
+// fpf_wave_body.h -- the wave kernel's device code (dpf_wave_kernel and its
+// helpers), included by fpf_wave.hip and embedded for hipRTC (fpf_rtc.cpp:
+// the per-feeder specialised build, FPF_WSPEC).  See fpf_wave.hip for the design.
+#pragma once
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+#include "fpf_wave_common.h"
+#include "fpf_generic_body.h"
+
+namespace fpf {
+
+// STG row r at index r + r / 16 (FPF_WAVE_SWZ, default on): a lane's slots sit 4
+// positions apart (position q = lane C + c), so the 16-byte Sld reads of 16
+// consecutive lanes hit rows 4 apart -- 4 of the 16 bank groups, a 4-way
+// conflict; one pad row every 16 spreads them over all 16
+#ifndef FPF_WAVE_SWZ
+#define FPF_WAVE_SWZ 1
+#endif
+__host__ __device__ __forceinline__ int swz_row(int r) { return FPF_WAVE_SWZ ? r + (r >> 4) : r; }
+
+// diagnostic ablation build (make ablate): FPF_WAVE_DBG bits switch pieces off;
+// results are wrong when set.  Compiled out of the product.
+#if defined(FPF_WAVE_ABL)
+#define DBG(bit) (FPF_WAVE_ABL & (bit))   // compile-time ablation (tools/build_ablations.sh)
+#elif defined(FPF_WAVE_ABLATE)
+#define DBG(bit) (f.dbg & (bit))
+#else
+#define DBG(bit) 0
+#endif
+
+#ifdef FPF_STAMPS
+// diagnostic build only: lane 0 of each of the first 64 wavefronts records
+// s_memtime at stage boundaries (never read by the kernel itself): [64][128],
+// 0 entry, 1 staged, 2 Sld set up, 4 + 8 it + k inside sweep it < 12 (k = 0 top,
+// 1 backward scan, 2 Ib, 3 convergence, 4 drops, 5 forward scan + stores,
+// 6 block offsets, 7 V), 120 after the loop, 121 V written out
+__device__ unsigned long long *fpf_wave_stamp_buf = nullptr;
+__device__ int fpf_wave_stamp_base = 0;   // the first recorded wave (global wave index)
+#define WSTAMP(idx)                                                                                   \
+    do {                                                                                              \
+        const int gw_ = blockIdx.x * WPB + (threadIdx.x >> 6) - fpf_wave_stamp_base;                   \
+        if (fpf_wave_stamp_buf && (threadIdx.x & 63) == 0 && gw_ >= 0 && gw_ < 64 && (idx) < 128)     \
+            fpf_wave_stamp_buf[gw_ * 128 + (idx)] = __builtin_amdgcn_s_memtime();                       \
+    } while (0)
+extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr, int base) {
+    unsigned long long *p = (unsigned long long *)dptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fpf_wave_stamp_base), &base, sizeof(base)) != hipSuccess) return -3;
+    return hipMemcpyToSymbol(HIP_SYMBOL(fpf_wave_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#else
+#define WSTAMP(idx) ((void)0)
+#endif
+
+constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
+constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging keeps in flight
+// the scenario-fastest batches' staging through the tables too (measured slower:
+// 44.1-44.5 vs 39.4-39.8 us on config 2, profiles/r04e); the feeder tables' loads
+// issued before the tile's (FPF_WAVE_EARLY_TABLES) or after its LDS stores (the
+// default: config 4 0.942-0.945 vs 0.953-0.958 ms, config 2 equal, profiles/r04f)
+#ifndef FPF_WAVE_L0_TABLE
+#define FPF_WAVE_L0_TABLE 0
+#endif
+#ifndef FPF_WAVE_LATE_VINIT   // the warm start's loads after the staging barrier (A/B)
+#define FPF_WAVE_LATE_VINIT 0
+#endif
+#ifndef FPF_WAVE_EARLY_TABLES
+#define FPF_WAVE_EARLY_TABLES 0
+#endif
+
+// experiments (tools/gpu_ab_trees.sh): IBO_LDS keeps the substation current of the
+// previous sweep (the convergence test's Ibo) in the scenario's LDS region instead
+// of 12 VGPRs of every lane; SLD_PREF reads slot 0's loads of the next sweep during
+// the forward sweep's LDS round trips
+#ifndef FPF_WAVE_IBO_LDS
+#define FPF_WAVE_IBO_LDS 0
+#endif
+#ifndef FPF_WAVE_SLD_PREF
+#define FPF_WAVE_SLD_PREF 0
+#endif
+constexpr int REGION_EXTRA = FPF_WAVE_IBO_LDS ? 3 : 0;
+
+template <int SPW, int C>
+struct WaveGeom {
+    static constexpr int L = 64 / SPW;                 // lanes per scenario
+    // waves per SIMD the registers allow (light outputs; the full-output variants of
+    // the larger geometries keep 2 and their registers)
+    static constexpr int MINW = SPW * C <= 2 ? 4 : (C <= 2 ? 3 : 2);
+    // what a workgroup of WPB waves can use of it: whole workgroups per CU (4
+    // SIMDs) -- 3 waves per SIMD with 8-wave workgroups is still one workgroup per
+    // CU, so those take the registers of 2 (config 5's 36-bus area: 37 scratch
+    // loads per sweep at the 168-VGPR cap, none at 256)
+    template <int WPB> static constexpr int eff_minw() { return (MINW * 4 / WPB) * WPB / 4; }
+};
+
+// the TEMP blocks are staged in LDS once per workgroup (a diagnostic build
+// reads them from global memory instead: L1/L2-resident, but the compiler
+// hoists the loads and spills -- 39 % slower, variants_r02a)
+#ifdef FPF_WAVE_TEMP_GLOBAL
+constexpr bool TEMP_IN_LDS = false;
+#else
+constexpr bool TEMP_IN_LDS = true;
+#endif
+
+template <int SPW, int C, bool FULL, int WPB>
+__global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, C>::template eff_minw<WPB>())) void dpf_wave_kernel(
+    WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
+#ifdef FPF_WSPEC
+    // the per-feeder hipRTC build (fpf_rtc.cpp: wave_rtc_source): the plan's
+    // uniform values as constants -- loop bounds, LDS carve-up and branches fold
+    // (fewer VGPRs and scalar spills, profiles/r04sp); the host checks they match
+    f.nn = FPF_WSPEC_NN;
+    f.nl = FPF_WSPEC_NL;
+    f.nblk = FPF_WSPEC_NBLK;
+    f.bdepth = FPF_WSPEC_BDEPTH;
+    f.ncomp = FPF_WSPEC_NCOMP;
+    f.temp_sym = FPF_WSPEC_TEMP_SYM;
+    f.off_in_x = FPF_WSPEC_OFF_IN_X;
+    f.stage_u = FPF_WSPEC_STAGE_U;
+    f.out_u = FPF_WSPEC_OUT_U;
+    f.has_mask = FPF_WSPEC_HAS_MASK;
+    f.has_rel = FPF_WSPEC_HAS_REL;
+    f.mxitr = FPF_WSPEC_MXITR;
+    f.dbg = 0;
+    f.stag_lo = f.stag_hi = f.stag_n = 0;
+#endif
+    constexpr int L = WaveGeom<SPW, C>::L, SPB = WPB * SPW;
+    constexpr int NT = WPB * 64;
+    extern __shared__ double2 lds[];
+    if (DBG(4096)) return;
+    if (o.skip && *o.skip) return;   // (the multi-area solve's device-side stop)
+    if ((int)blockIdx.x >= f.stag_lo && (int)blockIdx.x < f.stag_hi)
+        for (int i = 0; i < f.stag_n; ++i) __builtin_amdgcn_s_sleep(127);
+    WSTAMP(0);
+    // the guard's local list (OutDev::fix_dev): scenarios this workgroup flagged
+    __shared__ int fix_n, fix_ids[SPB];
+    if (threadIdx.x == 0) fix_n = 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int seg = lane / L, li = lane % L;
+    const int sc = wv * SPW + seg;                 // scenario within the workgroup
+    // XCD-aware tile order: blocks b and b + 8 share an XCD (and its L2), so they
+    // get neighbouring tiles -- the 128-byte rows two 8-scenario tiles share are
+    // fetched into one L2 (MI355X_MICROARCH.md, workgroup placement)
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int s0 = tile * SPB, s = s0 + sc;
+    const int nsb = min(SPB, B - s0);              // scenarios of this workgroup
+    const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
+    // LDS: per workgroup the TEMP values, the block-chain table and the slots'
+    // nodes; the staged loads STG [3][Nl + 1][SPB + 1] of (P, Q) / (bkva/3), one
+    // column per scenario (row Nl = 0 for empty slots; the +1 column spreads a
+    // slot's rows over the banks), read in place every sweep and overwritten by
+    // the scenario's V (node k at row k - 1) in its last sweep; per scenario the
+    // gathered scan values X ([3][XC], entry XC-1 = 0; backward and forward
+    // entries share it), the block offsets and the source voltage
+    const int ntm = f.temp_sym ? 4 : 9;                               // TEMP entries per slot
+    double2 *const tl = lds;                                          // [ntm][C][L] if TEMP_IN_LDS
+    int *const pairs = (int *)(tl + (TEMP_IN_LDS ? ntm * C * L : 0)); // [bdepth][2][nblk]
+    const int pair_n = (2 * bdepth * nblk + 3) & ~3;
+    int *const knode = pairs + pair_n;                                // [C][L] node of each slot
+    constexpr int SROW = SPB + 1;
+    const int PSTR = (swz_row(nl) + 1) * SROW;                        // double2 per phase plane of STG
+    double2 *const stg = (double2 *)(knode + C * L);
+    double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
+    const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
+    const int RS = (3 * XC + noff + 4 + REGION_EXTRA) | 1;           // double2 per region (+ the guard record)
+    double2 *const X = reg0 + sc * RS;
+    double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
+    // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
+    // pair read of the scenario precedes the offset stores in its one wave's
+    // program order), else after X
+    double2 *const OFF = f.off_in_x ? X : X + 3 * XC;
+    const int OS = f.off_in_x ? XC : nblk;
+    const bool live = sc < nsb;
+    int si[C], sb[C], bk[C];   // sb: the slot's (row, scenario) in a phase plane of STG
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int r = f.slot_row[c * L + li];
+        sb[c] = swz_row(r < 0 ? nl : r) * SROW + sc;
+        si[c] = f.slot_info[c * L + li];
+        bk[c] = f.slot_blk[c * L + li];
+    }
+    const double inv_s3 = 1.0 / f.s3;
+
+    // the multi-area solve's warm start (OutDev::vinit_re / _im): node k of each
+    // slot from the given V, loaded before the tile's loads so that their
+    // latencies overlap (the slot's node from the global table: LDS is not staged)
+    cx v[C][3];
+    const bool warm = o.vinit_re && live && !FPF_WAVE_LATE_VINIT;
+    if (warm) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (si_valid(si[c])) {
+                const int k = f.slot_node[c * L + li];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    v[c][p] = mk(o.vinit_re[((size_t)p * nn + k) * B + s], o.vinit_im[((size_t)p * nn + k) * B + s]);
+            }
+    }
+
+    // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced (16 scenarios = one
+    // 128-byte line per row), all of a thread's loads in flight, into STG scaled
+    // by 1/(bkva/3) (Sld, DPF_return7.cpp:46-50)
+    {
+        double *const sd = (double *)stg;
+        // element (f, row, j) of pq -> STG[f / 2][row][j].{re, im}
+        auto spos = [&](int fr, int j) {
+            const int fq = fr / nl, r = fr - fq * nl;
+            return 2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(r)) * SROW + j) + (fq & 1);
+        };
+        // the same for a known (field, row)
+        auto spos2 = [&](int fq, int r, int j) {
+            return 2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(r)) * SROW + j) + (fq & 1);
+        };
+        if ((int)threadIdx.x < 3 * SROW)   // the zero row of each phase plane
+            stg[((int)threadIdx.x / SROW) * PSTR + swz_row(nl) * SROW + (int)threadIdx.x % SROW] = make_double2(0.0, 0.0);
+        // the feeder tables (L2-resident): their loads issued first, in flight
+        // together with the tile's loads; stored to LDS after them
+        constexpr int UT = (9 * C * L + NT - 1) / NT;
+        double2 tt[TEMP_IN_LDS ? UT : 1];
+        const int np2 = 2 * bdepth * nblk;
+        int pv = 0, kv = 0;
+        auto table_loads = [&]() {
+            if (TEMP_IN_LDS) {
+#pragma unroll
+                for (int u = 0; u < UT; ++u) {
+                    const int i = u * NT + (int)threadIdx.x;
+                    tt[u] = ld_global2(f.slot_temp, i < ntm * C * L ? i : 0);
+                }
+            }
+            pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
+            kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
+        };
+        if (FPF_WAVE_EARLY_TABLES) table_loads();
+        constexpr int U = 8;
+        const int total = DBG(256) ? 0 : 6 * nl * SPB;
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        constexpr int US = WAVE_STAGE_U;
+        const int SU = f.stage_u;
+        if (SU > 0 && (o.smaj || (FPF_WAVE_L0_TABLE && (B & 1) == 0))) {
+            // table-driven (wave_stage_tables): chunk c = u NT + t, 16 bytes each, every
+            // load of the thread in flight with its two STG destinations; scenario
+            // major: the tile is one contiguous block of nsb x 6 Nl doubles;
+            // scenario fastest: chunk c is scenarios (2 (t % H), + 1) of pq line tb.x
+            // valid chunks: scenario major, the first nsb scenarios' (contiguous);
+            // scenario fastest, every line of the pairs below nsb
+            const int nchunk = DBG(256) ? 0 : (o.smaj ? nsb : SPB) * 3 * nl;
+            constexpr int H = SPB / 2;
+            const int jj = 2 * ((int)threadIdx.x % H);
+            const int2 *tab = (const int2 *)(o.smaj ? f.stage_smaj : f.stage_l0);
+            const d2v *src = (const d2v *)(pq + (size_t)s0 * 6 * nl);
+            int2 tb[US];
+            d2v r[US];
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                if (u < SU) {
+                    const int c = u * NT + (int)threadIdx.x;
+                    tb[u] = tab[c];
+                    const bool ok = c < nchunk && (o.smaj || jj < nsb);
+                    if (o.smaj) {
+                        r[u] = __builtin_nontemporal_load(src + (ok ? c : 0));
+                    } else {
+                        // (the line of chunk c is t / H + u NT / H: the load does not
+                        // wait for the table entry)
+                        const int fr = (int)threadIdx.x / H + u * (NT / H);
+                        const size_t ga = (size_t)fr * B + s0 + jj;
+                        r[u] = __builtin_nontemporal_load((const d2v *)(pq + (ok ? ga : 0)));
+                        r[u] = ok ? r[u] : d2v{0.0, 0.0};
+                    }
+                }
+            }
+#ifdef FPF_STAMPS
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            WSTAMP(3);
+#endif
+            double *const sd = (double *)stg;
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                const int c = u * NT + (int)threadIdx.x;
+                if (u < SU && c < 3 * nl * SPB && (o.smaj ? c < nchunk : true)) {
+                    sd[o.smaj ? tb[u].x : tb[u].y] = r[u].x * inv_s3;
+                    sd[o.smaj ? tb[u].y : tb[u].y + 2] = r[u].y * inv_s3;
+                }
+            }
+            if (o.smaj) {   // a partial last tile: zero loads in the columns of its missing scenarios
+                const int per = 6 * nl;
+                for (int i = threadIdx.x; i < (SPB - nsb) * per; i += NT) {
+                    const int j = nsb + i / per, fr = i % per;
+                    sd[spos(fr, j)] = 0.0;
+                }
+            }
+        } else if (o.smaj) {
+            // scenario-major layout: the tile's nsb scenarios are one contiguous
+            // block of nsb x 6 Nl doubles, read with 16-byte loads (6 Nl is even)
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            constexpr int U2 = 16;
+            const int per = 6 * nl, total2 = DBG(256) ? 0 : nsb * (per / 2);
+            const d2v *src = (const d2v *)(pq + (size_t)s0 * per);
+            // element e = 2 i of the block: scenario j = e / per, (field, row) of
+            // e % per -- walked 2 NT elements per load, no division per element
+            int j = 2 * (int)threadIdx.x / per;
+            RowWalk w;
+            w.init(2 * (int)threadIdx.x - j * per, 2 * NT, nl);
+            for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
+                d2v r[U2];
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    r[u] = __builtin_nontemporal_load(src + (i < total2 ? i : 0));
+                }
+#ifdef FPF_STAMPS
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (i0 == 0) WSTAMP(3);
+#endif
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    if (i < total2) {   // e and e + 1 belong to one scenario (per is even)
+                        sd[spos2(w.fq, w.rr, j)] = r[u].x * inv_s3;
+                        sd[w.rr + 1 < nl ? spos2(w.fq, w.rr + 1, j) : spos2(w.fq + 1, 0, j)] = r[u].y * inv_s3;
+                    }
+                    w.next();
+                    while (w.fq >= 6) { w.fq -= 6; ++j; }
+                }
+            }
+            // a partial last tile: zero loads in the columns of its missing scenarios
+            for (int i = threadIdx.x; i < (SPB - nsb) * per; i += NT) {
+                const int j = nsb + i / per, fr = i % per;
+                sd[spos(fr, j)] = 0.0;
+            }
+        } else if ((B & 1) == 0) {
+            // 16-byte loads (B even: every pair of scenarios is aligned), all of a
+            // thread's loads in flight at once for feeders up to ~128 rows
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            constexpr int U2 = 16, H = SPB / 2;
+            static_assert(NT % H == 0, "a thread keeps its scenario pair");
+            const int total2 = total / 2;
+            // pair i: scenarios j, j + 1 with j = 2 (i % H), the same for all of a
+            // thread's loads; (field, row) i / H walked NT / H rows per load
+            const int j = 2 * ((int)threadIdx.x % H);
+            RowWalk w, w2;   // the loads' walk, and the same walk again for the stores
+            w.init((int)threadIdx.x / H, NT / H, nl);
+            w2 = w;
+            for (int i0 = 0; i0 < total2; i0 += U2 * NT) {
+                d2v r[U2];
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    const int fr = w.fq * nl + w.rr;
+                    const bool ok = i < total2 && j < nsb;   // nsb is even
+                    const size_t ga = DBG(16384) ? (size_t)s0 * 6 * nl + 2 * (size_t)i : (size_t)fr * B + s0 + j;
+                    r[u] = __builtin_nontemporal_load((const d2v *)(pq + (ok ? ga : 0)));
+                    r[u] = ok ? r[u] : d2v{0.0, 0.0};
+                    w.next();
+                }
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    const int i = i0 + u * NT + (int)threadIdx.x;
+                    if (i < total2) {
+                        const int q = spos2(w2.fq, w2.rr, j);
+                        sd[q] = r[u].x * inv_s3;
+                        sd[q + 2] = r[u].y * inv_s3;
+                    }
+                    w2.next();
+                }
+            }
+        } else
+        for (int i0 = 0; i0 < total; i0 += U * NT) {
+            double r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                const int j = i % SPB, fr = i / SPB;
+                const bool ok = i < total && j < nsb;
+                r[u] = __builtin_nontemporal_load(pq + (ok ? (size_t)fr * B + s0 + j : 0));
+                r[u] = ok ? r[u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                if (i < total) sd[spos(i / SPB, i % SPB)] = r[u] * inv_s3;
+            }
+        }
+        if (!FPF_WAVE_EARLY_TABLES) table_loads();
+        if (TEMP_IN_LDS) {
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                const int i = u * NT + (int)threadIdx.x;
+                if (i < ntm * C * L) tl[i] = tt[u];
+            }
+        }
+        if ((int)threadIdx.x < np2) pairs[threadIdx.x] = pv;
+        for (int i = threadIdx.x + NT; i < np2; i += NT) pairs[i] = f.blk_pairs[i];
+        if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
+    }
+    if (o.hook && o.hook->pre_n > 0) {
+        // the multi-area solve (OutDev::hook): the rows children hang off carry
+        // their source powers too, scaled like the loads
+        __syncthreads();
+        const AreaHook *const h = o.hook;
+        double *const sd = (double *)stg;
+        for (int i = threadIdx.x; i < h->pre_n * 6 * SPB; i += NT) {
+            const int j = i % SPB, q = i / SPB, kid = q / 6, fq = q % 6;
+            if (j < nsb)
+                sd[2 * (((fq >> 1) * (swz_row(nl) + 1) + swz_row(h->pre_lrow[kid])) * SROW + j) + (fq & 1)] +=
+                    h->pre_sin[kid][(size_t)fq * B + s0 + j] * inv_s3;
+        }
+    }
+    __syncthreads();
+    WSTAMP(1);
+    if (DBG(8192)) return;
+    // this lane's block chain (lane b < nblk resolves block b), padded with the zero
+    // entry; the two indices of a pair packed in one register (XC < 2^16)
+    int bp[WAVE_BD];
+#pragma unroll
+    for (int j = 0; j < WAVE_BD; ++j) {
+        const bool ok = j < bdepth && li < nblk;
+        bp[j] = ok ? pairs[(2 * j) * nblk + li] | (pairs[(2 * j + 1) * nblk + li] << 16) : (XC - 1) | ((XC - 1) << 16);
+    }
+    if (li < 3) X[li * XC + XC - 1] = make_double2(0.0, 0.0);
+    double2 *const IBO = X + 3 * XC + noff + 4;   // (FPF_WAVE_IBO_LDS) Ibo per phase
+    if (FPF_WAVE_IBO_LDS && li < 3) IBO[li] = make_double2(0.0, 0.0);
+    // per-scenario results for the workgroup aggregate: [sc][loss, vmin, vmax, status]
+    __shared__ double res[SPB][4];
+
+    // the source voltage: V0 (DPF_return7.cpp:84-89), or this scenario's when the
+    // caller supplies one (an area of the multi-area solve, fed from its boundary bus)
+    {
+        cx v0[3] = {mk(f.V0[0], f.V0[1]), mk(f.V0[2], f.V0[3]), mk(f.V0[4], f.V0[5])};
+        if (o.vsrc && live) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) v0[p] = mk(o.vsrc[(size_t)(2 * p) * B + s], o.vsrc[(size_t)(2 * p + 1) * B + s]);
+        }
+        if (li < 3) stx(V0S, li, li == 0 ? v0[0] : (li == 1 ? v0[1] : v0[2]));
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (!warm || !si_valid(si[c]))
+#pragma unroll
+                for (int p = 0; p < 3; ++p) v[c][p] = v0[p];   // V(0..Nl-1) = V0  (:92-96)
+        if (o.vinit_re && live && FPF_WAVE_LATE_VINIT) {
+            // the multi-area solve's warm start: node k of each slot from the given V
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                if (si_valid(si[c])) {
+                    const int k = knode[c * L + li];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        v[c][p] = mk(o.vinit_re[((size_t)p * nn + k) * B + s], o.vinit_im[((size_t)p * nn + k) * B + s]);
+                }
+        }
+    }
+
+    // A scenario's results are recorded in its last sweep (converged, or the
+    // mxitr-th); its lanes then sweep along without storing until the wave's
+    // last scenario is done.
+    cx ibo[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+    bool done = !live;
+    // flat start (V = V0 on every node, DPF_return7.cpp:92-96, the feeder's own
+    // source): the first sweep's load currents use the uniform 1/|V0_p|^2, and
+    // sum_k |S_k|_1 of the guard record is taken from that sweep's Sld reads
+    const bool flat = !o.vsrc && !o.vinit_re;
+    // the convergence test's eps^2 (the multi-area solve's inexact outer
+    // iterations pass their own, OutDev::eps_dev)
+    const double eps2 = o.eps_dev ? *o.eps_dev * *o.eps_dev : f.eps * f.eps;
+    // the guard record V0S[3] = (sum_k |S_k|_1, closest |err2 - eps^2| of a decision
+    // in the coarse band, +inf: none) of the scenario, in LDS (fpf_api.cpp: guard_factor)
+    if (o.flag_count && !flat) {
+        double sabs = 0.0;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx x = ldx(stg, p * PSTR + sb[c]);
+                sabs += fabs(x.re) + fabs(x.im);
+            }
+        sabs = seg_incl<L>(sabs);
+        if (li == L - 1) V0S[3] = make_double2(sabs, INFINITY);
+    }
+#ifdef FPF_WAVE_STAGGER
+    // diagnostic: start the second half of the workgroup's waves (each shares a
+    // SIMD with one of the first half) later, so partners sit in different
+    // phases of a sweep (MI355X_MICROARCH.md "Two waves per SIMD", item 9)
+    if (WPB >= 8 && wv >= WPB / 2) __builtin_amdgcn_s_sleep(FPF_WAVE_STAGGER);
+#endif
+    WSTAMP(2);
+    cx slp[3];   // (FPF_WAVE_SLD_PREF) slot 0's loads, read a sweep ahead
+#pragma unroll
+    for (int p = 0; p < 3; ++p) slp[p] = FPF_WAVE_SLD_PREF ? ldx(stg, p * PSTR + sb[0]) : mk(0, 0);
+    for (int it = 0; __ballot(!done) != 0; ++it) {
+        WSTAMP(4 + 8 * it);
+        // ---- load currents (:106-130)
+        cx il[C][3], ib[C][3];
+#ifndef FPF_WAVE_GROUP
+#define FPF_WAVE_GROUP 1   // measured: 1 (grouped) -1.7 % on configs 2 and 4 against 0; 2 (pipelined) alike
+#endif
+#if FPF_WAVE_GROUP == 0
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(stg, p * PSTR + sb[c]), v[c][p]);
+#else
+        if (flat && it == 0) {
+            // IL = conj(S/V0) = conj(S) V0 / |V0|^2 (V0 != 0), every Sld read once
+            double sabs = 0.0;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                cx sl[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) sl[p] = ldx(stg, p * PSTR + sb[c]);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const double vr = f.V0[2 * p], vi = f.V0[2 * p + 1], r0 = f.rv0[p];
+                    il[c][p] = mk(fma(sl[p].re, vr, sl[p].im * vi) * r0, fma(sl[p].re, vi, -(sl[p].im * vr)) * r0);
+                    sabs += fabs(sl[p].re) + fabs(sl[p].im);
+                }
+            }
+            if (o.flag_count) {
+                sabs = seg_incl<L>(sabs);
+                if (li == L - 1) V0S[3] = make_double2(sabs, INFINITY);
+            }
+        } else {
+            // a slot's three Sld reads issued together (FPF_WAVE_GROUP 2: the next
+            // slot's before this slot's arithmetic); scheduling barriers keep the
+            // groups, so the register allocator cannot fall back to one read in
+            // flight at a time
+            cx sl[3], sn[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sl[p] = FPF_WAVE_SLD_PREF ? slp[p] : ldx(stg, p * PSTR + sb[0]);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) sn[p] = ldx(stg, p * PSTR + sb[c + 1]);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(sl[p], v[c][p]);
+                if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) sn[p] = ldx(stg, p * PSTR + sb[c + 1]);
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) sl[p] = sn[p];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#endif
+
+        // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of IL;
+        // Einc is gathered at subtree ends only (leaves)
+        cx tot[3], exl[3];
+        double sc6[6];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = il[0][p];
+            ib[0][p] = acc;
+#pragma unroll
+            for (int c = 1; c < C; ++c) { acc = cadd(acc, il[c][p]); ib[c][p] = acc; }
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<L>(sc6);
+        WSTAMP(5 + 8 * it);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx inc = mk(sc6[2 * p], sc6[2 * p + 1]);
+            tot[p] = inc;   // the segment total in its last lane
+            exl[p] = csub(inc, ib[C - 1][p]);   // the lane's exclusive prefix
+#pragma unroll
+            for (int c = 0; c < C; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // Einc at this slot
+        }
+        wfence();
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int ci = si_store_b(si[c]);
+            if (ci >= 0 && !DBG(32)) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, ib[c][p]);
+            }
+        }
+        wfence();
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            // Ib = Einc[last] - Eexc; Eexc of slot c = Einc of slot c-1, of slot 0 the lane's prefix
+            cx eprev = exl[p];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const cx e = ib[c][p];
+                ib[c][p] = csub(ldx(X, p * XC + si_last(si[c])), eprev);
+                eprev = e;
+            }
+        }
+
+        WSTAMP(6 + 8 * it);
+        // ---- convergence on the substation branch (:199-217): Ib(0) = the segment total;
+        // max_p |Ib(0,p) - Ibo(p)| < eps compared as squares
+        double err2 = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx io = FPF_WAVE_IBO_LDS ? ldx(IBO, p) : ibo[p];
+            const double dr = tot[p].re - io.re, di = tot[p].im - io.im;
+            err2 = fmax(err2, fma(dr, dr, di * di));
+            if (!FPF_WAVE_IBO_LDS) ibo[p] = tot[p];
+        }
+        if (FPF_WAVE_IBO_LDS && li == L - 1) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) stx(IBO, p, tot[p]);
+        }
+        // decided in the segment's last lane, broadcast by ballot
+        const unsigned long long cbits = __ballot(li == L - 1 && err2 < eps2);
+        const bool conv = (cbits >> (seg * L + L - 1)) & 1;
+        const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
+        if (o.flag_count) {
+            // ---- the convergence guard (fpf_opts.no_guard = 0): the decision above
+            // tests a scan-ordered Ib(0).  Where errmx lies within the rounding band
+            // of eps (fpf_api.cpp: guard_factor) the reference's sequential sum could
+            // decide the other way.  Decisions within 2^-9 of eps^2 (rare) keep their
+            // distance from eps^2 in the scenario's LDS record (no register stays
+            // live for it); the band itself is evaluated after the loop
+            const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
+            if (li == L - 1 && !done && dd <= 0x1p-9 * e2) {
+                double2 g = V0S[3];
+                g.y = fmin(g.y, dd);
+                V0S[3] = g;
+            }
+        }
+        if (fin && li == L - 1 && o.errmx) o.errmx[s] = sqrt(err2);
+        // the loss terms are needed only in a scenario's last sweep
+        const bool any_fin = __ballot(fin) != 0;
+        WSTAMP(7 + 8 * it);
+
+        // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
+        // Also Re(drop . conj(Ib)) per phase: on a feeder without zeroed phases
+        // PQb(0).re - sum_k PQL(k).re = s3 sum_a Re(drop_a conj(Ib_a)) exactly
+        // (V_k = V0 - A_k, sum_k A_k conj(IL_k) = sum_a drop_a conj(Ib_a)), so the
+        // VVC loss needs neither IL nor Ib after this point
+        cx g[C][3];
+        double lp[3] = {0.0, 0.0, 0.0};
+        if (f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
+            // one common off-diagonal zm: drop_a = (z_aa - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
+#if FPF_WAVE_GROUP == 0
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                // (ablation 65536: wave-uniform TEMP from the kernel arguments, no LDS reads)
+                const cx m = DBG(65536) ? mk(f.lb_v * 1e-3, f.ub_v * 1e-3) : ldx(tl, (3 * C + c) * L + li);
+                const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
+                const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx d = DBG(65536) ? mk(f.eps * (a + 1), f.V0[0] * 1e-3) : ldx(tl, (a * C + c) * L + li);
+                    const cx b = ib[c][a];
+                    g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
+                }
+            }
+#else
+            // a slot's four TEMP reads issued together (2: the next slot's first)
+            cx tq[4], tn[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) tn[j] = ldx(tl, (j * C + c + 1) * L + li);
+                }
+                const cx m = tq[3];
+                const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
+                const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const cx d = tq[a];
+                    const cx b = ib[c][a];
+                    g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
+                }
+                if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) tn[j] = ldx(tl, (j * C + c + 1) * L + li);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) tq[j] = tn[j];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
+        } else
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                cx tm[9];
+#pragma unroll
+                for (int l = 0; l < 3; ++l) {
+                    const int ti = ((l * 3 + a) * C + c) * L + li;
+                    if (DBG(1)) tm[l * 3 + a] = mk(0.001 * l, 0.002 * a);
+                    else if (TEMP_IN_LDS) tm[l * 3 + a] = ldx(tl, ti);
+                    else { const double2 t = ld_global2(f.slot_temp, ti); tm[l * 3 + a] = mk(t.x, t.y); }
+                }
+                g[c][a] = drop_col_fma(tm, ib[c][0], ib[c][1], ib[c][2], a);
+            }
+#ifdef FPF_WAVE_SB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+        // (a wave-uniform branch of its own: inside the slot loops the compiler turned
+        // the accumulation into selects executed every sweep)
+        if (any_fin) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
+        }
+        WSTAMP(8 + 8 * it);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            cx acc = g[0][p];
+#pragma unroll
+            for (int c = 1; c < C; ++c) { acc = cadd(acc, g[c][p]); g[c][p] = acc; }
+            sc6[2 * p] = acc.re;
+            sc6[2 * p + 1] = acc.im;
+        }
+        seg_incl_n<L>(sc6);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx ex = csub(mk(sc6[2 * p], sc6[2 * p + 1]), g[C - 1][p]);
+#pragma unroll
+            for (int c = 0; c < C; ++c) g[c][p] = cadd(ex, g[c][p]);   // Ginc at this slot
+        }
+        wfence();
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int ci = si_store_f(si[c]);
+            if (ci >= 0 && !DBG(64)) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+            }
+        }
+        wfence();
+        if (FPF_WAVE_SLD_PREF) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) slp[p] = ldx(stg, p * PSTR + sb[0]);
+        }
+        WSTAMP(9 + 8 * it);
+        // block offsets, one lane per block (block 0, node 1's chain, has none),
+        // stored as V0 - off so that V = (V0 - off) - Ginc is one subtraction per
+        // slot; the chain's index pairs sit in registers (bp), all its reads issue together
+        if (DBG(8)) {
+            if (li < 3) X[li * XC] = V0S[li];
+        } else if (nblk <= L && bdepth <= WAVE_BD) {
+            if (li < nblk) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+#pragma unroll
+                for (int j = 0; j < WAVE_BD; ++j) {
+                    if (j < bdepth) {   // uniform
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(ldx(V0S, p), of[p]));
+            }
+        } else {
+            for (int b = li; b < nblk; b += L) {
+                cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+                for (int j = 0; j < bdepth; ++j) {
+                    const int pa = pairs[(2 * j) * nblk + b], mi = pairs[(2 * j + 1) * nblk + b];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
+                }
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(ldx(V0S, p), of[p]));
+            }
+        }
+        wfence();
+        WSTAMP(10 + 8 * it);
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx vr = csub(ldx(OFF, p * OS + bk[c]), g[c][p]);   // V0 - A(k)
+                if (FULL) g[c][p] = vr;
+                v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;
+            }
+        if (FULL && f.has_rel) {
+            // below a zeroed ancestor m: V(k,p) = A(m) - A(k) = Vr(k) - Vr(m), Vr = V0 - A
+            // before the zeroing (held in g)
+            wfence();
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int ci = si_store_f(si[c]);
+                if (ci >= 0) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(X, p * XC + ci, g[c][p]);
+                }
+            }
+            wfence();
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const int mr = f.slot_mref[(p * C + c) * L + li];
+                    if (mr >= 0 && !((si_mask(si[c]) >> p) & 1)) v[c][p] = csub(g[c][p], ldx(X, p * XC + mr));
+                }
+        }
+        wfence();
+        WSTAMP(11 + 8 * it);
+
+        if (fin && !DBG(128)) {
+            // ---- a scenario's last sweep: V in node order into its region (Sld is
+            // not needed again; the workgroup writes V out after the loop), loss
+            // (VoltVarCtrl.cpp:1152-1161), Vmin/Vmax (V_abc_list.cpp:7-81,
+            // VoltVarCtrl.cpp:1201-1207); whole segments
+            double mn = INFINITY, mx = -INFINITY, x;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (si_valid(si[c])) {
+                    const int k = knode[c * L + li];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        stx(stg, p * PSTR + swz_row(k - 1) * SROW + sc, v[c][p]);   // over the scenario's own Sld
+                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                        const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
+                        mn = fmin(mn, m2);
+                        mx = fmax(mx, m2);
+                    }
+                }
+            }
+            if (FPF_WAVE_IBO_LDS) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) ibo[p] = ldx(IBO, p);   // (this sweep's Ib(0))
+            }
+            if (li == L - 1) {   // the lane holding Ib(0)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const cx v0p = ldx(V0S, p);
+                    // substation row 0: V0 (in V0S), Ib(0) = this sweep's total, no load
+                    if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0p, mk(0, 0), ibo[p]);
+                    if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
+                        const cx sb = cmul(cmul(v0p, mk(f.s3, 0.0)), cconj(ibo[p]));
+                        o.s_in[(size_t)(2 * p) * B + s] = sb.re;
+                        o.s_in[(size_t)(2 * p + 1) * B + s] = sb.im;
+                    }
+                    const double m2 = fma(v0p.re, v0p.re, v0p.im * v0p.im);
+                    mn = fmin(mn, m2);
+                    mx = fmax(mx, m2);
+                }
+            }
+            if (!FULL || !f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
+                // every Lnum_p + 1 = Nn: V_abc_list keeps every row, so the extremes are
+                // plain min/max; loss = s3 sum Re(drop conj(Ib))
+                x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
+                mn = sqrt(seg_reduce_min<L>(mn));
+                mx = sqrt(seg_reduce_max<L>(mx));
+            } else {
+                // general V_abc_list: per phase the first K_p nonzero |V| in row order,
+                // zero padded; loss from PQb(0) and PQL as the reference sums them
+                wfence();
+                double sl = 0.0;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        if (si_valid(si[c])) sl += f.s3 * (v[c][p].re * il[c][p].re + v[c][p].im * il[c][p].im);
+                sl = seg_incl<L>(sl);
+                x = 0.0;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) x += cmul(cmul(ldx(V0S, p), mk(f.s3, 0.0)), cconj(ibo[p])).re;
+                x -= sl;
+                mn = INFINITY;
+                mx = -INFINITY;
+                const unsigned long long segbits = L == 64 ? ~0ull : ((1ull << L) - 1ull) << (seg * L);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const int K = f.K[p];
+                    int cnt = 0;
+                    for (int k0 = 0; k0 < nn; k0 += L) {
+                        const int k = k0 + li;
+                        double m = 0.0;
+                        if (k < nn) {
+                            const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
+                            m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
+                        }
+                        const bool nz = k < nn && m != 0.0;
+                        const unsigned long long bal = __ballot(nz) & segbits;
+                        const int rank = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+                        if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
+                        cnt += __popcll(bal);
+                    }
+                    if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+                }
+                mn = seg_reduce_min<L>(mn);
+                mx = seg_reduce_max<L>(mx);
+            }
+            if (li == L - 1) {
+                // (the output addresses formed here, not kept in registers across the loop)
+                int sf = s;
+                __asm__ volatile("" : "+v"(sf));
+                if (o.iters) o.iters[sf] = it + 1;
+                if (o.status) o.status[sf] = conv ? 0 : 1;
+                if (o.loss) o.loss[sf] = x;
+                if (o.vmin) o.vmin[sf] = mn;
+                if (o.vmax) o.vmax[sf] = mx;
+                res[sc][1] = mn;
+                res[sc][2] = mx;
+                res[sc][0] = x;
+                res[sc][3] = conv ? 0.0 : 1.0;
+            }
+            wfence();
+        }
+        done = done || fin;
+    }
+    WSTAMP(120);
+
+    // ---- the guard band (fpf_api.cpp: guard_factor) for the scenarios with a decision
+    // in the coarse band: errmx within tau = guard_k sum_k |IL_k|_1 of eps, where
+    // sum_k |IL_k|_1 <= sqrt2 sum_k |S_k|_1 / min_k |V_k| over the nonzero V (the
+    // final V; 1.25 covers its drift from the deciding sweep's).  Flagged scenarios
+    // are re-solved on the exact kernel (dpf_fixup_kernel)
+    if (o.flag_count && live) {
+        const double2 g = V0S[3];
+        const bool cand = g.y < INFINITY;
+        if (__ballot(cand) != 0) {
+            double m2 = INFINITY;
+            for (int k = li; k < nn; k += L) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
+                    const double d = fma(vv.re, vv.re, vv.im * vv.im);
+                    if (d > 0.0) m2 = fmin(m2, d);
+                }
+            }
+            m2 = seg_reduce_min<L>(m2);
+            const double tau = 1.25 * f.guard_k * 1.4142135623730951 * g.x / sqrt(m2);
+            const bool near = cand && g.y <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
+            if (li == L - 1 && near)
+                guard_flag(o, s, &fix_n, fix_ids);
+            if (li == L - 1 && o.guard) o.guard[s] = near ? 1 : 0;
+        } else if (li == L - 1 && o.guard) {
+            o.guard[s] = 0;
+        }
+    } else if (live && li == L - 1 && o.guard) {
+        o.guard[s] = 0;   // (guard off)
+    }
+
+    // ---- fused batch aggregate [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over,
+    // n_under, n_scen] over converged scenarios: the workgroup's partial in
+    // scenario order, published with agent-scope stores; one ticket per
+    // workgroup; the last to arrive folds the partials in workgroup order
+    // (deterministic) -- the hand-off of MI355X_MICROARCH.md "Valid forms".
+    // Published before the V stores, so the ticket does not wait for them.
+    // the write-out table (wave_stage_tables; L2-resident), in flight across the barrier
+    constexpr int UO = WAVE_STAGE_U;
+    const int OU = (!FULL && (o.v_re || o.v_im) && !DBG(1024)) ? f.out_u : 0;
+    int otab[UO];
+    {
+        const int32_t *ot = o.smaj ? f.out_smaj : f.out_l0;
+#pragma unroll
+        for (int u = 0; u < UO; ++u)
+            if (u < OU) otab[u] = ot[u * NT + (int)threadIdx.x];
+    }
+    WSTAMP(122);
+    __syncthreads();
+    WSTAMP(123);
+    if (o.hook && o.hook->post_n > 0) {
+        // the multi-area solve (OutDev::hook): each child's source voltage = V at
+        // its boundary bus, the largest move into the iteration's slot
+        const AreaHook *const h = o.hook;
+        double d = 0.0;
+        for (int i = threadIdx.x; i < h->post_n * 3 * SPB; i += NT) {
+            const int j = i % SPB, q = i / SPB, kid = q / 3, p = q % 3;
+            if (j < nsb) {
+                const double2 vv = stg[p * PSTR + swz_row(h->post_lb[kid] - 1) * SROW + j];
+                double *const vs = h->post_vsrc[kid] + (size_t)(2 * p) * B + s0 + j;
+                d = fmax(d, fmax(fabs(vv.x - vs[0]), fabs(vv.y - vs[B])));
+                vs[0] = vv.x;
+                vs[B] = vv.y;
+            }
+        }
+        for (int w = 32; w > 0; w >>= 1) d = fmax(d, __shfl_xor(d, w));
+        if (lane == 0 && d > 0.0) atomicMax(o.move, (unsigned long long)__double_as_longlong(d));
+    }
+    __shared__ int last_wg;
+    const bool agg = o.agg && !DBG(2048);
+    if (agg && threadIdx.x == 0) {
+        double ls = 0, mn = INFINITY, mx = -INFINITY, nc = 0, nnc = 0, no = 0, nu = 0;
+        for (int j = 0; j < nsb; ++j) {
+            if (res[j][3] == 0.0) {
+                ls += res[j][0];
+                mn = fmin(mn, res[j][1]);
+                mx = fmax(mx, res[j][2]);
+                nc += 1;
+                if (res[j][2] > f.ub_v) no += 1;
+                if (res[j][1] < f.lb_v) nu += 1;
+            } else {
+                nnc += 1;
+            }
+        }
+        const double part[8] = {ls, mn, mx, nc, nnc, no, nu, (double)nsb};
+        double *dst = o.partials + 8 * (size_t)tile;   // folded in tile (scenario) order
+        for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_wg = t == gridDim.x - 1;
+    }
+    // ---- the workgroup's V, coalesced: consecutive scenarios of one (phase, node),
+    // or (scenario major) the tile's contiguous [nsb][3][Nn] block
+    if (OU > 0) {
+        // element i = u NT + t of the tile's block, read from STG at otab[u]
+        const int per = 3 * nn, ntot = SPB * per, nval = o.smaj ? nsb * per : ntot;
+        double2 vv[UO];
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int i = u * NT + (int)threadIdx.x;
+            if (u < OU && i < ntot) vv[u] = stg[otab[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int i = u * NT + (int)threadIdx.x;
+            if (u < OU && i < nval) {
+                size_t d;
+                if (o.smaj) {
+                    d = (size_t)s0 * per + i;
+                } else {
+                    const int j = i % SPB, r = i / SPB;   // (SPB a power of two)
+                    if (j >= nsb) continue;
+                    d = (size_t)r * B + s0 + j;
+                }
+                if (o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + d);
+                if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + d);
+            }
+        }
+    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj) {
+        // scenario-major layout: the tile's V is one contiguous [nsb][3][Nn] block
+        const int per = 3 * nn, total = nsb * per;
+        // element i: scenario j = i / per, (phase p, node k) of i % per, walked NT apart
+        int j = (int)threadIdx.x / per;
+        RowWalk w;
+        w.init((int)threadIdx.x - j * per, NT, nn);
+        while (w.fq >= 3) { w.fq -= 3; ++j; }
+        for (int i = threadIdx.x; i < total; i += NT) {
+            const int p = w.fq, k = w.rr;
+            const double2 vv = k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + swz_row(k - 1) * SROW + j];
+            if (o.v_re) __builtin_nontemporal_store(vv.x, o.v_re + (size_t)s0 * per + i);
+            if (o.v_im) __builtin_nontemporal_store(vv.y, o.v_im + (size_t)s0 * per + i);
+            w.next();
+            while (w.fq >= 3) { w.fq -= 3; ++j; }
+        }
+    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
+        constexpr int UV = 4;
+        static_assert(NT % SPB == 0, "a thread keeps its scenario");
+        const int total = 3 * nn * SPB;
+        // element i: scenario j = i % SPB (the same for all of a thread's
+        // elements), (phase, node) of i / SPB walked NT / SPB apart
+        RowWalk w;
+        w.init((int)threadIdx.x / SPB, NT / SPB, nn);
+        for (int i0 = 0; i0 < total; i0 += UV * NT) {
+            double2 vv[UV];
+#pragma unroll
+            for (int u = 0; u < UV; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                const int j = (int)threadIdx.x % SPB, p = w.fq, k = w.rr;
+                vv[u] = i >= total ? make_double2(0.0, 0.0)
+                                   : (k == 0 ? reg0[j * RS + 3 * XC + noff + p] : stg[p * PSTR + swz_row(k - 1) * SROW + j]);
+                w.next();
+            }
+#pragma unroll
+            for (int u = 0; u < UV; ++u) {
+                const int i = i0 + u * NT + (int)threadIdx.x;
+                const int j = i % SPB, r = i / SPB;   // r = p*nn + k
+                if (DBG(32768)) {   // ablation: contiguous [B][3 nn] re / im planes (scenario-major emulation)
+                    if (i < total && o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + (size_t)s0 * 3 * nn + i);
+                    if (i < total && o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + (size_t)s0 * 3 * nn + i);
+                } else if (i < total && j < nsb) {
+                    if (o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + (size_t)r * B + s0 + j);
+                    if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + (size_t)r * B + s0 + j);
+                }
+            }
+        }
+    }
+    WSTAMP(121);
+    if (agg) {
+        __syncthreads();
+        if (last_wg) {
+            // thread i folds workgroups i, i + NT, ... in order, then a fixed tree
+            double a[8] = {0, INFINITY, -INFINITY, 0, 0, 0, 0, 0};
+            for (unsigned b = threadIdx.x; b < gridDim.x; b += NT) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const double r = __hip_atomic_load(o.partials + 8 * (size_t)b + q, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                    a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
+                }
+            }
+            double *sh = (double *)stg;   // [8][NT] (STG and the regions are dead)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sh[q * NT + threadIdx.x] = a[q];
+            __syncthreads();
+            for (int w = NT / 2; w > 0; w >>= 1) {
+                if ((int)threadIdx.x < w) {
+                    const int t = threadIdx.x;
+                    sh[0 * NT + t] += sh[0 * NT + t + w];
+                    sh[1 * NT + t] = fmin(sh[1 * NT + t], sh[1 * NT + t + w]);
+                    sh[2 * NT + t] = fmax(sh[2 * NT + t], sh[2 * NT + t + w]);
+#pragma unroll
+                    for (int q = 3; q < 8; ++q) sh[q * NT + t] += sh[q * NT + t + w];
+                }
+                __syncthreads();
+            }
+            if (threadIdx.x < 8) o.agg[threadIdx.x] = sh[threadIdx.x * NT];
+            if (threadIdx.x == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // (every workgroup's flags were appended before its ticket)
+            if (threadIdx.x == 0 && o.flag_out)
+                *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (o.check && threadIdx.x == 0) {
+        // the multi-area solve's stop test (OutDev::check): the last workgroup to
+        // finish (every workgroup has passed the skip test by then)
+        const unsigned t = __hip_atomic_fetch_add(o.check_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            areas_stop_test(*o.check, (int32_t *)o.skip);
+            __hip_atomic_store(o.check_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (o.fix_dev) {
+        // the guard's local mode (a solve without an aggregate): the scenarios this
+        // workgroup flagged are re-solved on the exact body by its first wave, state
+        // in the (now dead) LDS, after every store of the fast results has landed
+        // (the exact body gets an LDS copy of the output pointers: taking the kernel
+        // argument's address would put the whole OutDev in scratch memory and turn
+        // every o.* read of the sweep loop into a scratch load)
+        __shared__ OutDev osh;
+        __syncthreads();
+        if (fix_n > 0) {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == 0) osh = o;
+            __syncthreads();
+            if (wv == 0) g3::g3_fixup_local(o.fix_dev, B, pq, (double *)lds, &osh, fix_ids, fix_n);
+        }
+    }
+}
+
+}  // namespace fpf

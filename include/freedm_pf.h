@@ -97,7 +97,9 @@ typedef struct fpf_opts {
     double ub_v;       /* 1.05  load_system_data.cpp:24                    */
     int    tile;       /* scenarios per workgroup for the tiled kernel, 0 = auto */
     int    specialize; /* 1 (default): compile the tiled kernel for the feeder's topology
-                          with hipRTC at fpf_feeder_create; 0: interpret its programs */
+                          with hipRTC at fpf_feeder_create, and the wave kernel for its
+                          plan at its first launch of >= 2048 scenarios (identical
+                          results); 0: interpret the tiled programs, static wave kernel */
     int    exact;      /* 1: the specialised kernel repeats the reference's roundings
                           (complex divide as libgcc __divdc3, no FMA): V, PQb, PQL, loss
                           bit-identical to the oracle.  0 (default): load currents as
@@ -292,6 +294,19 @@ int         fpf_areas_solve(fpf_areas *a, int n_scen, const double *pq, double t
 long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
                                   const double *z, int z_rows, int z_cols,
                                   const fpf_opts *opts, char *buf, size_t buf_size);
+
+/* Diagnostics (no device needed): the hipRTC source of the wave kernel built for
+ * this feeder's plan (its uniform values as constants; launches of >= 2048
+ * scenarios run it when opts->specialize, the static kernel otherwise).
+ * big_batch: the large-batch workgroup size; full: the full-output variant.
+ * Returns as fpf_feeder_rtc_source; FPF_ERR_UNSUPPORTED if the feeder does not
+ * run the per-wavefront wave kernel. */
+long        fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols,
+                                       const double *z, int z_rows, int z_cols,
+                                       const fpf_opts *opts, int big_batch, int full,
+                                       char *buf, size_t buf_size);
+/* Diagnostics: the per-plan wave kernels built with hipRTC so far in this process. */
+int         fpf_wave_rtc_builds(void);
 
 /* Diagnostics (no device needed): the wave kernel's plan for this feeder.
  * out[0..7] = {accepted (1/0), scenarios per wavefront, slots per lane,

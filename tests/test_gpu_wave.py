@@ -123,3 +123,57 @@ def test_light_outputs_match_full():
     for k, h in (("v_re", "V_re"), ("v_im", "V_im"), ("iters", "iters"), ("loss", "loss"), ("vmin", "vmin"),
                  ("vmax", "vmax")):
         np.testing.assert_array_equal(out[k].cpu().numpy(), full[h], err_msg=k)
+
+
+def _zeroed_feeder():
+    f = F.demo_feeder()
+    Z = np.vstack([f.Z, np.diag([0, 2.0 + 6.0j, 0])])
+    Dl = f.Dl.copy()
+    Dl[6, 3] = 3
+    Dl[7:9, [6, 7, 10, 11]] = 0
+    return F.Feeder(Dl, Z, name="demo-rel")
+
+
+@pytest.mark.parametrize("which", ["123", "123-1,4", "30", "nested", "zeroed"])
+def test_specialised_build_matches_static(which, monkeypatch):
+    """fpf_opts.specialize (default): a wave launch of >= 2048 scenarios runs the
+    per-plan hipRTC build (fpf_rtc.cpp: wave_rtc_function) -- the same source with
+    the plan's values as constants, so every output is the static kernel's bit
+    for bit (full outputs and the light variant the benchmark runs), and both
+    are the oracle's at the north-star bar."""
+    import ctypes as C
+    import torch
+    from freedm_amd import PowerFlow, _lib
+    if which == "123-1,4":
+        monkeypatch.setenv("FPF_WAVE_GEOM", "1,4")
+    f = {"123": lambda: F.synthetic_feeder(123, 123), "123-1,4": lambda: F.synthetic_feeder(123, 123),
+         "30": lambda: F.synthetic_feeder(30, 30), "nested": nested_feeder, "zeroed": _zeroed_feeder}[which]()
+    B = 2304
+    pq = F.scenario_loads(f, np.arange(B))
+    L = _lib.load()
+    L.fpf_wave_rtc_builds.restype = C.c_int
+    n0 = L.fpf_wave_rtc_builds()
+    spec = PowerFlow(f, kernel="wave")
+    stat = PowerFlow(f, kernel="wave", specialize=False)
+    a, b = spec.solve(pq), stat.solve(pq)
+    n1 = L.fpf_wave_rtc_builds()
+    assert n1 >= n0 + 1 or n0 > 0   # (built here, or by an earlier test of the same plan)
+    for k in a:
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    dev = torch.device("cuda:0")
+    res = []
+    for pf in (spec, stat):
+        out = {"v_re": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
+               "v_im": torch.zeros((3, pf.nn, B), dtype=torch.float64, device=dev),
+               "iters": torch.zeros(B, dtype=torch.int32, device=dev),
+               "status": torch.zeros(B, dtype=torch.int8, device=dev),
+               "loss": torch.zeros(B, dtype=torch.float64, device=dev),
+               "vmin": torch.zeros(B, dtype=torch.float64, device=dev),
+               "vmax": torch.zeros(B, dtype=torch.float64, device=dev)}
+        pf.solve_device(torch.from_numpy(pq).to(dev), out)
+        torch.cuda.synchronize()
+        res.append({k: v.cpu().numpy() for k, v in out.items()})
+    for k in res[0]:
+        np.testing.assert_array_equal(res[0][k], res[1][k], err_msg="light " + k)
+    # and the oracle, on a slice
+    _check(f, pq[:, :, :64])

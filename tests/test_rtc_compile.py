@@ -47,3 +47,47 @@ def test_rtc_source_compiles(nn, tracks, monkeypatch):
     assert n.value > 1000
     R.hiprtcDestroyProgram(C.byref(prog))
     assert time.time() - t0 < 120
+
+
+def _compile(src, name, extra=()):
+    R = _hiprtc()
+    prog = C.c_void_p()
+    assert R.hiprtcCreateProgram(C.byref(prog), src.encode(), b"fpf_rtc_wave.hip", 0, None, None) == 0
+    assert R.hiprtcAddNameExpression(prog, name.encode()) == 0
+    o = OPTS + list(extra)
+    opts = (C.c_char_p * len(o))(*o)
+    rc = R.hiprtcCompileProgram(prog, len(o), opts)
+    n = C.c_size_t()
+    R.hiprtcGetProgramLogSize(prog, C.byref(n))
+    log = C.create_string_buffer(n.value + 1)
+    R.hiprtcGetProgramLog(prog, log)
+    assert rc == 0, log.value.decode(errors="replace")[-4000:]
+    low = C.c_char_p()
+    R.hiprtcGetLoweredName.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p)]
+    assert R.hiprtcGetLoweredName(prog, name.encode(), C.byref(low)) == 0
+    lowered = low.value.decode()
+    R.hiprtcGetCodeSize(prog, C.byref(n))
+    assert n.value > 1000
+    R.hiprtcDestroyProgram(C.byref(prog))
+    return lowered
+
+
+@pytest.mark.parametrize("nn,big,full", [(9, 1, 0), (60, 0, 1), (123, 1, 0)])
+def test_wave_rtc_source_compiles(nn, big, full):
+    """The per-plan wave kernel (fpf_rtc.cpp: wave_rtc_source, fpf_wave_body.h
+    under FPF_WSPEC) compiles with the static build's flags; its plan constants
+    are the ones fpf_feeder_wave_plan reports."""
+    from wave_rtc_dump import wave_rtc_source
+    from freedm_amd import demo_feeder, synthetic_feeder
+    from test_wave_plan import _plan
+    f = demo_feeder() if nn == 9 else synthetic_feeder(nn, nn)
+    src = wave_rtc_source(f, big, full)
+    plan = _plan(f)
+    assert f"#define FPF_WSPEC_NCOMP {plan['ncomp']}\n" in src
+    assert f"#define FPF_WSPEC_NBLK {plan['nblk']}\n" in src
+    assert f"#define FPF_WSPEC_NN {nn}\n" in src
+    tail = src.rsplit("template __global__ void ", 1)[1]
+    name = tail.split("(")[0]
+    assert name.startswith(f"fpf::dpf_wave_kernel<{plan['spw']}, {plan['C']}, {'true' if full else 'false'},")
+    lowered = _compile(src, name, [b"-mllvm", b"-amdgpu-sched-strategy=iterative-ilp"])
+    assert lowered.startswith("_ZN3fpf15dpf_wave_kernelI")
