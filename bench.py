@@ -569,6 +569,16 @@ def launch_ranks(n: int, argv: list) -> int:
     return rc
 
 
+def _wave_rtc_builds():
+    """per-plan hipRTC wave kernels built in this process (fpf_opts.specialize:
+    the wave launches of >= 2048 scenarios run them, fpf_rtc.cpp)"""
+    import ctypes
+    from freedm_amd import _lib
+    L = _lib.load()
+    L.fpf_wave_rtc_builds.restype = ctypes.c_int
+    return int(L.fpf_wave_rtc_builds())
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] == "--multi-leg":   # (bench.py's own child, _multi_leg_child)
         print(json.dumps(multi_leg(int(sys.argv[2]))), flush=True)
@@ -752,7 +762,8 @@ def main():
             "config": {"workload": f"BASELINE config {args.config}: {n_nodes}-bus feeder, {B} scenarios per GPU per step",
                        "feeder": feeder.name, "scenarios_per_gpu": B, "kernel": pf.kernel,
                        "input_batches": n_in, "input_mib": n_in * batch_bytes / 2 ** 20,
-                       "tile": pf.info["tile"], "specialized": pf.info["specialized"], "exact": bool(args.exact),
+                       "tile": pf.info["tile"], "specialized": pf.info["specialized"],
+                       "wave_rtc_builds": _wave_rtc_builds(), "exact": bool(args.exact),
                        "layout": ["[6][Nl][B] scenario fastest", "[B][6][Nl] scenario major"][layout],
                        "parallelism": f"scenario shards x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

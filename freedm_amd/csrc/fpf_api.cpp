@@ -2216,7 +2216,7 @@ extern "C" long fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols, 
     analyse_tiled(h);
     WaveHost wh;
     analyse_wave(h, wh);
-    if (!wh.ok || wh.wps || wh.coop) return FPF_ERR_UNSUPPORTED;
+    if (!wh.ok || wh.coop) return FPF_ERR_UNSUPPORTED;
     // the plan values fpf_feeder_create puts in the launch's WaveDev
     WaveDev w{};
     w.nn = h.nn;
@@ -2232,9 +2232,13 @@ extern "C" long fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols, 
     w.off_in_x = wh.off_in_x;
     w.temp_sym = wh.temp_sym;
     w.mxitr = o.mxitr;
-    std::vector<int32_t> a, b;
-    w.stage_u = wave_stage_tables(w, a, b);
-    w.out_u = wave_out_tables(w, a, b);
+    w.wps = wh.wps;
+    w.ncode = h.ncode;
+    if (!w.wps) {
+        std::vector<int32_t> a, b;
+        w.stage_u = wave_stage_tables(w, a, b);
+        w.out_u = wave_out_tables(w, a, b);
+    }
     std::string name;
     const std::string src = wave_rtc_source(w, full != 0, &name);
     if (buf && buf_size > 0) {

@@ -441,10 +441,13 @@ int rtc_build(int device, const RtcSpec &spec, RtcKernel *out, std::string *err)
 void rtc_release(const RtcKernel &k);   // drop one reference; the last unloads the code object
 hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const double *pq, const OutDev &o,
                       hipStream_t st);
-// the wave kernel compiled for one plan (its uniform values as constants,
-// fpf_wave_body.h: FPF_WSPEC) and variant; built on first use, kept for the
+// the wave kernel (w.wps: the wave-block kernel) compiled for one plan (its
+// uniform values as constants, fpf_wave_body.h / fpf_wblk_body.h: FPF_WSPEC) and
+// variant; built on first use, kept for the
 // process.  NULL if the build failed (the static kernel runs)
 hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full);
+// the smallest launch that runs it (FPF_WAVE_RTC: 0 never, 1 always, n; default 2048)
+int wave_rtc_min();
 std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name);
 #endif
 

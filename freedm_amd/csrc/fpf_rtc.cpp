@@ -316,7 +316,8 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
     return 0;
 }
 
-// ---- the wave kernel per plan (fpf_wave_body.h, FPF_WSPEC): the same source as
+// ---- the wave kernel (fpf_wave_body.h) and the wave-block kernel
+// (fpf_wblk_body.h) per plan, FPF_WSPEC: the same source as
 // the static build with the plan's uniform values defined as constants, so the
 // arithmetic -- and every result -- is the static kernel's.  Measured -4 to -5 %
 // kernel time on the 123-bus feeder (profiles/r04sp, r04rtc).
@@ -329,12 +330,28 @@ std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
       << "\n#define FPF_WSPEC_STAGE_U " << w.stage_u << "\n#define FPF_WSPEC_OUT_U " << w.out_u
       << "\n#define FPF_WSPEC_HAS_MASK " << w.has_mask << "\n#define FPF_WSPEC_HAS_REL " << w.has_rel
       << "\n#define FPF_WSPEC_MXITR " << w.mxitr << "\n";
-    for (const char *part : kRtcWaveSources) s << part;
     char nm[96];
-    snprintf(nm, sizeof nm, "fpf::dpf_wave_kernel<%d, %d, %s, %d>", w.spw, w.C, full ? "true" : "false", w.wpb);
+    if (w.wps) {   // the wave-block kernel (fpf_wblk_body.h); full: its FULL variant
+        s << "#define FPF_WSPEC_NCODE " << w.ncode << "\n";
+        for (const char *part : kRtcWblkSources) s << part;
+        snprintf(nm, sizeof nm, "fpf::dpf_wblk_kernel<%d, %s, %d, %s>", w.wps, full || w.has_rel ? "true" : "false", w.C,
+                 w.has_rel ? "true" : "false");
+    } else {
+        for (const char *part : kRtcWaveSources) s << part;
+        snprintf(nm, sizeof nm, "fpf::dpf_wave_kernel<%d, %d, %s, %d>", w.spw, w.C, full ? "true" : "false", w.wpb);
+    }
     s << "\ntemplate __global__ void " << nm << "(fpf::WaveDev, int, const double *, fpf::OutDev);\n";
     *name = nm;
     return s.str();
+}
+
+int wave_rtc_min() {
+    static const int v = [] {
+        const char *e = getenv("FPF_WAVE_RTC");
+        if (e && *e) return atoi(e) == 0 ? INT32_MAX : (atoi(e) == 1 ? 1 : atoi(e));
+        return 2048;
+    }();
+    return v;
 }
 
 int g_wave_rtc_builds = 0;   // successful builds in this process (fpf_wave_rtc_builds)
@@ -349,10 +366,13 @@ hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
     if (it != built.end()) return it->second;
     RtcKernel k{};
     std::string err;
-    // the static build's ILP-first scheduler (Makefile: fpf_wave.o)
     hipFunction_t fn = nullptr;
-    if (compile_load(src, "fpf_rtc_wave.hip", nullptr, name.c_str(),
-                     {"-mllvm", "-amdgpu-sched-strategy=iterative-ilp"}, &k, &err) == 0) {
+    // the static build's ILP-first scheduler (Makefile: fpf_wave.o / fpf_wblk.o);
+    // FPF_WAVE_RTC_SCHED / FPF_WBLK_RTC_SCHED = 0: the default one (experiments)
+    const char *se = getenv(w.wps ? "FPF_WBLK_RTC_SCHED" : "FPF_WAVE_RTC_SCHED");
+    std::vector<const char *> opts;
+    if (!(se && atoi(se) == 0)) opts = {"-mllvm", "-amdgpu-sched-strategy=iterative-ilp"};
+    if (compile_load(src, "fpf_rtc_wave.hip", nullptr, name.c_str(), opts, &k, &err) == 0) {
         int stat = 0;
         if (hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.fn) == hipSuccess &&
             hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - stat) ==

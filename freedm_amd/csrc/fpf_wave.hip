@@ -112,15 +112,6 @@ bool wave_wpb_supported(int spw, int c, int wpb) {
 }
 
 namespace {
-// the smallest launch that runs the hipRTC build (FPF_WAVE_RTC: 0 never, 1 always)
-int wave_rtc_min() {
-    static const int v = [] {
-        const char *e = getenv("FPF_WAVE_RTC");
-        if (e && *e) return atoi(e) == 0 ? INT32_MAX : (atoi(e) == 1 ? 1 : atoi(e));
-        return 2048;
-    }();
-    return v;
-}
 typedef void (*WaveKernel)(WaveDev, int, const double *, OutDev);
 template <int SPW, int C>
 WaveKernel pick(bool full, int wpb) {

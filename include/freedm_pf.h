@@ -299,8 +299,8 @@ long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
  * this feeder's plan (its uniform values as constants; launches of >= 2048
  * scenarios run it when opts->specialize, the static kernel otherwise).
  * big_batch: the large-batch workgroup size; full: the full-output variant.
- * Returns as fpf_feeder_rtc_source; FPF_ERR_UNSUPPORTED if the feeder does not
- * run the per-wavefront wave kernel. */
+ * Feeders of 257..2048 branches: the wave-block kernel's build.  Returns as
+ * fpf_feeder_rtc_source; FPF_ERR_UNSUPPORTED if the feeder runs neither. */
 long        fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols,
                                        const double *z, int z_rows, int z_cols,
                                        const fpf_opts *opts, int big_batch, int full,

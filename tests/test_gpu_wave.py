@@ -157,7 +157,7 @@ def test_specialised_build_matches_static(which, monkeypatch):
     stat = PowerFlow(f, kernel="wave", specialize=False)
     a, b = spec.solve(pq), stat.solve(pq)
     n1 = L.fpf_wave_rtc_builds()
-    assert n1 >= n0 + 1 or n0 > 0   # (built here, or by an earlier test of the same plan)
+    assert n1 >= 1 and n1 >= n0   # (built here or by an earlier test of the same plan)
     for k in a:
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
     dev = torch.device("cuda:0")

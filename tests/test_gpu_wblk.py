@@ -280,3 +280,33 @@ def test_wblk_heavy_2048_bus():
         np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
         np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-8)
         pf.close()
+
+
+@pytest.mark.parametrize("which", ["300", "1100", "masked", "restart"])
+def test_wblk_specialised_build_matches_static(which):
+    """fpf_opts.specialize (default): a wave-block launch of >= 2048 scenarios runs
+    the per-plan hipRTC build (fpf_rtc.cpp: wave_rtc_function, fpf_wblk_body.h
+    under FPF_WSPEC) -- every output bit for bit the static kernel's, full
+    outputs, zeroed phases and the segmented restart included; the oracle on a
+    slice."""
+    import ctypes as C
+    from freedm_amd import PowerFlow, _lib
+    from oracle import oracle as O
+    f = {"300": lambda: F.synthetic_feeder(300, 300), "1100": lambda: F.synthetic_feeder(1100, 1100),
+         "masked": lambda: _masked_feeder(), "restart": lambda: _masked_feeder(restart=True)}[which]()
+    B = 2048
+    pq = F.scenario_loads(f, np.arange(B))
+    L = _lib.load()
+    L.fpf_wave_rtc_builds.restype = C.c_int
+    n0 = L.fpf_wave_rtc_builds()
+    spec, stat = PowerFlow(f), PowerFlow(f, specialize=False)
+    assert spec.kernel == "wave" and spec.info["tile"] == 1
+    a, b = spec.solve(pq), stat.solve(pq)
+    assert L.fpf_wave_rtc_builds() >= max(n0, 1)   # (here or by an earlier test of the same plan)
+    for k in a:
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    c = O.dpf_batch(f.Dl, f.Z, pq[:, :, :24], nthreads=8)
+    conv = c["status"] == 0
+    assert (a["iters"][:24] == c["iters"]).all()
+    assert _vrel(a["V_re"][..., :24][..., conv], a["V_im"][..., :24][..., conv], c["V_re"][..., conv],
+                 c["V_im"][..., conv]) <= 1e-10
