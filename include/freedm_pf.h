@@ -192,7 +192,9 @@ int         fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int ncols,
                               const fpf_opts *opts, fpf_feeder **out);
 void        fpf_feeder_destroy(fpf_feeder *feeder);
 int         fpf_feeder_get_info(const fpf_feeder *feeder, fpf_feeder_info *info);
-/* Pre-size device scratch for batches up to max_scen (no allocation later). */
+/* Pre-size device scratch for batches up to max_scen (no allocation later); with
+ * opts.specialize, also build the wave kernel those batches run (hipRTC, once
+ * per plan in a process) so that no solve pays for the compile. */
 int         fpf_feeder_reserve(fpf_feeder *feeder, int max_scen);
 
 /* Host-memory batch: copies in, solves, copies out; blocks.  agg may be NULL. */

@@ -91,3 +91,15 @@ def test_wave_rtc_source_compiles(nn, big, full):
     assert name.startswith(f"fpf::dpf_wave_kernel<{plan['spw']}, {plan['C']}, {'true' if full else 'false'},")
     lowered = _compile(src, name, [b"-mllvm", b"-amdgpu-sched-strategy=iterative-ilp"])
     assert lowered.startswith("_ZN3fpf15dpf_wave_kernelI")
+
+
+@pytest.mark.parametrize("nn", [700, 2048])
+def test_wblk_rtc_source_compiles(nn):
+    """The per-plan wave-block kernel (fpf_wblk_body.h under FPF_WSPEC) compiles."""
+    from wave_rtc_dump import wave_rtc_source
+    from freedm_amd import synthetic_feeder
+    src = wave_rtc_source(synthetic_feeder(nn, nn), 1, 0)
+    assert f"#define FPF_WSPEC_NN {nn}\n" in src and "#define FPF_WSPEC_NCODE " in src
+    name = src.rsplit("template __global__ void ", 1)[1].split("(")[0]
+    assert name.startswith("fpf::dpf_wblk_kernel<")
+    assert _compile(src, name, [b"-mllvm", b"-amdgpu-sched-strategy=iterative-ilp"]).startswith("_ZN3fpf15dpf_wblk_kernelI")
