@@ -345,13 +345,12 @@ std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
     return s.str();
 }
 
+// (read per call: tests switch it)
+constexpr int WAVE_RTC_DEFAULT_MIN = INT32_MAX;
 int wave_rtc_min() {
-    static const int v = [] {
-        const char *e = getenv("FPF_WAVE_RTC");
-        if (e && *e) return atoi(e) == 0 ? INT32_MAX : (atoi(e) == 1 ? 1 : atoi(e));
-        return 2048;
-    }();
-    return v;
+    const char *e = getenv("FPF_WAVE_RTC");
+    if (e && *e) return atoi(e) == 0 ? INT32_MAX : (atoi(e) == 1 ? 1 : atoi(e));
+    return WAVE_RTC_DEFAULT_MIN;
 }
 
 int g_wave_rtc_builds = 0;   // successful builds in this process (fpf_wave_rtc_builds)

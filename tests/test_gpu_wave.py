@@ -144,6 +144,7 @@ def test_specialised_build_matches_static(which, monkeypatch):
     import ctypes as C
     import torch
     from freedm_amd import PowerFlow, _lib
+    monkeypatch.setenv("FPF_WAVE_RTC", "2048")
     if which == "123-1,4":
         monkeypatch.setenv("FPF_WAVE_GEOM", "1,4")
     f = {"123": lambda: F.synthetic_feeder(123, 123), "123-1,4": lambda: F.synthetic_feeder(123, 123),

@@ -283,7 +283,7 @@ def test_wblk_heavy_2048_bus():
 
 
 @pytest.mark.parametrize("which", ["300", "1100", "masked", "restart"])
-def test_wblk_specialised_build_matches_static(which):
+def test_wblk_specialised_build_matches_static(which, monkeypatch):
     """fpf_opts.specialize (default): a wave-block launch of >= 2048 scenarios runs
     the per-plan hipRTC build (fpf_rtc.cpp: wave_rtc_function, fpf_wblk_body.h
     under FPF_WSPEC) -- every output bit for bit the static kernel's, full
@@ -292,6 +292,7 @@ def test_wblk_specialised_build_matches_static(which):
     import ctypes as C
     from freedm_amd import PowerFlow, _lib
     from oracle import oracle as O
+    monkeypatch.setenv("FPF_WAVE_RTC", "2048")
     f = {"300": lambda: F.synthetic_feeder(300, 300), "1100": lambda: F.synthetic_feeder(1100, 1100),
          "masked": lambda: _masked_feeder(), "restart": lambda: _masked_feeder(restart=True)}[which]()
     B = 2048

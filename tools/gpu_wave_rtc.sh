@@ -6,6 +6,7 @@ set -o pipefail
 P=${P:-r04rtc}
 mkdir -p gpurun_out/$P
 export TMPDIR=/tmp
+export FPF_WAVE_RTC=${FPF_WAVE_RTC:-2048}
 timeout -k 10 500 python3 -u -m pytest tests/test_gpu_wave.py tests/test_gpu_wblk.py tests/test_rtc_compile.py -x -v --timeout 150 --timeout-method thread > gpurun_out/$P/pytest.log 2>&1 || { echo "TESTS FAILED"; tail -30 gpurun_out/$P/pytest.log; exit 1; }
 tail -2 gpurun_out/$P/pytest.log
 summ() { python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; r4=d.get("roofline_config4"); a=d.get("config5_areas"); print("kernel_ms %.5f frac %.4f rtc %s" % (r["kernel_ms"], r["frac"], d["config"].get("wave_rtc_builds")), ("| c4 kernel_ms %.4f frac %.4f | c5 %.3fx" % (r4["kernel_ms"], r4["frac"], a["vs_monolithic"])) if r4 else "")'; }
