@@ -264,7 +264,7 @@ int compile_load(const std::string &src, const char *file, const char *fname, co
         hiprtcDestroyProgram(&prog);
         return -1;
     }
-    std::string lowered = fname;
+    std::string lowered = fname ? fname : "";
     if (name_expr) {
         const char *low = nullptr;
         if (hiprtcGetLoweredName(prog, name_expr, &low) != HIPRTC_SUCCESS || !low) {

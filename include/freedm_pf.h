@@ -97,9 +97,10 @@ typedef struct fpf_opts {
     double ub_v;       /* 1.05  load_system_data.cpp:24                    */
     int    tile;       /* scenarios per workgroup for the tiled kernel, 0 = auto */
     int    specialize; /* 1 (default): compile the tiled kernel for the feeder's topology
-                          with hipRTC at fpf_feeder_create, and the wave kernel for its
-                          plan at its first launch of >= 2048 scenarios (identical
-                          results); 0: interpret the tiled programs, static wave kernel */
+                          with hipRTC at fpf_feeder_create (and, with FPF_WAVE_RTC=n set,
+                          the wave kernel for its plan, run by launches of >= n
+                          scenarios; identical results); 0: interpret the tiled
+                          programs, static wave kernel */
     int    exact;      /* 1: the specialised kernel repeats the reference's roundings
                           (complex divide as libgcc __divdc3, no FMA): V, PQb, PQL, loss
                           bit-identical to the oracle.  0 (default): load currents as
@@ -193,8 +194,8 @@ int         fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int ncols,
 void        fpf_feeder_destroy(fpf_feeder *feeder);
 int         fpf_feeder_get_info(const fpf_feeder *feeder, fpf_feeder_info *info);
 /* Pre-size device scratch for batches up to max_scen (no allocation later); with
- * opts.specialize, also build the wave kernel those batches run (hipRTC, once
- * per plan in a process) so that no solve pays for the compile. */
+ * opts.specialize and FPF_WAVE_RTC, also build the wave kernel those batches run
+ * (hipRTC, once per plan in a process) so that no solve pays for the compile. */
 int         fpf_feeder_reserve(fpf_feeder *feeder, int max_scen);
 
 /* Host-memory batch: copies in, solves, copies out; blocks.  agg may be NULL. */
@@ -298,8 +299,8 @@ long        fpf_feeder_rtc_source(const double *dl, int nl, int ncols,
                                   const fpf_opts *opts, char *buf, size_t buf_size);
 
 /* Diagnostics (no device needed): the hipRTC source of the wave kernel built for
- * this feeder's plan (its uniform values as constants; launches of >= 2048
- * scenarios run it when opts->specialize, the static kernel otherwise).
+ * this feeder's plan (its uniform values as constants; run by launches of >= n
+ * scenarios when opts->specialize and FPF_WAVE_RTC=n, the static kernel otherwise).
  * big_batch: the large-batch workgroup size; full: the full-output variant.
  * Feeders of 257..2048 branches: the wave-block kernel's build.  Returns as
  * fpf_feeder_rtc_source; FPF_ERR_UNSUPPORTED if the feeder runs neither. */
