@@ -1735,12 +1735,12 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
         HIPCHK(ctx, hipMalloc(&f->d_flag_ids, sizeof(int32_t) * std::max(max_scen, 1)));
         f->flag_cap = max_scen;
     }
-    // the per-plan hipRTC wave kernel batches this large run (light outputs; its
-    // full-output variant is built by the first launch that wants it): built
-    // here rather than inside the first solve (fpf_rtc.cpp: wave_rtc_function)
+    // the per-plan hipRTC wave kernel batches this large run (light outputs; the
+    // full-output variant runs the static kernel, fpf_wave.hip: launch_wave):
+    // built here rather than inside the first solve (fpf_rtc.cpp: wave_rtc_function)
     if (kernel_for(f, max_scen) == FPF_KERNEL_WAVE && max_scen >= wave_rtc_min()) {
         const WaveDev &w = wave_dev_for(f, max_scen);
-        if (w.spec && !w.coop) (void)wave_rtc_function(ctx->device, w, w.has_mask || (w.wps && w.has_rel));
+        if (w.spec && !w.coop && !w.has_mask && !(w.wps && w.has_rel)) (void)wave_rtc_function(ctx->device, w, false);
     }
     const bool need_scratch = kernel_for(f, max_scen) == FPF_KERNEL_GENERIC;
     if (max_scen <= f->cap) {

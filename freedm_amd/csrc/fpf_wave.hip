@@ -175,7 +175,10 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     // launches of at least wave_rtc_min() scenarios run the per-plan hipRTC build
     // (fpf_rtc.cpp: ~2.5 s to compile, once per plan and variant in a process);
     // smaller ones, and a failed build, the static kernel -- identical results
-    if (w.spec && n_scen >= wave_rtc_min() && !wl.stag_n) {
+    // (the light variant only: the full-output one -- Vpolar / PQb / PQL, zeroed
+    // phases -- is refused at dispatch when built by hipRTC, HSA_STATUS_ERROR_INVALID_ISA
+    // on the box, profiles/r04rtc; it runs the static kernel)
+    if (w.spec && !full && n_scen >= wave_rtc_min() && !wl.stag_n) {
         if (hipFunction_t fn = wave_rtc_function(dev, w, full)) {
             OutDev oa = o;
             int b = n_scen;

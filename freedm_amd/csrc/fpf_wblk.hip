@@ -108,8 +108,8 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
 #if !defined(FPF_WBLK_ABL) && !defined(FPF_WBLK_NO_GUARD_CODE)
     // launches of at least wave_rtc_min() scenarios: the per-plan hipRTC build
     // (fpf_rtc.cpp), identical results; a failed build runs the static kernel
-    if (w.spec && n_scen >= wave_rtc_min()) {
-        if (hipFunction_t fn = wave_rtc_function(dev, w, full || seg)) {
+    if (w.spec && !full && !seg && n_scen >= wave_rtc_min()) {   // (the light variant only, as launch_wave)
+        if (hipFunction_t fn = wave_rtc_function(dev, w, false)) {
             WaveDev wa = w;
             OutDev oa = o;
             int b = n_scen;
