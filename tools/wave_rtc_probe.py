@@ -1,6 +1,7 @@
 """One specialised (hipRTC) wave launch against the static kernel on the GPU box:
-python tools/wave_rtc_probe.py <nodes> <full 0/1> -- light (solve_device) or
-full (solve) outputs; prints the max difference and the build count."""
+python tools/wave_rtc_probe.py <nodes> <full 0/1> [prefull] -- light
+(solve_device) or full (solve) outputs; prints whether they are identical and
+the build count."""
 import ctypes as C
 import os
 import sys
@@ -12,9 +13,13 @@ import torch  # noqa: E402
 from freedm_amd import PowerFlow, _lib, feeder as F  # noqa: E402
 
 n, full = int(sys.argv[1]), int(sys.argv[2])
+prefull = len(sys.argv) > 3 and sys.argv[3] == "prefull"   # a static full-output solve first
 f = F.synthetic_feeder(n, n)
 B = 4096
 pq = F.scenario_loads(f, np.arange(B))
+if prefull:
+    PowerFlow(f, kernel="wave", specialize=False).solve(pq)
+    print("static full-output solve done", flush=True)
 L = _lib.load()
 L.fpf_wave_rtc_builds.restype = C.c_int
 dev = torch.device("cuda:0")
