@@ -16,7 +16,9 @@ the default fast mode: all sweeps, V, per-scenario loss / Vmin / Vmax /
 iterations), inputs resident in HBM, per-scenario results kept for every
 step.  After the K timed steps the study aggregate over all K x 4096 results
 is reduced once on each GPU (deterministic) and combined across GPUs by one
-RCCL all-reduce (the only collective of the path), inside the timed region.
+RCCL all-gather folded in rank order (the only collective of the path and of
+the timed region: freedm_amd/dist.py timed_study); each rank reads its clock
+right after it, and the max over ranks is taken outside the region.
 value = converged scenarios of all ranks / max-over-ranks wall time.
 
 Also reported: the roofline of the dominant kernel (algorithmic bytes per
@@ -699,26 +701,27 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    ev1.record(stream)
-    t_submit = time.perf_counter() - t0
-    total = study_aggregate().clone()
-    # the one collective: combine the per-GPU study aggregates over RCCL/xGMI
-    D.combine_aggregates(total)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    t_submit = 0.0
+
+    def run_steps():
+        nonlocal t_submit
+        t = time.perf_counter()
+        ev0.record(stream)
+        for i in range(args.steps):
+            step(i)
+        ev1.record(stream)
+        t_submit = time.perf_counter() - t
+
+    # the timed region: the K solves, the study aggregate and the one collective
+    # (an all-gather of the per-GPU aggregates over RCCL/xGMI, folded in rank
+    # order); each rank reads its clock without a further barrier
+    elapsed, tot = D.timed_study(run_steps, study_aggregate, sync=lambda: torch.cuda.synchronize(dev))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     avg_kern_s = ev0.elapsed_time(ev1) / args.steps / 1e3
-    tot = total.cpu().numpy()
     n_conv_all = float(tot[3])
     value = n_conv_all / elapsed
     nb, nn = pf.info["nb"], pf.nn

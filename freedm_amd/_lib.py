@@ -27,7 +27,7 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_gradient_at", "fpf_vvc_round",
            "fpf_vvc_gradient_batch", "fpf_feeder_check", "fpf_vvc_round_batch", "fpf_feeder_wave_rtc_source",
-           "fpf_wave_rtc_builds"]
+           "fpf_wave_rtc_builds", "fpf_rtc_compile", "fpf_rtc_compiler"]
 
 
 class FpfOpts(C.Structure):
@@ -181,6 +181,11 @@ def load(path: str | None = None):
                                           C.c_double, C.c_double, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int),
                                           _dp, _dp, _dp, _dp, C.POINTER(C.c_int8)]
         L.fpf_vvc_round_batch.restype = C.c_int
+    if hasattr(L, "fpf_rtc_compile") or path == LIB_PATH:
+        L.fpf_rtc_compile.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
+        L.fpf_rtc_compile.restype = C.c_long
+        L.fpf_rtc_compiler.argtypes = []
+        L.fpf_rtc_compiler.restype = C.c_char_p
     for name in ("fpf_ctx_create", "fpf_feeder_create", "fpf_feeder_get_info", "fpf_feeder_reserve",
                  "fpf_solve_batch", "fpf_solve_batch_device", "fpf_aggregate_device", "fpf_feeder_check"):
         getattr(L, name).restype = C.c_int

@@ -12,9 +12,15 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <unistd.h>
+#include <elf.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <type_traits>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -239,46 +245,182 @@ std::string rtc_source(const RtcSpec &sp) {
 }
 
 namespace {
-// compile src for gfx950 and load it on the current device: the kernel fname,
-// or, given name_expr (a template instantiation), its lowered name
-int compile_load(const std::string &src, const char *file, const char *fname, const char *name_expr,
-                 std::vector<const char *> opts, RtcKernel *k, std::string *err) {
+// ---- which hipRTC compiles.  A process that imported PyTorch before this
+// library (the Python mirror, bench.py, the GPU tests) has PyTorch's bundled
+// HIP runtime, libhiprtc and libamd_comgr (ROCm 7.0) loaded under the same
+// sonames, so the linked hiprtc* symbols resolve to that older compiler.  It
+// builds the wave kernel with 32 AGPRs on top of the VGPRs the launch bounds
+// allow (264 registers for a 512-thread workgroup, i.e. 2 waves per SIMD x 264
+// > 512): the workgroup can never be resident, and the command processor
+// rejects the dispatch (EC_QUEUE_PACKET_DISPATCH_REGISTER_INVALID, reported as
+// HSA_STATUS_ERROR_INVALID_ISA -- profiles/r04rtc, profiles/r05rtc).  So the
+// image's own hipRTC (the compiler the static kernels were built with) is
+// loaded into a private link-map namespace (dlmopen), where its dlopen of
+// comgr finds the image's comgr next to it instead of the process's.  The
+// linked symbols remain the fallback; every build is checked for residency
+// (rtc_resident) either way.
+struct RtcApi {
+    decltype(&hiprtcCreateProgram) create;
+    decltype(&hiprtcAddNameExpression) add_name;
+    decltype(&hiprtcCompileProgram) compile;
+    decltype(&hiprtcGetProgramLogSize) log_size;
+    decltype(&hiprtcGetProgramLog) log;
+    decltype(&hiprtcGetLoweredName) lowered;
+    decltype(&hiprtcGetCodeSize) code_size;
+    decltype(&hiprtcGetCode) code;
+    decltype(&hiprtcDestroyProgram) destroy;
+    decltype(&hiprtcGetErrorString) errstr;
+    std::string where;   // the library the entry points came from
+    // the private namespace has its own libc, whose environ still points at the
+    // array the process had when it was loaded; a setenv since then may have
+    // freed that array (comgr reads its environment on every compile), so it is
+    // pointed at the process's current one before each compile (sync_env)
+    char ***ns_environ = nullptr;
+    void sync_env() const {
+        if (ns_environ) *ns_environ = environ;
+    }
+};
+
+const RtcApi &rtc_api() {
+    static const RtcApi api = [] {
+        RtcApi a{&hiprtcCreateProgram, &hiprtcAddNameExpression, &hiprtcCompileProgram, &hiprtcGetProgramLogSize,
+                 &hiprtcGetProgramLog, &hiprtcGetLoweredName, &hiprtcGetCodeSize, &hiprtcGetCode,
+                 &hiprtcDestroyProgram, &hiprtcGetErrorString, "linked"};
+        std::vector<std::string> cands;
+        if (const char *e = getenv("FPF_HIPRTC_LIB")) {
+            if (!*e || !strcmp(e, "linked")) return a;   // (diagnostics: the process's own hiprtc)
+            cands.push_back(e);
+        }
+        if (const char *r = getenv("ROCM_PATH")) cands.push_back(std::string(r) + "/lib/libhiprtc.so");
+        cands.push_back("/opt/rocm/lib/libhiprtc.so");
+        for (const std::string &p : cands) {
+            void *h = dlmopen(LM_ID_NEWLM, p.c_str(), RTLD_NOW | RTLD_LOCAL);
+            if (!h) continue;
+            RtcApi b = a;
+            bool ok = true;
+            auto get = [&](auto &fn, const char *sym) {
+                void *s = dlsym(h, sym);
+                if (!s) ok = false;
+                else fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(s);
+            };
+            get(b.create, "hiprtcCreateProgram");
+            get(b.add_name, "hiprtcAddNameExpression");
+            get(b.compile, "hiprtcCompileProgram");
+            get(b.log_size, "hiprtcGetProgramLogSize");
+            get(b.log, "hiprtcGetProgramLog");
+            get(b.lowered, "hiprtcGetLoweredName");
+            get(b.code_size, "hiprtcGetCodeSize");
+            get(b.code, "hiprtcGetCode");
+            get(b.destroy, "hiprtcDestroyProgram");
+            get(b.errstr, "hiprtcGetErrorString");
+            b.ns_environ = static_cast<char ***>(dlsym(h, "environ"));
+            if (!b.ns_environ) ok = false;
+            if (ok) {
+                b.where = p;
+                return b;
+            }
+            dlclose(h);
+        }
+        return a;
+    }();
+    return api;
+}
+
+// the compiled code object's kernel descriptor (AMDHSA ABI): registers per
+// lane (VGPRs + AGPRs, COMPUTE_PGM_RSRC1 granule 8 on gfx950) and the fixed
+// private segment; false if the object has no such kernel
+bool co_kernel_desc(const std::string &co, const std::string &kname, int *regs, int *scratch) {
+    const auto *eh = reinterpret_cast<const Elf64_Ehdr *>(co.data());
+    if (co.size() < sizeof(Elf64_Ehdr) || memcmp(eh->e_ident, ELFMAG, SELFMAG) || eh->e_shoff + (size_t)eh->e_shnum *
+        sizeof(Elf64_Shdr) > co.size())
+        return false;
+    const auto *sh = reinterpret_cast<const Elf64_Shdr *>(co.data() + eh->e_shoff);
+    const std::string kd = kname + ".kd";
+    for (int i = 0; i < eh->e_shnum; ++i) {
+        if (sh[i].sh_type != SHT_SYMTAB && sh[i].sh_type != SHT_DYNSYM) continue;
+        const Elf64_Shdr &st = sh[sh[i].sh_link];
+        const auto *sym = reinterpret_cast<const Elf64_Sym *>(co.data() + sh[i].sh_offset);
+        for (size_t j = 0; j < sh[i].sh_size / sizeof(Elf64_Sym); ++j) {
+            if (sym[j].st_name >= st.sh_size || kd != co.data() + st.sh_offset + sym[j].st_name) continue;
+            const Elf64_Shdr &sec = sh[sym[j].st_shndx];
+            const size_t off = sec.sh_offset + (sym[j].st_value - sec.sh_addr);
+            if (off + 64 > co.size()) return false;
+            uint32_t rsrc1, pss;
+            memcpy(&pss, co.data() + off + 4, 4);     // kernel_descriptor_t: +0 group, +4 private segment
+            memcpy(&rsrc1, co.data() + off + 48, 4);  // +48 compute_pgm_rsrc1
+            *regs = ((int)(rsrc1 & 63) + 1) * 8;
+            *scratch = (int)pss;
+            return true;
+        }
+    }
+    return false;
+}
+
+// compile src for gfx950: the code object and the lowered kernel name (fname,
+// or, given name_expr -- a template instantiation -- its lowered name)
+int compile_co(const std::string &src, const char *file, const char *fname, const char *name_expr,
+               std::vector<const char *> opts, std::string *code, std::string *lowered, std::string *err) {
+    const RtcApi &R = rtc_api();
+    static std::mutex env_mu;   // (one compile at a time reads the synced environment)
+    std::lock_guard<std::mutex> elk(env_mu);
+    R.sync_env();
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), file, 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (R.create(&prog, src.c_str(), file, 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         *err = "hiprtcCreateProgram failed";
         return -1;
     }
-    if (name_expr && hiprtcAddNameExpression(prog, name_expr) != HIPRTC_SUCCESS) {
-        hiprtcDestroyProgram(&prog);
+    if (name_expr && R.add_name(prog, name_expr) != HIPRTC_SUCCESS) {
+        R.destroy(&prog);
         *err = "hiprtcAddNameExpression failed";
         return -1;
     }
     opts.insert(opts.begin(), {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"});
-    hiprtcResult rr = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
+    hiprtcResult rr = R.compile(prog, (int)opts.size(), opts.data());
     if (rr != HIPRTC_SUCCESS) {
         size_t n = 0;
-        hiprtcGetProgramLogSize(prog, &n);
+        R.log_size(prog, &n);
         std::string log(n, '\0');
-        if (n) hiprtcGetProgramLog(prog, &log[0]);
-        *err = std::string("hipRTC compile failed: ") + hiprtcGetErrorString(rr) + "\n" + log.substr(0, 4000);
-        hiprtcDestroyProgram(&prog);
+        if (n) R.log(prog, &log[0]);
+        *err = std::string("hipRTC compile failed: ") + R.errstr(rr) + "\n" + log.substr(0, 4000);
+        R.destroy(&prog);
         return -1;
     }
-    std::string lowered = fname ? fname : "";
+    *lowered = fname ? fname : "";
     if (name_expr) {
         const char *low = nullptr;
-        if (hiprtcGetLoweredName(prog, name_expr, &low) != HIPRTC_SUCCESS || !low) {
-            hiprtcDestroyProgram(&prog);
+        if (R.lowered(prog, name_expr, &low) != HIPRTC_SUCCESS || !low) {
+            R.destroy(&prog);
             *err = "hiprtcGetLoweredName failed";
             return -1;
         }
-        lowered = low;
+        *lowered = low;
     }
     size_t n = 0;
-    hiprtcGetCodeSize(prog, &n);
-    std::string code(n, '\0');
-    hiprtcGetCode(prog, &code[0]);
-    hiprtcDestroyProgram(&prog);
+    R.code_size(prog, &n);
+    code->assign(n, '\0');
+    R.code(prog, &(*code)[0]);
+    R.destroy(&prog);
+    return 0;
+}
+
+// can a workgroup of nt threads be resident at all: its waves share a CU's 4
+// SIMDs, each with 512 registers per lane
+bool rtc_resident(const std::string &co, const std::string &kname, int nt, std::string *err) {
+    int regs = 0, scratch = 0;
+    if (!co_kernel_desc(co, kname, &regs, &scratch)) {
+        *err = "no kernel descriptor for " + kname;
+        return false;
+    }
+    const int waves_per_simd = ((nt + 63) / 64 + 3) / 4;
+    if (regs * waves_per_simd > 512) {
+        *err = "the build needs " + std::to_string(regs) + " registers per lane: a workgroup of " +
+               std::to_string(nt) + " threads cannot be resident (" + rtc_api().where + ")";
+        return false;
+    }
+    return true;
+}
+
+int load_co(const std::string &code, const std::string &lowered, RtcKernel *k, std::string *err) {
     if (hipModuleLoadData(&k->mod, code.data()) != hipSuccess) {
         *err = "hipModuleLoadData failed";
         return -1;
@@ -290,27 +432,67 @@ int compile_load(const std::string &src, const char *file, const char *fname, co
     }
     return 0;
 }
+
+int compile_load(const std::string &src, const char *file, const char *fname, const char *name_expr,
+                 std::vector<const char *> opts, int nt, RtcKernel *k, std::string *err) {
+    std::string code, lowered;
+    if (compile_co(src, file, fname, name_expr, std::move(opts), &code, &lowered, err) != 0) return -1;
+    if (!rtc_resident(code, lowered, nt, err)) return -1;
+    return load_co(code, lowered, k, err);
+}
 }  // namespace
+
+extern "C" long fpf_rtc_compile(const char *src, const char *name_expr, int ilp, int *regs, char *buf,
+                                size_t buf_size) {
+    if (!src || !name_expr) return FPF_ERR_ARG;
+    std::string code, lowered, err;
+    std::vector<const char *> opts;
+    if (ilp) opts = {"-mllvm", "-amdgpu-sched-strategy=iterative-ilp"};
+    if (compile_co(src, "fpf_rtc_check.hip", nullptr, name_expr, opts, &code, &lowered, &err) != 0) {
+        if (getenv("FPF_DEBUG")) fprintf(stderr, "fpf_rtc_compile: %s\n", err.c_str());
+        return FPF_ERR_UNSUPPORTED;
+    }
+    if (regs) {
+        int scratch = 0;
+        if (!co_kernel_desc(code, lowered, regs, &scratch)) *regs = -1;
+    }
+    if (buf && buf_size) memcpy(buf, code.data(), std::min(buf_size, code.size()));
+    return (long)code.size();
+}
+
+extern "C" const char *fpf_rtc_compiler(void) { return rtc_api().where.c_str(); }
 
 int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
     const std::string src = rtc_source(sp);
-    std::lock_guard<std::mutex> lk(g_mu);
     auto key = std::make_pair(device, src);
-    auto it = g_cache.find(key);
-    if (it != g_cache.end()) {
+    auto cached = [&] {
+        auto it = g_cache.find(key);
+        if (it == g_cache.end()) return false;
         ++it->second.refs;
         *out = it->second.k;
-        return 0;
+        return true;
+    };
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (cached()) return 0;
     }
+    // compiled without g_mu held (~seconds): other feeders' builds, releases and
+    // the wave kernels' cache lookups go on meanwhile
     RtcKernel k{};
 #ifdef FPF_STAMPS
-    if (compile_load(src, "fpf_rtc_tiled.hip", "fpf_rtc_tiled", nullptr, {"-DFPF_STAMPS"}, &k, err) != 0) return -1;
+    if (compile_load(src, "fpf_rtc_tiled.hip", "fpf_rtc_tiled", nullptr, {"-DFPF_STAMPS"}, sp.nt, &k, err) != 0)
+        return -1;
 #else
-    if (compile_load(src, "fpf_rtc_tiled.hip", "fpf_rtc_tiled", nullptr, {}, &k, err) != 0) return -1;
+    if (compile_load(src, "fpf_rtc_tiled.hip", "fpf_rtc_tiled", nullptr, {}, sp.nt, &k, err) != 0) return -1;
 #endif
     k.nt = sp.nt;
     // dynamic LDS above the default 64 KiB (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (cached()) {   // another thread built the same source meanwhile: keep one module
+        (void)hipModuleUnload(k.mod);
+        return 0;
+    }
     g_cache[key] = RtcEntry{k, 1};
     *out = k;
     return 0;
@@ -359,19 +541,30 @@ hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
     std::string name;
     const std::string src = wave_rtc_source(w, full, &name);
     static std::map<std::pair<int, std::string>, hipFunction_t> built;   // NULL: the build failed
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_pair(device, src);
-    auto it = built.find(key);
-    if (it != built.end()) return it->second;
+    static std::mutex build_mu;   // one compile at a time; g_mu is not held across it
+    const auto key = std::make_pair(device, src);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = built.find(key);
+        if (it != built.end()) return it->second;
+    }
+    std::lock_guard<std::mutex> blk(build_mu);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);   // (another thread may have built it meanwhile)
+        auto it = built.find(key);
+        if (it != built.end()) return it->second;
+    }
     RtcKernel k{};
-    std::string err;
+    std::string err, code, lowered;
     hipFunction_t fn = nullptr;
     // the static build's ILP-first scheduler (Makefile: fpf_wave.o / fpf_wblk.o);
     // FPF_WAVE_RTC_SCHED / FPF_WBLK_RTC_SCHED = 0: the default one (experiments)
     const char *se = getenv(w.wps ? "FPF_WBLK_RTC_SCHED" : "FPF_WAVE_RTC_SCHED");
     std::vector<const char *> opts;
     if (!(se && atoi(se) == 0)) opts = {"-mllvm", "-amdgpu-sched-strategy=iterative-ilp"};
-    if (compile_load(src, "fpf_rtc_wave.hip", nullptr, name.c_str(), opts, &k, &err) == 0) {
+    const int nt = 64 * (w.wps ? w.wps : w.wpb);
+    if (compile_co(src, "fpf_rtc_wave.hip", nullptr, name.c_str(), opts, &code, &lowered, &err) == 0 &&
+        rtc_resident(code, lowered, nt, &err) && load_co(code, lowered, &k, &err) == 0) {
         int stat = 0;
         if (hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.fn) == hipSuccess &&
             hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - stat) ==
@@ -381,6 +574,7 @@ hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
             err = "hipFuncSetAttribute failed";
     }
     if (!fn && getenv("FPF_DEBUG")) fprintf(stderr, "wave_rtc_function: %s (the static kernel runs)\n", err.c_str());
+    std::lock_guard<std::mutex> lk(g_mu);
     if (fn) ++g_wave_rtc_builds;
     built[key] = fn;   // (the module stays loaded for the process)
     return fn;

@@ -6,7 +6,8 @@ ROCm, "gloo" for CPU tests), rank r solves a contiguous range of global
 scenario ids, and scenario inputs are a pure function of the global id
 (feeder.scenario_loads / hosting_loads), so results do not depend on the
 shard.  The only exchange is the final combine of the per-GPU study
-aggregates -- one all-reduce of 8 doubles:
+aggregates -- one all-gather of 8 doubles per rank, folded in rank order on
+every rank (deterministic, the same fold as fold_aggregates):
 
     [loss_sum, vmin, vmax, n_conv, n_nonconv, n_over, n_under, n_scen]
      sum       min   max   sum ...
@@ -16,6 +17,8 @@ only "broadcast" is the per-peer UDP Gradient message of VoltVarCtrl.cpp:1497-15
 which stays with the Broker.
 """
 from __future__ import annotations
+
+import time
 
 import numpy as np
 
@@ -40,13 +43,16 @@ def batches(lo: int, hi: int, batch: int):
 
 
 def fold_aggregates(rows) -> np.ndarray:
-    """Deterministic host fold of aggregate rows (the combine the all-reduce performs)."""
+    """Deterministic host fold of aggregate rows, in row (rank) order: sums of
+    fields 0 and 3..7 accumulated one row after another, min of vmin, max of
+    vmax (the combine of include/freedm_pf.h: fpf_aggregate_fold)."""
     rows = np.asarray(rows, dtype=np.float64).reshape(-1, 8)
-    out = np.zeros(8)
-    out[0] = rows[:, 0].sum()
-    out[1] = rows[:, 1].min(initial=np.inf)
-    out[2] = rows[:, 2].max(initial=-np.inf)
-    out[3:] = rows[:, 3:].sum(axis=0)
+    out = np.array([0.0, np.inf, -np.inf, 0.0, 0.0, 0.0, 0.0, 0.0])
+    for r in rows:
+        out[0] += r[0]
+        out[1] = min(out[1], r[1])
+        out[2] = max(out[2], r[2])
+        out[3:] += r[3:]
     return out
 
 
@@ -62,21 +68,42 @@ def aggregate_results(status, loss, vmin, vmax, lb_v: float = 0.96, ub_v: float 
                     dtype=np.float64)
 
 
-def combine_aggregates(agg, group=None):
-    """All-reduce one rank's 8-double aggregate (torch tensor, on the device for
-    nccl/RCCL or on the CPU for gloo) in place into the study aggregate: sums for
-    fields 0 and 3..7, min for vmin, max for vmax.  Two collectives of 8 and 2
-    doubles -- the study's only exchange."""
+def gather_aggregates(agg, group=None):
+    """Every rank's 8-double aggregate as a [world, 8] tensor on every rank:
+    ONE collective (all_gather; RCCL on device tensors, gloo on host ones)."""
     import torch
     import torch.distributed as dist
 
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        return agg
-    mm = torch.stack([agg[1], -agg[2]])
-    tot = agg.clone()
-    dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
-    agg.copy_(tot)
-    agg[1] = mm[0]
-    agg[2] = -mm[1]
+        return agg.reshape(1, 8)
+    if dist.get_backend(group) == "gloo":
+        agg = agg.cpu()
+    parts = [torch.empty_like(agg) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, agg.contiguous(), group=group)
+    return torch.stack(parts)
+
+
+def combine_aggregates(agg, group=None):
+    """Combine one rank's 8-double aggregate (torch tensor) in place into the
+    study aggregate: gather_aggregates (the study's only exchange) folded in
+    rank order (fold_aggregates) -- every rank gets the same bits."""
+    import torch
+
+    rows = gather_aggregates(agg, group)
+    agg.copy_(torch.from_numpy(fold_aggregates(rows.cpu().numpy())).to(agg.device))
     return agg
+
+
+def timed_study(run_steps, study_aggregate, sync=None, group=None, clock=time.perf_counter):
+    """The timed region of a sharded study (bench.py): the rank's solves, its
+    study aggregate, then exactly one collective (gather_aggregates) and the
+    rank-order fold.  The clock is read once the folded aggregate is on the host
+    -- no barrier inside the region; the caller takes the max over ranks of the
+    elapsed times afterwards.  Returns (elapsed seconds, the folded aggregate)."""
+    t0 = clock()
+    run_steps()
+    rows = gather_aggregates(study_aggregate(), group)
+    tot = fold_aggregates(rows.cpu().numpy())   # (waits for the rank's device work)
+    if sync is not None:
+        sync()
+    return clock() - t0, tot

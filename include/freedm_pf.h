@@ -310,6 +310,18 @@ long        fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols,
                                        char *buf, size_t buf_size);
 /* Diagnostics: the per-plan wave kernels built with hipRTC so far in this process. */
 int         fpf_wave_rtc_builds(void);
+/* Diagnostics (no device needed): compile src with the hipRTC the library uses
+ * (the ROCm image's own, loaded into a private namespace so that a process which
+ * loaded another HIP runtime first -- e.g. PyTorch's bundled one -- still compiles
+ * with the compiler the static kernels were built with; fpf_rtc_compiler names
+ * it) and the library's options (ilp: the static wave kernels' scheduler).
+ * *regs (may be NULL): registers per lane (VGPRs + AGPRs) from the kernel
+ * descriptor, the figure the library's residency check uses (-1: not found).
+ * Writes at most buf_size bytes of the gfx950 code object and returns its full
+ * size, or FPF_ERR_*. */
+long        fpf_rtc_compile(const char *src, const char *name_expr, int ilp, int *regs,
+                            char *buf, size_t buf_size);
+const char *fpf_rtc_compiler(void);
 
 /* Diagnostics (no device needed): the wave kernel's plan for this feeder.
  * out[0..7] = {accepted (1/0), scenarios per wavefront, slots per lane,

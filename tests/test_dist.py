@@ -134,3 +134,58 @@ def test_bench_two_ranks_share_one_gpu():
     assert d["n_gpus"] == 2 and d["rccl_world"] == 2
     agg = d["aggregate"]
     assert agg["n_scen"] == 2 * 3 * 4096 and agg["n_conv"] == agg["n_scen"]
+
+
+COLLECTIVES = ("all_reduce", "all_gather", "all_gather_into_tensor", "barrier", "broadcast", "reduce",
+               "reduce_scatter", "reduce_scatter_tensor", "all_to_all", "all_to_all_single", "gather", "scatter")
+
+
+def _timed_rank_main(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    f = F.synthetic_feeder(30, 30)
+    lo, hi = D.shard_range(rank, world, N_STUDY)
+    from oracle import oracle as O
+    r = O.dpf_batch(f.Dl, f.Z, F.hosting_loads(f, np.arange(lo, hi)), nthreads=2, want_full=False)
+    row = torch.from_numpy(D.aggregate_results(r["status"], r["loss"], r["vmin"], r["vmax"]))
+    calls = []
+    saved = {n: getattr(dist, n) for n in COLLECTIVES if hasattr(dist, n)}
+    for n, fn in saved.items():
+        setattr(dist, n, (lambda n, fn: lambda *a, **k: (calls.append(n), fn(*a, **k))[1])(n, fn))
+    try:
+        elapsed, tot = D.timed_study(lambda: None, lambda: row)
+    finally:
+        for n, fn in saved.items():
+            setattr(dist, n, fn)
+    np.save(os.path.join(out_dir, f"row{rank}.npy"), row.numpy())
+    np.save(os.path.join(out_dir, f"tot{rank}.npy"), tot)
+    with open(os.path.join(out_dir, f"calls{rank}.txt"), "w") as fh:
+        fh.write(" ".join(calls))
+    dist.destroy_process_group()
+
+
+def test_timed_region_has_one_collective():
+    """bench.py's timed region (dist.timed_study): exactly one collective -- the
+    all-gather of the per-rank aggregates -- and no barrier; every rank's study
+    aggregate is fold_aggregates of the shards' rows in rank order, bit for bit."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_timed_rank_main, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
+        rows = [np.load(os.path.join(d, f"row{k}.npy")) for k in range(2)]
+        for k in range(2):
+            assert open(os.path.join(d, f"calls{k}.txt")).read().split() == ["all_gather"]
+            np.testing.assert_array_equal(np.load(os.path.join(d, f"tot{k}.npy")), D.fold_aggregates(rows))
+    assert D.fold_aggregates(rows)[7] == N_STUDY
+
+
+def test_fold_aggregates_rank_order():
+    rows = np.array([[1e16, 0.99, 1.01, 5, 0, 0, 0, 5], [1.0, 0.97, 1.02, 3, 1, 0, 1, 4],
+                     [-1e16, 0.98, 1.00, 2, 0, 1, 0, 2]])
+    out = D.fold_aggregates(rows)
+    assert out[0] == (1e16 + 1.0) + -1e16   # sequential, in rank order (0.0 here, not 1.0)
+    assert (out[1], out[2]) == (0.97, 1.02) and list(out[3:]) == [10, 1, 1, 1, 11]
+    ident = D.fold_aggregates(np.zeros((0, 8)))
+    assert ident[0] == 0 and ident[1] == np.inf and ident[2] == -np.inf

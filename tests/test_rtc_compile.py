@@ -103,3 +103,69 @@ def test_wblk_rtc_source_compiles(nn):
     name = src.rsplit("template __global__ void ", 1)[1].split("(")[0]
     assert name.startswith("fpf::dpf_wblk_kernel<")
     assert _compile(src, name, [b"-mllvm", b"-amdgpu-sched-strategy=iterative-ilp"]).startswith("_ZN3fpf15dpf_wblk_kernelI")
+
+
+def _notes(co: bytes) -> dict:
+    import re
+    import subprocess
+    import tempfile
+    exe = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(exe):
+        pytest.skip("llvm-readelf not available")
+    with tempfile.NamedTemporaryFile(suffix=".co") as t:
+        t.write(co)
+        t.flush()
+        txt = subprocess.run([exe, "--notes", t.name], capture_output=True, text=True, check=True).stdout
+    return {k: int(re.findall(rf"\.{k}:\s+(\d+)", txt)[-1]) for k in ("agpr_count", "vgpr_count",
+                                                                        "max_flat_workgroup_size")}
+
+
+@pytest.mark.parametrize("big,full", [(0, 0), (1, 0), (0, 1)])
+def test_wave_rtc_build_is_resident_with_torch_loaded(big, full):
+    """Round 4's dispatch abort (HSA_STATUS_ERROR_INVALID_ISA, profiles/r04rtc):
+    in a process that imported PyTorch first, the linked hiprtc* symbols are
+    PyTorch's bundled (older) hipRTC/comgr, which built the 512-thread wave
+    kernel with 32 AGPRs on top of its VGPRs -- 264 registers x 2 waves per SIMD
+    > 512, a workgroup that can never be resident, so the command processor
+    refused the dispatch.  The library now compiles with the image's own hipRTC
+    (dlmopen, fpf_rtc.cpp: rtc_api): every build of the config-2 plan fits."""
+    import torch  # noqa: F401  (the failing configuration: torch's HIP libraries loaded first)
+    from wave_rtc_dump import wave_rtc_source
+    from freedm_amd import _lib, synthetic_feeder
+    L = _lib.load()
+    assert L.fpf_rtc_compiler().decode().endswith("libhiprtc.so"), L.fpf_rtc_compiler()
+    src = wave_rtc_source(synthetic_feeder(123, 123), big, full)
+    name = src.rsplit("template __global__ void ", 1)[1].split("(")[0].encode()
+    regs = C.c_int(0)
+    n = L.fpf_rtc_compile(src.encode(), name, 1, C.byref(regs), None, 0)
+    assert n > 1000
+    buf = C.create_string_buffer(n)
+    assert L.fpf_rtc_compile(src.encode(), name, 1, None, buf, n) == n
+    md = _notes(buf.raw)
+    waves_per_simd = -(-md["max_flat_workgroup_size"] // 256)
+    assert md["agpr_count"] == 0, md
+    assert -(-md["vgpr_count"] // 8) * 8 == regs.value, (md, regs.value)   # the descriptor the check reads
+    assert regs.value * waves_per_simd <= 512, md
+
+
+def test_rtc_compile_survives_setenv():
+    """The private-namespace hipRTC has its own libc, whose environ was the
+    process's array at load time: a setenv that reallocates the process's array
+    freed it, and the next compile (comgr reads its environment) crashed -- the
+    round-5 GPU test run died this way at its second plan (monkeypatch.setenv of
+    FPF_WAVE_GEOM).  fpf_rtc.cpp syncs the namespace's environ before each compile."""
+    from wave_rtc_dump import wave_rtc_source
+    from freedm_amd import _lib, synthetic_feeder
+    L = _lib.load()
+    src = wave_rtc_source(synthetic_feeder(30, 30), 1, 0)
+    name = src.rsplit("template __global__ void ", 1)[1].split("(")[0].encode()
+    assert L.fpf_rtc_compile(src.encode(), name, 0, None, None, 0) > 1000
+    added = [f"FPF_TEST_ENV_GROW_{i}" for i in range(200)]
+    try:
+        for k in added:   # (grows the process's environ array until it moves)
+            os.environ[k] = "x" * 64
+        assert L.fpf_rtc_compile(src.encode(), name, 0, None, None, 0) > 1000
+    finally:
+        for k in added:
+            os.environ.pop(k, None)
+    assert L.fpf_rtc_compile(src.encode(), name, 0, None, None, 0) > 1000
