@@ -1816,8 +1816,9 @@ int fpf::fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const
 // The paired kernel's sticky fault word (set by a launch whose exchange wait gave
 // up; its scenarios have status FPF_EXCHANGE_FAILED): FPF_ERR_EXCHANGE once, then clear
 int fpf::take_exchange_fault(fpf_feeder *f) {
-    if (!f || !f->h_xerr || !__atomic_load_n(f->h_xerr, __ATOMIC_ACQUIRE)) return FPF_OK;
-    __atomic_store_n(f->h_xerr, 0u, __ATOMIC_RELEASE);
+    // (one read-and-clear: a launch on another stream that sets the word between a
+    // separate load and store would lose its report)
+    if (!f || !f->h_xerr || !__atomic_exchange_n(f->h_xerr, 0u, __ATOMIC_ACQ_REL)) return FPF_OK;
     return fail(f->ctx, FPF_ERR_EXCHANGE,
                 "paired wave-block kernel: an exchange wait gave up (scenarios with status FPF_EXCHANGE_FAILED)");
 }

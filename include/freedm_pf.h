@@ -218,9 +218,14 @@ int         fpf_solve_batch(fpf_feeder *feeder, int n_scen, const double *pq,
  * no_guard) use none of it and overlap freely.
  * Returns FPF_OK or an error (the non-converged count is in d_agg / status).
  * Asynchronous faults: a paired-kernel launch whose exchange gave up sets a
- * sticky word of the feeder; the next fpf_solve_batch_device or
- * fpf_feeder_check on the feeder returns FPF_ERR_EXCHANGE (and clears it)
- * without enqueueing anything. */
+ * sticky word of the feeder (one per feeder, not per launch).  The next entry
+ * on the feeder that reads it reports FPF_ERR_EXCHANGE once and clears it:
+ * fpf_feeder_check; fpf_solve_batch_device at entry, before it enqueues anything
+ * (its own batch is then NOT enqueued -- call it again); and the blocking entries
+ * (fpf_solve_batch, fpf_vvc_*, fpf_areas_solve) after their own launches, where
+ * the report may also come from an earlier asynchronous launch on the feeder
+ * that nobody checked.  Call fpf_feeder_check after asynchronous launches to
+ * attribute a fault to them. */
 int         fpf_solve_batch_device(fpf_feeder *feeder, int n_scen, const double *d_pq,
                                    const fpf_outputs *d_out, double *d_agg, void *stream);
 /* Wait for `stream` (a hipStream_t, NULL = the default stream), then report the
