@@ -527,8 +527,13 @@ std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
     return s.str();
 }
 
-// (read per call: tests switch it)
-constexpr int WAVE_RTC_DEFAULT_MIN = INT32_MAX;
+// launches of at least this many scenarios run the per-plan build: the
+// large-batch geometry (4-wave workgroups of the wave kernel from 16 384
+// scenarios on) and the wave-block kernel's batches -- config 4 0.908 -> 0.863 ms,
+// config 3 10.08 -> 9.72 ms (profiles/r05rtc); config 2's 8-wave geometry runs the
+// static kernel (its hipRTC build measured slower: 38.1 -> 39.4 us).  FPF_WAVE_RTC=n
+// sets the threshold, 0 turns the per-plan builds off (read per call: tests switch it)
+constexpr int WAVE_RTC_DEFAULT_MIN = 16384;
 int wave_rtc_min() {
     const char *e = getenv("FPF_WAVE_RTC");
     if (e && *e) return atoi(e) == 0 ? INT32_MAX : (atoi(e) == 1 ? 1 : atoi(e));

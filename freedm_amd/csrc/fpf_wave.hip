@@ -174,10 +174,9 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
 #if !defined(FPF_STAMPS) && !defined(FPF_WAVE_ABL) && !defined(FPF_WAVE_ABLATE)
     // launches of at least wave_rtc_min() scenarios run the per-plan hipRTC build
     // (fpf_rtc.cpp: ~2.5 s to compile, once per plan and variant in a process);
-    // smaller ones, and a failed build, the static kernel -- identical results
-    // (the light variant only: the full-output one -- Vpolar / PQb / PQL, zeroed
-    // phases -- is refused at dispatch when built by hipRTC, HSA_STATUS_ERROR_INVALID_ISA
-    // on the box, profiles/r04rtc; it runs the static kernel)
+    // smaller ones, and a failed or non-resident build, the static kernel --
+    // identical results (the light variant only: the full-output one -- Vpolar /
+    // PQb / PQL, zeroed phases -- spills heavily either way and keeps the static build)
     if (w.spec && !full && n_scen >= wave_rtc_min() && !wl.stag_n) {
         if (hipFunction_t fn = wave_rtc_function(dev, w, full)) {
             OutDev oa = o;

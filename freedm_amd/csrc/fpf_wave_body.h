@@ -480,6 +480,12 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     // phases of a sweep (MI355X_MICROARCH.md "Two waves per SIMD", item 9)
     if (WPB >= 8 && wv >= WPB / 2) __builtin_amdgcn_s_sleep(FPF_WAVE_STAGGER);
 #endif
+#ifdef FPF_WAVE_PRIO
+    // diagnostic: static issue priority for the second half of the workgroup's
+    // waves, which share SIMDs with the first half (MI355X_MICROARCH.md "Two
+    // waves per SIMD", item 4); 4-wave workgroups: the odd workgroups
+    if (WPB >= 8 ? wv >= WPB / 2 : (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(FPF_WAVE_PRIO);
+#endif
     WSTAMP(2);
     cx slp[3];   // (FPF_WAVE_SLD_PREF) slot 0's loads, read a sweep ahead
 #pragma unroll

@@ -97,10 +97,13 @@ typedef struct fpf_opts {
     double ub_v;       /* 1.05  load_system_data.cpp:24                    */
     int    tile;       /* scenarios per workgroup for the tiled kernel, 0 = auto */
     int    specialize; /* 1 (default): compile the tiled kernel for the feeder's topology
-                          with hipRTC at fpf_feeder_create (and, with FPF_WAVE_RTC=n set,
-                          the wave kernel for its plan, run by launches of >= n
-                          scenarios; identical results); 0: interpret the tiled
-                          programs, static wave kernel */
+                          with hipRTC at fpf_feeder_create, and the wave / wave-block
+                          kernel for its plan (its uniform values as constants), run by
+                          launches of >= 16384 scenarios (FPF_WAVE_RTC=n: >= n, 0: never;
+                          built by fpf_feeder_reserve or the first such launch, ~2.5 s
+                          once per plan in a process; identical results -- a build that
+                          fails or could not be resident runs the static kernel);
+                          0: interpret the tiled programs, static wave kernels */
     int    exact;      /* 1: the specialised kernel repeats the reference's roundings
                           (complex divide as libgcc __divdc3, no FMA): V, PQb, PQL, loss
                           bit-identical to the oracle.  0 (default): load currents as

@@ -136,9 +136,6 @@ def _zeroed_feeder():
     return F.Feeder(Dl, Z, name="demo-rel")
 
 
-@pytest.mark.skipif(os.environ.get("FPF_TEST_WAVE_RTC") != "1",
-                    reason="the hipRTC wave build is refused at dispatch on the box "
-                           "(HSA_STATUS_ERROR_INVALID_ISA, profiles/r04rtc); opt-in experiment")
 @pytest.mark.parametrize("which", ["123", "123-1,4", "30", "nested", "zeroed"])
 def test_specialised_build_matches_static(which, monkeypatch):
     """fpf_opts.specialize with FPF_WAVE_RTC=2048: a light-output wave launch of

@@ -284,9 +284,6 @@ def test_wblk_heavy_2048_bus():
         pf.close()
 
 
-@pytest.mark.skipif(os.environ.get("FPF_TEST_WAVE_RTC") != "1",
-                    reason="the hipRTC wave build is refused at dispatch on the box "
-                           "(HSA_STATUS_ERROR_INVALID_ISA, profiles/r04rtc); opt-in experiment")
 @pytest.mark.parametrize("n", [300, 1100])
 def test_wblk_specialised_build_matches_static(n, monkeypatch):
     """fpf_opts.specialize with FPF_WAVE_RTC=2048: a light-output wave-block
