@@ -409,7 +409,10 @@ void analyse_tiled(HostFeeder &h) {
 // Ib the backward sweep hands up a block (DPF_return7.cpp:147-157) flows to the
 // node's forward source (:176-178) -- the sweep then computes subtree sums.
 constexpr size_t WAVE_LDS_BUDGET = 159 * 1024;   // 160 KiB per CU minus the kernel's static LDS
-constexpr int WAVE_SMALL_WPB_MIN_SCEN = 16384;    // batches from here on use WaveHost::wpb_big_batch
+// batches from here on use WaveHost::wpb_big_batch (and, fpf_rtc.cpp, the per-plan
+// build): config 2's 4 096-scenario batch on 4-wave workgroups with the per-plan
+// build 37.3 us against 38.9-39.2 on one 8-wave workgroup per CU, static (profiles/r05wio)
+constexpr int WAVE_SMALL_WPB_MIN_SCEN = 4096;
 
 struct WaveHost {
     bool ok = false;
@@ -844,8 +847,10 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     auto lds_at = [&](int wpb) { probe.wpb = wpb; return wave_lds_bytes(probe); };
     // Measured (profiles/r02a, 123-bus): two 8-scenario workgroups per CU are
     // 11 % faster on a 131 072-scenario batch (config 4), one 16-scenario
-    // workgroup 6 % faster on a 4 096 batch (config 2, one workgroup per CU:
-    // nothing to overlap) -- so wpb_big_batch is used from WAVE_SMALL_WPB_MIN_SCEN.
+    // workgroup 6 % faster on a 4 096 batch then (config 2, static kernels); with
+    // the per-plan hipRTC build of the 4-wave geometry config 2 runs 4 % faster on
+    // two 8-scenario workgroups (profiles/r05wio) -- so wpb_big_batch is used from
+    // WAVE_SMALL_WPB_MIN_SCEN = 4096, the per-plan build's threshold.
     int wpb = 0, wpb_big_batch = 0;
     if (lds_at(big) <= WAVE_LDS_BUDGET) wpb = big;
     else if (lds_at(small) <= WAVE_LDS_BUDGET) wpb = small;
@@ -1606,6 +1611,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
                 wv[g]->out_u = UO[g];
                 wv[g]->out_smaj = UO[g] ? (const int32_t *)((char *)f->d_stage_tab + off[g][2]) : nullptr;
                 wv[g]->out_l0 = UO[g] ? (const int32_t *)((char *)f->d_stage_tab + off[g][3]) : nullptr;
+                wave_io_units(*wv[g]);
             }
         }
     }
@@ -2246,6 +2252,7 @@ extern "C" long fpf_feeder_wave_rtc_source(const double *dl, int nl, int ncols, 
         std::vector<int32_t> a, b;
         w.stage_u = wave_stage_tables(w, a, b);
         w.out_u = wave_out_tables(w, a, b);
+        wave_io_units(w);
     }
     std::string name;
     const std::string src = wave_rtc_source(w, full != 0, &name);

@@ -166,6 +166,11 @@ struct WaveDev {
     // index out_*[i] (row 0: the scenario's V0S); out_u per thread, 0: none
     const int32_t *out_smaj, *out_l0;
     int32_t out_u;
+    // per-wave IO (scenario major, wave_io_units): a wave stages its own
+    // scenarios' loads (stage_uw chunks per lane of the stage_smaj table) and
+    // writes its own V (out_uw elements per lane of out_smaj) -- no workgroup
+    // barrier waits for the slowest wave's loads or sweeps; 0: the workgroup's IO
+    int32_t stage_uw, out_uw;
     double rv0[3];              // 1/|V0_p|^2 (the flat start's first load currents)
     // wave-block kernel (fpf_wblk.hip): one scenario per workgroup of wps
     // wavefronts (L = 64 wps lanes, C slots per lane) for feeders of 257..2048
@@ -372,6 +377,9 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
 int wave_stage_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0);
 // the write-out tables (WaveDev::out_smaj / out_l0, [u][NT] int); 0 if above the limit
 int wave_out_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0);
+// per-wave IO units (WaveDev::stage_uw / out_uw) of a geometry whose tables exist
+// (stage_u / out_u set); 0 where a wave's share exceeds the kernel's limit
+void wave_io_units(WaveDev &w);
 size_t wave_lds_bytes(const WaveDev &w);
 hipError_t launch_transpose(const double *in, double *out, size_t rows, size_t cols, hipStream_t st);
 hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);

@@ -510,6 +510,7 @@ std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
       << "\n#define FPF_WSPEC_BDEPTH " << w.bdepth << "\n#define FPF_WSPEC_NCOMP " << w.ncomp
       << "\n#define FPF_WSPEC_TEMP_SYM " << w.temp_sym << "\n#define FPF_WSPEC_OFF_IN_X " << w.off_in_x
       << "\n#define FPF_WSPEC_STAGE_U " << w.stage_u << "\n#define FPF_WSPEC_OUT_U " << w.out_u
+      << "\n#define FPF_WSPEC_STAGE_UW " << w.stage_uw << "\n#define FPF_WSPEC_OUT_UW " << w.out_uw
       << "\n#define FPF_WSPEC_HAS_MASK " << w.has_mask << "\n#define FPF_WSPEC_HAS_REL " << w.has_rel
       << "\n#define FPF_WSPEC_MXITR " << w.mxitr << "\n";
     char nm[96];
@@ -528,12 +529,13 @@ std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
 }
 
 // launches of at least this many scenarios run the per-plan build: the
-// large-batch geometry (4-wave workgroups of the wave kernel from 16 384
-// scenarios on) and the wave-block kernel's batches -- config 4 0.908 -> 0.863 ms,
-// config 3 10.08 -> 9.72 ms (profiles/r05rtc); config 2's 8-wave geometry runs the
-// static kernel (its hipRTC build measured slower: 38.1 -> 39.4 us).  FPF_WAVE_RTC=n
-// sets the threshold, 0 turns the per-plan builds off (read per call: tests switch it)
-constexpr int WAVE_RTC_DEFAULT_MIN = 16384;
+// large-batch geometry (4-wave workgroups of the wave kernel, fpf_api.cpp:
+// WAVE_SMALL_WPB_MIN_SCEN) and the wave-block kernel's batches -- config 4 0.908 ->
+// 0.863 ms, config 3 10.08 -> 9.72 ms (profiles/r05rtc), config 2 38.9-39.2 ->
+// 37.3 us with the 4-wave geometry (profiles/r05wio; the 8-wave geometry's build
+// measured slower, 38.1 -> 39.4 us).  FPF_WAVE_RTC=n sets the threshold, 0 turns
+// the per-plan builds off (read per call: tests switch it)
+constexpr int WAVE_RTC_DEFAULT_MIN = 4096;
 int wave_rtc_min() {
     const char *e = getenv("FPF_WAVE_RTC");
     if (e && *e) return atoi(e) == 0 ? INT32_MAX : (atoi(e) == 1 ? 1 : atoi(e));

@@ -94,6 +94,16 @@ int wave_stage_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<
     return U;
 }
 
+void wave_io_units(WaveDev &w) {
+    w.stage_uw = w.out_uw = 0;
+    if (getenv("FPF_WAVE_WG_IO")) return;   // (experiments: the workgroup's IO)
+    const int suw = (w.spw * 3 * w.nl + 63) / 64, ouw = (w.spw * 3 * w.nn + 63) / 64;
+    if (w.stage_u > 0 && w.out_u > 0 && suw <= WAVE_STAGE_U && ouw <= WAVE_STAGE_U) {
+        w.stage_uw = suw;
+        w.out_uw = ouw;
+    }
+}
+
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;

@@ -117,6 +117,8 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     f.off_in_x = FPF_WSPEC_OFF_IN_X;
     f.stage_u = FPF_WSPEC_STAGE_U;
     f.out_u = FPF_WSPEC_OUT_U;
+    f.stage_uw = FPF_WSPEC_STAGE_UW;
+    f.out_uw = FPF_WSPEC_OUT_UW;
     f.has_mask = FPF_WSPEC_HAS_MASK;
     f.has_rel = FPF_WSPEC_HAS_REL;
     f.mxitr = FPF_WSPEC_MXITR;
@@ -196,9 +198,18 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             }
     }
 
+    // per-wave IO (WaveDev::stage_uw, scenario major, not with the area hooks): a
+    // wave stages its own SPW scenarios and writes its own V; the workgroup's one
+    // barrier waits only for the shared tables
+    const bool wio = o.smaj && f.stage_uw > 0 && !o.hook && !DBG(256);
+    const int wsc0 = wv * SPW, wnw = max(0, min(SPW, nsb - wsc0));   // this wave's first scenario, its live ones
     // ---- the workgroup's loads P/Q [6][Nl][nsb], coalesced (16 scenarios = one
     // 128-byte line per row), all of a thread's loads in flight, into STG scaled
     // by 1/(bkva/3) (Sld, DPF_return7.cpp:46-50)
+    typedef double d2w __attribute__((ext_vector_type(2)));
+    int2 wtb[WAVE_STAGE_U];
+    d2w wr[WAVE_STAGE_U];
+    double *const sd0 = (double *)stg;
     {
         double *const sd = (double *)stg;
         // element (f, row, j) of pq -> STG[f / 2][row][j].{re, im}
@@ -229,13 +240,28 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             pv = (int)threadIdx.x < np2 ? f.blk_pairs[threadIdx.x] : 0;
             kv = (int)threadIdx.x < C * L ? f.slot_node[threadIdx.x] : 0;
         };
-        if (FPF_WAVE_EARLY_TABLES) table_loads();
+        if (FPF_WAVE_EARLY_TABLES || wio) table_loads();
         constexpr int U = 8;
         const int total = DBG(256) ? 0 : 6 * nl * SPB;
         typedef double d2v __attribute__((ext_vector_type(2)));
         constexpr int US = WAVE_STAGE_U;
         const int SU = f.stage_u;
-        if (SU > 0 && (o.smaj || (FPF_WAVE_L0_TABLE && (B & 1) == 0))) {
+        if (wio) {
+            // per-wave staging: this wave's SPW scenarios are one contiguous block of
+            // SPW x 6 Nl doubles; chunk c = u 64 + lane goes where the tile table puts
+            // the tile's chunk c (scenarios 0 .. SPW-1), shifted to this wave's columns
+            const int nchw = wnw * 3 * nl, SUW = f.stage_uw;
+            const int2 *tab = (const int2 *)f.stage_smaj;
+            const d2v *src = (const d2v *)(pq + (size_t)(s0 + wsc0) * 6 * nl);
+#pragma unroll
+            for (int u = 0; u < US; ++u) {
+                if (u < SUW) {
+                    const int c = u * 64 + lane;
+                    wtb[u] = tab[c];
+                    wr[u] = __builtin_nontemporal_load(src + (c < nchw ? c : 0));
+                }
+            }
+        } else if (SU > 0 && (o.smaj || (FPF_WAVE_L0_TABLE && (B & 1) == 0))) {
             // table-driven (wave_stage_tables): chunk c = u NT + t, 16 bytes each, every
             // load of the thread in flight with its two STG destinations; scenario
             // major: the tile is one contiguous block of nsb x 6 Nl doubles;
@@ -379,7 +405,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 if (i < total) sd[spos(i / SPB, i % SPB)] = r[u] * inv_s3;
             }
         }
-        if (!FPF_WAVE_EARLY_TABLES) table_loads();
+        if (!FPF_WAVE_EARLY_TABLES && !wio) table_loads();
         if (TEMP_IN_LDS) {
 #pragma unroll
             for (int u = 0; u < UT; ++u) {
@@ -390,8 +416,23 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         if ((int)threadIdx.x < np2) pairs[threadIdx.x] = pv;
         for (int i = threadIdx.x + NT; i < np2; i += NT) pairs[i] = f.blk_pairs[i];
         if ((int)threadIdx.x < C * L) knode[threadIdx.x] = kv;
+        if (wio) {
+            // the shared tables are in LDS: one barrier, with this wave's loads still
+            // in flight (a barrier does not drain vector memory), then the wave
+            // stores its own loads and goes on without waiting for the others
+            __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            const int nchw = wnw * 3 * nl;
+#pragma unroll
+            for (int u = 0; u < WAVE_STAGE_U; ++u) {
+                const int c = u * 64 + lane;
+                if (u < f.stage_uw && c < nchw) {
+                    sd0[wtb[u].x + 2 * wsc0] = wr[u].x * inv_s3;
+                    sd0[wtb[u].y + 2 * wsc0] = wr[u].y * inv_s3;
+                }
+            }
+        }
     }
-    if (o.hook && o.hook->pre_n > 0) {
+    if (o.hook && o.hook->pre_n > 0) {   // (never with per-wave IO)
         // the multi-area solve (OutDev::hook): the rows children hang off carry
         // their source powers too, scaled like the loads
         __syncthreads();
@@ -404,7 +445,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     h->pre_sin[kid][(size_t)fq * B + s0 + j] * inv_s3;
         }
     }
-    __syncthreads();
+    if (!wio) __syncthreads();
     WSTAMP(1);
     if (DBG(8192)) return;
     // this lane's block chain (lane b < nblk resolves block b), padded with the zero
@@ -953,7 +994,34 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     // Published before the V stores, so the ticket does not wait for them.
     // the write-out table (wave_stage_tables; L2-resident), in flight across the barrier
     constexpr int UO = WAVE_STAGE_U;
-    const int OU = (!FULL && (o.v_re || o.v_im) && !DBG(1024)) ? f.out_u : 0;
+    const bool vout = !FULL && (o.v_re || o.v_im) && !DBG(1024);
+    if (wio && vout) {
+        // per-wave write-out: this wave's [wnw][3][Nn] block, element i = u 64 + lane
+        // read from STG where the tile table puts the tile's element i (scenarios
+        // 0 .. SPW-1), shifted to this wave's columns (row 0: its regions)
+        const int per = 3 * nn, nval = wnw * per, OUW = f.out_uw;
+        const int32_t *ot = f.out_smaj;
+        double2 vv[UO];
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            if (u < OUW) {
+                const int i = u * 64 + lane;
+                int q = ot[i < SPW * per ? i : 0];
+                q += q >= 3 * PSTR ? wsc0 * RS : wsc0;
+                vv[u] = stg[q];
+            }
+        }
+        const size_t d0 = (size_t)(s0 + wsc0) * per;
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int i = u * 64 + lane;
+            if (u < OUW && i < nval) {
+                if (o.v_re) __builtin_nontemporal_store(vv[u].x, o.v_re + d0 + i);
+                if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + d0 + i);
+            }
+        }
+    }
+    const int OU = (vout && !wio) ? f.out_u : 0;
     int otab[UO];
     {
         const int32_t *ot = o.smaj ? f.out_smaj : f.out_l0;
@@ -962,7 +1030,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             if (u < OU) otab[u] = ot[u * NT + (int)threadIdx.x];
     }
     WSTAMP(122);
-    __syncthreads();
+    // (per-wave IO: no barrier unless the tail needs the workgroup -- the fused
+    // aggregate, the area hooks' stop test, the guard's local re-solve)
+    const bool tail_wg = !wio || o.agg || o.check || o.fix_dev || o.hook;
+    if (tail_wg) __syncthreads();
     WSTAMP(123);
     if (o.hook && o.hook->post_n > 0) {
         // the multi-area solve (OutDev::hook): each child's source voltage = V at
@@ -1032,7 +1103,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 if (o.v_im) __builtin_nontemporal_store(vv[u].y, o.v_im + d);
             }
         }
-    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj) {
+    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && o.smaj && !wio) {
         // scenario-major layout: the tile's V is one contiguous [nsb][3][Nn] block
         const int per = 3 * nn, total = nsb * per;
         // element i: scenario j = i / per, (phase p, node k) of i % per, walked NT apart
@@ -1048,7 +1119,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             w.next();
             while (w.fq >= 3) { w.fq -= 3; ++j; }
         }
-    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024)) {
+    } else if (!FULL && (o.v_re || o.v_im) && !DBG(1024) && !o.smaj) {
         constexpr int UV = 4;
         static_assert(NT % SPB == 0, "a thread keeps its scenario");
         const int total = 3 * nn * SPB;

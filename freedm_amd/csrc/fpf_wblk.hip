@@ -105,7 +105,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
             attr_done.insert(key);
         }
     }
-#if !defined(FPF_WBLK_ABL) && !defined(FPF_WBLK_NO_GUARD_CODE)
+#if !defined(FPF_WBLK_ABL) && !defined(FPF_WBLK_NO_GUARD_CODE) && !defined(FPF_STAMPS)
     // launches of at least wave_rtc_min() scenarios: the per-plan hipRTC build
     // (fpf_rtc.cpp), identical results; a failed build runs the static kernel
     if (w.spec && !full && !seg && n_scen >= wave_rtc_min()) {   // (the light variant only, as launch_wave)

@@ -23,6 +23,32 @@ constexpr bool GUARD_CODE = false;
 constexpr bool GUARD_CODE = true;
 #endif
 
+#if defined(FPF_STAMPS) && !defined(FPF_WSPEC)
+// diagnostic build only (tools/wblk_stamps.py): thread 0 of each of 64 workgroups
+// from fpf_wblk_stamp_base on records s_memtime at stage boundaries, [64][128]:
+// 0 entry, 1 staged (after the barrier), 4 + 8 it + k in sweep it < 14 (k = 0 top,
+// 1 backward scan + wave totals, 2 Ib gathered, 3 drops, 4 forward scan + wave
+// totals, 5 block offsets, 6 V), 120 after the loop, 121 extremes, 122 results,
+// 123 V written
+__device__ unsigned long long *fpf_wblk_stamp_buf = nullptr;
+__device__ unsigned fpf_wblk_stamp_base = 0;
+#define BSTAMP(idx)                                                                                    \
+    do {                                                                                               \
+        const unsigned w_ = blockIdx.x - fpf_wblk_stamp_base;                                          \
+        if (fpf_wblk_stamp_buf && threadIdx.x == 0 && w_ < 64u && (idx) < 128)                         \
+            fpf_wblk_stamp_buf[w_ * 128 + (idx)] = __builtin_amdgcn_s_memtime();                        \
+    } while (0)
+extern "C" int fpf_debug_set_wblk_stamp_buffer(void *dptr, unsigned base) {
+    unsigned long long *p = (unsigned long long *)dptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fpf_wblk_stamp_base), &base, sizeof(base)) != hipSuccess) return -3;
+    return hipMemcpyToSymbol(HIP_SYMBOL(fpf_wblk_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#define BSTAMP_IT(k) BSTAMP(it < 14 ? 4 + 8 * it + (k) : 999)
+#else
+#define BSTAMP(idx) ((void)0)
+#define BSTAMP_IT(k) ((void)0)
+#endif
+
 namespace {
 constexpr int WB_C = 4;   // slots per lane
 constexpr int WB_BD = 6;  // block-chain depth resolved from registers (deeper: the LDS loop)
@@ -50,6 +76,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     extern __shared__ double2 lds[];
     if (o.skip && *o.skip) return;   // (the multi-area solve's device-side stop)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    BSTAMP(0);
     const int s = xcd_tile(blockIdx.x, gridDim.x);   // this workgroup's scenario
     const int nblk = f.nblk, nn = f.nn, nl = f.nl, bdepth = f.bdepth, XC = f.ncomp + 1;
     const int ntz = f.temp_sym ? 4 : 9, PS = nl + 1;
@@ -161,6 +188,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         lg[c] = f.slot_lng[c * L + tid];
     }
     __syncthreads();
+    BSTAMP(1);
     if (WABL(4)) return;
 
     // flat start (V = V0 on every node, DPF_return7.cpp:92-96, the feeder's own
@@ -205,6 +233,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double dmin = INFINITY;  // closest |err2 - eps^2| of a decision in the guard's coarse band
     double err2_last = 0.0;
     for (;; ++it) {
+        BSTAMP_IT(0);
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
         if (flat && it == 0) {
@@ -248,6 +277,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             for (int q = 0; q < 6; ++q) wtb[8 * wv + q] = sc6[q];
         }
         __syncthreads();
+        BSTAMP_IT(1);
         wave_prefix<W, true>(wtb, wv, lane, pre, tot6);
         cx tot[3], exl[3];
 #pragma unroll
@@ -279,6 +309,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             }
         }
 
+        BSTAMP_IT(2);
         // ---- convergence on the substation branch (:199-217), compared as squares;
         // the same in every lane of the workgroup
         double err2 = 0.0;
@@ -342,6 +373,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
         }
 
+        BSTAMP_IT(3);
         if (SEG) {
             // ---- forward sweep (:163-195): V = V0 - A(k), A(k) = off(block) + Gseg(k),
             // Gseg the block-local path sum of the drops (a prefix scan segmented at
@@ -476,6 +508,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 for (int q = 0; q < 6; ++q) wtf[8 * wv + q] = sc6[q];
             }
             __syncthreads();
+            BSTAMP_IT(4);
             wave_prefix<W, false>(wtf, wv, lane, pre, tot6);
     #pragma unroll
             for (int p = 0; p < 3; ++p) {
@@ -523,6 +556,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
             }
             __syncthreads();
+            BSTAMP_IT(5);
     #pragma unroll
             for (int c = 0; c < C; ++c)
     #pragma unroll
@@ -531,6 +565,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
                 }
         }
+        BSTAMP_IT(6);
 
         if (fin) {
             // ---- the last sweep: V of node k over Sld row k - 1 (every Sld read of
@@ -565,6 +600,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             break;
         }
     }
+    BSTAMP(120);
     __syncthreads();
 
     // ---- Vmin/Vmax (V_abc_list.cpp:7-81, VoltVarCtrl.cpp:1201-1207)
@@ -622,6 +658,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         }
     }
     __syncthreads();
+    BSTAMP(121);
 
     // ---- per-scenario results and the fused batch aggregate [loss_sum, vmin, vmax,
     // n_conv, n_nonconv, n_over, n_under, n_scen]: the scenario's partial, published
@@ -700,6 +737,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             last_wg = t == gridDim.x - 1;
         }
     }
+    BSTAMP(122);
     // ---- V out: [3][Nn][B] re / im planes, column s (or the scenario's
     // contiguous [3][Nn] block in the scenario-major layout)
     if (!FULL && (o.v_re || o.v_im) && !WABL(2)) {
@@ -719,6 +757,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             }
         }
     }
+    BSTAMP(123);
     if (agg) {
         __syncthreads();
         if (last_wg) {

@@ -99,7 +99,7 @@ typedef struct fpf_opts {
     int    specialize; /* 1 (default): compile the tiled kernel for the feeder's topology
                           with hipRTC at fpf_feeder_create, and the wave / wave-block
                           kernel for its plan (its uniform values as constants), run by
-                          launches of >= 16384 scenarios (FPF_WAVE_RTC=n: >= n, 0: never;
+                          launches of >= 4096 scenarios (FPF_WAVE_RTC=n: >= n, 0: never;
                           built by fpf_feeder_reserve or the first such launch, ~2.5 s
                           once per plan in a process; identical results -- a build that
                           fails or could not be resident runs the static kernel);
