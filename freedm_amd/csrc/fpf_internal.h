@@ -454,6 +454,7 @@ hipError_t rtc_launch(const RtcKernel &k, const FeederDev &f, int n_scen, const 
 // variant; built on first use, kept for the
 // process.  NULL if the build failed (the static kernel runs)
 hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full);
+hipFunction_t wave_rtc_function_src(int device, const WaveDev &w, bool full);   // (uncached by plan)
 // the smallest launch that runs it (FPF_WAVE_RTC: 0 never, 1 always, n; default 2048)
 int wave_rtc_min();
 std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name);

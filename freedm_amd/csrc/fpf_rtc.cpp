@@ -17,6 +17,7 @@
 #include <elf.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -545,6 +546,27 @@ int wave_rtc_min() {
 int g_wave_rtc_builds = 0;   // successful builds in this process (fpf_wave_rtc_builds)
 
 hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
+    // every launch looks its build up: by the plan values the source is made of
+    // (forming the ~300 KB source and comparing it as the key cost ~10 us a launch),
+    // then, for a plan not seen yet, by the source itself
+    typedef std::array<int32_t, 24> PlanKey;
+    const char *se0 = getenv(w.wps ? "FPF_WBLK_RTC_SCHED" : "FPF_WAVE_RTC_SCHED");
+    const PlanKey pk = {device, (int)full, w.nn, w.nl, w.nblk, w.bdepth, w.ncomp, w.temp_sym, w.off_in_x, w.stage_u,
+                        w.out_u, w.stage_uw, w.out_uw, w.has_mask, w.has_rel, w.mxitr, w.ncode, w.wps, w.spw, w.C,
+                        w.wpb, se0 ? atoi(se0) : -1, 0, 0};
+    static std::map<PlanKey, hipFunction_t> by_plan;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = by_plan.find(pk);
+        if (it != by_plan.end()) return it->second;
+    }
+    const hipFunction_t fn = wave_rtc_function_src(device, w, full);
+    std::lock_guard<std::mutex> lk(g_mu);
+    by_plan[pk] = fn;
+    return fn;
+}
+
+hipFunction_t wave_rtc_function_src(int device, const WaveDev &w, bool full) {
     std::string name;
     const std::string src = wave_rtc_source(w, full, &name);
     static std::map<std::pair<int, std::string>, hipFunction_t> built;   // NULL: the build failed

@@ -169,11 +169,17 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     // first - 1) index pairs, packed two per register, so that all of a chain's X
     // reads issue together every sweep instead of one dependent pair per level
     const bool chain_regs = bdepth <= WB_BD && nblk <= NT && XC < 65536;
+    // one (block, phase) per thread where the workgroup has 3 nblk threads (thread
+    // t: block t % nblk, phase t / nblk): a third of the chain reads and adds per
+    // thread, on every wave instead of the first nblk / 64 (round 5: the block
+    // offsets were 28 % of a config-3 sweep with one block per thread, 3 phases each)
+    const bool off3 = chain_regs && 3 * nblk <= NT;
+    const int op3 = off3 ? tid / nblk : 0, ob3 = off3 ? tid - op3 * nblk : tid;
     int bp[WB_BD];
 #pragma unroll
     for (int j = 0; j < WB_BD; ++j) {
-        const bool ok = chain_regs && j < bdepth && tid < nblk;
-        bp[j] = ok ? f.blk_pairs[(2 * j) * nblk + tid] | (f.blk_pairs[(2 * j + 1) * nblk + tid] << 16)
+        const bool ok = chain_regs && j < bdepth && (off3 ? tid < 3 * nblk : tid < nblk);
+        bp[j] = ok ? f.blk_pairs[(2 * j) * nblk + ob3] | (f.blk_pairs[(2 * j + 1) * nblk + ob3] << 16)
                    : (XC - 1) | ((XC - 1) << 16);
     }
     int si[C], sb[C], bk[C], cz[C];
@@ -429,7 +435,16 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             if (!WABL(8)) __syncthreads();
             // block offsets, one thread per block, stored as V0 - off(b) (and off(b)
             // itself for the restart below a zeroed phase); one X read per chain level
-            if (chain_regs) {
+            if (off3) {
+                if (tid < 3 * nblk) {
+                    cx of = mk(0, 0);
+    #pragma unroll
+                    for (int j = 0; j < WB_BD; ++j)
+                        if (j < bdepth) of = cadd(of, ldx(X, op3 * XC + (bp[j] & 0xffff)));   // uniform bound
+                    stx(OFF, op3 * nblk + ob3, csub(ldx(V0S, op3), of));
+                    if (FULL && f.has_rel) stx(OFFA, op3 * nblk + ob3, of);
+                }
+            } else if (chain_regs) {
                 if (tid < nblk) {
                     cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     #pragma unroll
@@ -527,7 +542,16 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             if (!WABL(8)) __syncthreads();
             // block offsets, one thread per block, stored as V0 - off(b): off(b) = sum over
             // b's block-ancestor chain of Ginc[tap] - Ginc[first - 1] (block 0: 0)
-            if (chain_regs) {
+            if (off3) {
+                if (tid < 3 * nblk) {
+                    cx of = mk(0, 0);
+    #pragma unroll
+                    for (int j = 0; j < WB_BD; ++j)
+                        if (j < bdepth)   // uniform; levels past a chain's depth read the zero entry
+                            of = cadd(of, csub(ldx(X, op3 * XC + (bp[j] & 0xffff)), ldx(X, op3 * XC + (bp[j] >> 16))));
+                    stx(OFF, op3 * nblk + ob3, csub(ldx(V0S, op3), of));
+                }
+            } else if (chain_regs) {
                 if (tid < nblk) {
                     cx of[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
     #pragma unroll

@@ -18,10 +18,13 @@ which stays with the Broker.
 """
 from __future__ import annotations
 
+import os
+import sys
 import time
 
 import numpy as np
 
+TRACE = bool(os.environ.get("FPF_BENCH_TRACE"))   # (diagnostics: timed_study's stages on stderr)
 AGG_FIELDS = ("loss_sum", "vmin", "vmax", "n_conv", "n_nonconv", "n_over", "n_under", "n_scen")
 
 
@@ -46,14 +49,14 @@ def fold_aggregates(rows) -> np.ndarray:
     """Deterministic host fold of aggregate rows, in row (rank) order: sums of
     fields 0 and 3..7 accumulated one row after another, min of vmin, max of
     vmax (the combine of include/freedm_pf.h: fpf_aggregate_fold)."""
-    rows = np.asarray(rows, dtype=np.float64).reshape(-1, 8)
-    out = np.array([0.0, np.inf, -np.inf, 0.0, 0.0, 0.0, 0.0, 0.0])
-    for r in rows:
+    out = [0.0, np.inf, -np.inf, 0.0, 0.0, 0.0, 0.0, 0.0]
+    for r in np.asarray(rows, dtype=np.float64).reshape(-1, 8).tolist():
         out[0] += r[0]
         out[1] = min(out[1], r[1])
         out[2] = max(out[2], r[2])
-        out[3:] += r[3:]
-    return out
+        for q in range(3, 8):
+            out[q] += r[q]
+    return np.array(out)
 
 
 def aggregate_results(status, loss, vmin, vmax, lb_v: float = 0.96, ub_v: float = 1.05) -> np.ndarray:
@@ -94,16 +97,35 @@ def combine_aggregates(agg, group=None):
     return agg
 
 
-def timed_study(run_steps, study_aggregate, sync=None, group=None, clock=time.perf_counter):
+def timed_study(run_steps, study_aggregate, sync=None, group=None, clock=time.perf_counter, host=None):
     """The timed region of a sharded study (bench.py): the rank's solves, its
     study aggregate, then exactly one collective (gather_aggregates) and the
     rank-order fold.  The clock is read once the folded aggregate is on the host
     -- no barrier inside the region; the caller takes the max over ranks of the
-    elapsed times afterwards.  Returns (elapsed seconds, the folded aggregate)."""
+    elapsed times afterwards.  host: a pinned [world * 8] float64 tensor the rows
+    are copied into (one asynchronous copy, then sync(); else rows.cpu()).
+    Returns (elapsed seconds, the folded aggregate)."""
     t0 = clock()
     run_steps()
-    rows = gather_aggregates(study_aggregate(), group)
-    tot = fold_aggregates(rows.cpu().numpy())   # (waits for the rank's device work)
-    if sync is not None:
-        sync()
-    return clock() - t0, tot
+    t1 = clock()
+    agg = study_aggregate()
+    t2 = clock()
+    rows = gather_aggregates(agg, group)
+    t3 = clock()
+    if host is not None and rows.device.type != "cpu":
+        host.copy_(rows.reshape(-1), non_blocking=True)
+        if sync is not None:
+            sync()   # (waits for the rank's device work and the copy)
+        rh = host.numpy()
+    else:
+        rh = rows.cpu().numpy()   # (waits for the rank's device work)
+        if sync is not None:
+            sync()
+    t4 = clock()
+    tot = fold_aggregates(rh)
+    t5 = clock()
+    if TRACE:
+        print(f"timed_study: steps {1e6 * (t1 - t0):.1f} us, aggregate enqueue {1e6 * (t2 - t1):.1f}, gather "
+              f"{1e6 * (t3 - t2):.1f}, to host (waits) {1e6 * (t4 - t3):.1f}, fold {1e6 * (t5 - t4):.1f}",
+              file=sys.stderr, flush=True)
+    return t5 - t0, tot

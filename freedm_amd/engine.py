@@ -245,6 +245,23 @@ class PowerFlow:
         solve._keep = keep
         return solve, aggregate
 
+    def bind_aggregate(self, out: dict, agg, n_scen: int | None = None, stream=None):
+        """aggregate_device with its ctypes arguments bound once: a zero-argument
+        callable that enqueues the deterministic aggregate of `out` into `agg`."""
+        L = _lib.load()
+        B = int(out["loss"].shape[0]) if n_scen is None else int(n_scen)
+        st = C.c_void_p(None if stream is None else (stream if isinstance(stream, int) else int(stream.cuda_stream)))
+        args = (self.h, B, C.c_void_p(_ptr(out["status"])), C.c_void_p(_ptr(out["loss"])),
+                C.c_void_p(_ptr(out["vmin"])), C.c_void_p(_ptr(out["vmax"])), C.c_void_p(_ptr(agg)), st)
+        fa, ctx = L.fpf_aggregate_device, self.ctx
+
+        def aggregate():
+            rc = fa(*args)
+            if rc < 0:
+                raise DPFError(rc, ctx.err())
+        aggregate._keep = (out, agg)
+        return aggregate
+
     def aggregate_device(self, out: dict, agg, n_scen: int | None = None, stream=None) -> None:
         """Enqueue the deterministic batch aggregate of per-scenario device outputs."""
         L = _lib.load()
