@@ -14,7 +14,11 @@ rank r solves ids [r*4096, (r+1)*4096)).  One step = one pass of the hot path
 over that batch: one launch of libfreedm_pf's DPF kernel (the wave kernel in
 the default fast mode: all sweeps, V, per-scenario loss / Vmin / Vmax /
 iterations), inputs resident in HBM, per-scenario results kept for every
-step.  After the K timed steps the study aggregate over all K x 4096 results
+step.  The K steps go round robin onto two HIP streams (--streams): the
+batches are independent, so a launch starts on the CUs its predecessor's last
+workgroups free instead of waiting for the whole grid to drain (a 4096-scenario
+launch is one round of workgroups; measured 109 -> 125 M scenarios/s,
+profiles/r05c3).  After the K timed steps the study aggregate over all K x 4096 results
 is reduced once on each GPU (deterministic) and combined across GPUs by one
 RCCL all-gather folded in rank order (the only collective of the path and of
 the timed region: freedm_amd/dist.py timed_study); each rank reads its clock
@@ -22,8 +26,12 @@ right after it, and the max over ranks is taken outside the region.
 value = converged scenarios of all ranks / max-over-ranks wall time.
 
 Also reported: the roofline of the dominant kernel (algorithmic bytes per
-SURVEY.md 8(d) / its HIP-event time), and the CPU oracle (oracle/ref_dpf.c,
-a scalar port) timed on the host's cores on a bounded sample.
+SURVEY.md 8(d) / one launch's HIP-event time: with two streams the K launches
+are re-run back to back on one stream after the timed region for it, so that it
+is the kernel's own duration, as a rocprofv3 trace of --streams 1 reports it;
+the timed region's GPU time per launch is `kernel_ms_timed_region`), and the CPU
+oracle (oracle/ref_dpf.c, a scalar port) timed on the host's cores on a bounded
+sample.
 """
 from __future__ import annotations
 
@@ -608,8 +616,9 @@ def main():
                     help="distinct input batches the steps cycle through (0: enough for > 256 MiB of inputs, so "
                          "the Infinity Cache cannot hold them; 1: re-solve one batch)")
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 throughput leg of the config-2 run")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="launch the steps round robin on this many HIP streams (independent batches)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="launch the steps round robin on this many HIP streams (independent batches; "
+                         "measured: 2 beats 1 and 4, profiles/r05st)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -746,7 +755,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    avg_kern_s = ev0.elapsed_time(ev1) / args.steps / 1e3
+    # the GPU time per launch in the timed region (with S > 1 streams the launches
+    # overlap: a launch starts on the CUs the previous one's last workgroups free)
+    pipe_kern_s = ev0.elapsed_time(ev1) / args.steps / 1e3
+    avg_kern_s = pipe_kern_s
+    if S > 1:
+        # the roofline is the kernel's: one launch's own duration, the same K
+        # launches back to back on one stream after the timed region (what a
+        # rocprofv3 kernel trace of `--streams 1` reports per launch)
+        serial = [pf.bind_device(d_pqs[i % n_in], dict(v_out, **{k: t[i] for k, t in res.items()}), stream=stream)[0]
+                  for i in range(K)]
+        torch.cuda.synchronize(dev)
+        ev0.record(stream)
+        for i in range(args.steps):
+            serial[i]()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        avg_kern_s = ev0.elapsed_time(ev1) / args.steps / 1e3
     n_conv_all = float(tot[3])
     value = n_conv_all / elapsed
     nb, nn = pf.info["nb"], pf.nn
@@ -797,6 +822,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "model": model,
                          "bytes_alg_per_scenario": bytes_launch / B, "kernel_ms": avg_kern_s * 1e3,
+                         "kernel_ms_timed_region": pipe_kern_s * 1e3,
                          "fp64": {"achieved": fp64_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": fp64_tflops / FP64_PEAK_TFLOPS,
                                   "mean_sweeps": k_sum / (B * args.steps),

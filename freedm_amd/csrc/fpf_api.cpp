@@ -426,6 +426,10 @@ struct WaveHost {
     std::vector<double> temp;
     std::vector<double> lng, code_z;   // wave-block kernel: per slot lng, per code Zl (fpf_internal.h)
     std::vector<int32_t> code;
+    // the sequential-order plan (analyse_wave_lag): tables the tree plan declines
+    int has_lag = 0, nlag = 0;
+    std::vector<int32_t> lagx;    // [C][L] extra backward pair hi | lo << 9 | (V_prev store index + 1) << 18
+    std::vector<int32_t> bbase;   // [nblk] base of a block's chain: -1 V0, else the V_prev entry
 };
 
 // The tables of the paired wave-block kernel (fpf_wcoop.hip, 2049..4096
@@ -535,9 +539,256 @@ static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps
     w.ok = true;
 }
 
+// Tables of the wave kernel for the Dl tables the tree plan above declines -- a
+// lateral block listed before its tap's row, a block whose rows do not chain
+// (row m + 1 not starting at row m's receiving bus), a branch fed from a node
+// whose row comes later -- which the reference solves with its sequential
+// semantics (DPF_return7.cpp:134-195).  Two forests over the nodes, both
+// following row order:
+//   * backward (:134-160): Ibl flows from row m + 1 to row m inside a block, so
+//     row m's node is the P-parent of row m + 1's node; a block head hangs off its
+//     tap t = sbus(head) when the separator before it is processed before t's row
+//     (t's row comes earlier: Ib(t) takes the block's total and hands it up); else
+//     the block's total is added to Ib(t) after t's row was processed ("post-add":
+//     Ib(t) alone takes it) and the head is a P-root.  With every P-subtree a
+//     contiguous range of a depth-first order, Ib(k) = Einc[last(k)] - Eexc[pos(k)]
+//     plus, at a post-add target, one more such difference over its detached trees
+//     (laid out one after another);
+//   * forward (:163-195): V(r_m) = V(sbus_m) - drop_m with V(sbus_m) of this sweep
+//     when sbus_m's row comes earlier ("new"), of the previous sweep otherwise
+//     (V_prev, "old"; V0 for the substation and row 0).  The forward paths are cut
+//     into F-segments, runs of consecutive positions each fed by the one before;
+//     a segment's base is V at its F-parent (a block-offset chain of Ginc pairs, as
+//     the tree plan's blocks) or, at an F-root, V0 or V_prev of its source -- which
+//     the slot holding that source stores into LDS at the top of every sweep.
+// Zeroed phases are declined (the generic kernel runs those tables); the loss
+// then takes the reference's PQb / PQL form (the kernel's FULL variant).
+void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_why) {
+    auto no = [&](const std::string &why) { w.ok = false; w.why = tree_why + "; sequential-order plan: " + why; };
+    if (getenv("FPF_NO_WAVE_LAG")) return no("disabled (FPF_NO_WAVE_LAG)");
+    const int nl = h.nl, nn = h.nn, n = nn - 1;
+    int spw = 0, C = 0;
+    if (!wave_geometry(n, &spw, &C)) return no("more than 256 branches");
+    const int L = 64 / spw;
+    std::vector<int> row_of(nn, -1), fw_of(nn, -1);
+    {
+        int fwi = 0;
+        for (int m = 0; m < nl; ++m) {
+            if (h.at(m, 0) == 0) continue;
+            const double rb = h.at(m, 2), sb = h.at(m, 1);
+            if (rb != std::floor(rb) || sb != std::floor(sb) || !(h.at(m, 0) >= 1) || h.at(m, 0) != std::floor(h.at(m, 0)))
+                return no("fractional bus or branch number");
+            const int k = (int)rb, src = (int)sb;
+            if (k < 1 || k >= nn) return no("rbus outside 1..nn-1");
+            if (row_of[k] >= 0) return no("duplicate rbus");
+            if (m == 0 && k != 1) return no("row 0 is not a branch to node 1");
+            if (m > 0 && (src < 0 || src >= nn)) return no("sbus outside 0..nn-1");
+            row_of[k] = m;
+            fw_of[k] = fwi++;
+        }
+        for (int k = 1; k < nn; ++k)
+            if (row_of[k] < 0) return no("node without a branch row");
+        for (int k = 1; k < nn; ++k)
+            if (h.fw[fw_of[k]].mask & 7) return no("zeroed phases");
+    }
+    // P-forest (backward) and F-forest (forward)
+    std::vector<int> ppar(nn, -1), post(nn, -1), fpar(nn, -1), fsrc(nn, 0);   // fsrc: an F-root's source (0: V0)
+    std::vector<int> chain(nn, -1);
+    std::vector<std::vector<int>> lat(nn), detached(nn);
+    for (int m = 0; m < nl; ++m) {
+        if (h.at(m, 0) == 0) continue;
+        const int k = (int)h.at(m, 2);
+        if (m == 0) {
+            fsrc[k] = 0;   // V(1) = V0 - drop (:163-168)
+        } else {
+            const int sb = (int)h.at(m, 1);
+            if (sb == 0) fsrc[k] = 0;                       // V(0) is never written: V0
+            else if (row_of[sb] < m) fpar[k] = sb;          // this sweep's V(sbus)
+            else fsrc[k] = sb;                              // the previous sweep's
+            if (h.at(m - 1, 0) != 0) {
+                const int pk = (int)h.at(m - 1, 2);
+                ppar[k] = pk;
+                chain[pk] = k;
+            } else {
+                const int t = sb;   // the separator at m - 1 adds into Ib(sbus(m)) (:138-146)
+                if (row_of[t] < m - 1) {
+                    ppar[k] = t;
+                    lat[t].push_back(k);
+                } else {
+                    post[k] = t;
+                    detached[t].push_back(k);
+                }
+            }
+        }
+    }
+    // depth-first order of the P-forest: node 1's tree, then the detached trees
+    // grouped by their post-add target (one range per target)
+    std::vector<int> pos(nn, -1), at, size(nn, 1);
+    std::vector<int> lo_t(nn, -1), hi_t(nn, -1);
+    auto dfs = [&](int root) {
+        std::vector<int> st = {root};
+        while (!st.empty()) {
+            const int k = st.back();
+            st.pop_back();
+            pos[k] = (int)at.size();
+            at.push_back(k);
+            for (int l : lat[k]) st.push_back(l);
+            if (chain[k] >= 0) st.push_back(chain[k]);
+        }
+    };
+    dfs(1);
+    for (int t = 1; t < nn; ++t) {
+        if (detached[t].empty()) continue;
+        lo_t[t] = (int)at.size();
+        for (int hd : detached[t]) dfs(hd);
+        hi_t[t] = (int)at.size() - 1;
+    }
+    if ((int)at.size() != n) return no("the backward structure does not reach every node");
+    for (int q = n - 1; q > 0; --q)
+        if (ppar[at[q]] >= 1) size[ppar[at[q]]] += size[at[q]];
+    // F-segments: runs of positions each fed (this sweep) by the one before
+    std::vector<int> blk(n, 0), bfirst;
+    for (int q = 0; q < n; ++q) {
+        if (q == 0 || fpar[at[q]] != at[q - 1]) bfirst.push_back(q);
+        blk[q] = (int)bfirst.size() - 1;
+    }
+    const int nblk = (int)bfirst.size();
+    if (nblk > 511) return no("too many forward segments");
+    // V_prev sources
+    std::vector<int> lagid(nn, -1);
+    int nlag = 0;
+    for (int b = 0; b < nblk; ++b) {
+        const int hd = at[bfirst[b]];
+        if (fpar[hd] < 0 && fsrc[hd] > 0 && lagid[fsrc[hd]] < 0) lagid[fsrc[hd]] = nlag++;
+    }
+    if (nlag > 64) return no("too many sources of the previous sweep");
+    // gathered positions: backward = P-subtree ends; forward = F-parents of
+    // segment heads and the positions before segment heads
+    std::vector<int> cb(n, -1), cf(n, -1);
+    int nb_c = 0, nf_c = 0;
+    for (int q = 0; q < n; ++q) {
+        const int e = q + size[at[q]] - 1;
+        if (cb[e] < 0) cb[e] = nb_c++;
+    }
+    auto needf = [&](int q) { if (cf[q] < 0) cf[q] = nf_c++; };
+    for (int b = 1; b < nblk; ++b) {
+        const int hd = at[bfirst[b]];
+        if (fpar[hd] >= 0) needf(pos[fpar[hd]]);
+        needf(bfirst[b] - 1);
+    }
+    const bool off_in_x = false;
+    const int ncomp = std::max(std::max(nb_c, nf_c), 1);
+    if (ncomp > 510) return no("too many gathered positions");
+    // block chains: (F-parent, head - 1) per level up to a root segment,
+    // (zero, head - 1) for a root segment past position 0, and its base
+    std::vector<std::vector<std::pair<int, int>>> chainp(nblk);
+    std::vector<int32_t> bbase(nblk, -1);
+    int bdepth = 0;
+    for (int b = 1; b < nblk; ++b) {
+        int cur = b, guard = 0;
+        while (true) {
+            const int hq = bfirst[cur], hd = at[hq];
+            if (fpar[hd] >= 0) {
+                chainp[b].push_back({cf[pos[fpar[hd]]], cf[hq - 1]});
+                cur = blk[pos[fpar[hd]]];
+            } else {
+                if (hq > 0) chainp[b].push_back({ncomp, cf[hq - 1]});
+                bbase[b] = fsrc[hd] > 0 ? lagid[fsrc[hd]] : -1;
+                break;
+            }
+            if (++guard > nn) return no("forward chain does not end");
+        }
+        bdepth = std::max(bdepth, (int)chainp[b].size());
+    }
+    w.pairs.assign((size_t)std::max(bdepth, 1) * 2 * nblk, ncomp);
+    for (int b = 1; b < nblk; ++b)
+        for (size_t j = 0; j < chainp[b].size(); ++j) {
+            w.pairs[(2 * j) * nblk + b] = chainp[b][j].first;
+            w.pairs[(2 * j + 1) * nblk + b] = chainp[b][j].second;
+        }
+    const size_t S = (size_t)C * L;
+    w.row.assign(S, -1);
+    w.node.assign(S, -1);
+    w.info.assign(S, (ncomp << 13));
+    w.blk.assign(S, 0);
+    w.mref.assign(3 * S, -1);
+    w.temp.assign(9 * S * 2, 0.0);
+    w.lagx.assign(S, ncomp | (ncomp << 9));
+    for (int q = 0; q < n; ++q) {
+        const int k = at[q], c = q % C, lane = q / C, i = c * L + lane;
+        w.row[i] = row_of[k];
+        w.node[i] = k;
+        w.info[i] = (int32_t)((uint32_t)(8 | ((cb[q] + 1) << 4) | (cb[q + size[k] - 1] << 13) | ((cf[q] + 1) << 22)));
+        w.blk[i] = blk[q];
+        int hi = ncomp, lo = ncomp;
+        if (lo_t[k] >= 0) {
+            hi = cb[hi_t[k]];
+            lo = cb[lo_t[k] - 1];
+        }
+        w.lagx[i] = hi | (lo << 9) | ((lagid[k] + 1) << 18);
+        for (int j = 0; j < 9; ++j) {
+            w.temp[((j * C + c) * L + lane) * 2 + 0] = h.tz[(size_t)fw_of[k] * 18 + 2 * j];
+            w.temp[((j * C + c) * L + lane) * 2 + 1] = h.tz[(size_t)fw_of[k] * 18 + 2 * j + 1];
+        }
+    }
+    bool sym = !getenv("FPF_WAVE_NO_SYM");
+    for (int q = 0; q < n && sym; ++q) {
+        const double *t = &h.tz[(size_t)fw_of[at[q]] * 18];
+        for (int j = 1; j < 9 && sym; ++j)
+            if (j % 4 != 0) sym = t[2 * j] == t[2] && t[2 * j + 1] == t[3];
+    }
+    if (sym) {
+        std::vector<double> ts(4 * S * 2, 0.0);
+        for (int q = 0; q < n; ++q) {
+            const int c = q % C, lane = q / C;
+            const double *t = &h.tz[(size_t)fw_of[at[q]] * 18];
+            for (int a = 0; a < 3; ++a) {
+                ts[((a * C + c) * L + lane) * 2 + 0] = t[2 * (4 * a)] - t[2];
+                ts[((a * C + c) * L + lane) * 2 + 1] = t[2 * (4 * a) + 1] - t[3];
+            }
+            ts[((3 * C + c) * L + lane) * 2 + 0] = t[2];
+            ts[((3 * C + c) * L + lane) * 2 + 1] = t[3];
+        }
+        w.temp.swap(ts);
+    }
+    w.temp_sym = sym ? 1 : 0;
+    w.bbase = bbase;
+    w.n = n;
+    w.spw = spw;
+    w.C = C;
+    w.nblk = nblk;
+    w.bdepth = bdepth;
+    w.ncomp = ncomp;
+    w.has_rel = 0;
+    w.has_mask = 0;
+    w.off_in_x = off_in_x ? 1 : 0;
+    w.wps = 0;
+    w.has_lag = 1;
+    w.nlag = nlag;
+    WaveDev probe{};
+    probe.spw = spw;
+    probe.C = C;
+    probe.nl = nl;
+    probe.nblk = nblk;
+    probe.bdepth = bdepth;
+    probe.ncomp = ncomp;
+    probe.off_in_x = 0;
+    probe.temp_sym = w.temp_sym;
+    probe.nlag = nlag;
+    const int big = spw * C <= 2 ? 16 : 8, small = big / 2;
+    auto lds_at = [&](int wpb) { probe.wpb = wpb; return wave_lds_bytes(probe); };
+    int wpb = 0;
+    if (lds_at(big) <= WAVE_LDS_BUDGET) wpb = big;
+    else if (lds_at(small) <= WAVE_LDS_BUDGET) wpb = small;
+    else return no("per-scenario LDS above the budget");
+    w.wpb = wpb;
+    w.wpb_big_batch = (spw * C > 2 && 2 * (lds_at(small) + 1024) <= 160 * 1024) ? small : wpb;
+    w.ok = true;
+}
+
 void analyse_wave(const HostFeeder &h, WaveHost &w) {
     auto no = [&](const std::string &why) { w.ok = false; w.why = why; };
-    if (!h.wf) return no("not well formed: " + h.wf_why);
+    if (!h.wf) return analyse_wave_lag(h, w, "not well formed: " + h.wf_why);
     const int nl = h.nl, nn = h.nn, n = nn - 1;
     int spw = 0, C = 0, wps = 0, coop = 0;
     if (!wave_geometry(n, &spw, &C)) {
@@ -561,7 +812,7 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
         if (m == 0) continue;
         if (h.at(m - 1, 0) != 0) {
             if ((int)h.at(m - 1, 2) != src)
-                return no("row " + std::to_string(m) + ": the backward chain leaves the feeder tree");
+                return analyse_wave_lag(h, w, "row " + std::to_string(m) + ": the backward chain leaves the feeder tree");
             chain[src] = k;
         } else {
             lat[src].push_back(k);
@@ -1469,6 +1720,7 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         const size_t o_tmp = push_blob(wb, wh.temp), o_pairs = push_blob(wb, wh.pairs);
         const size_t o_lng = push_blob(wb, wh.lng), o_code = push_blob(wb, wh.code), o_cz = push_blob(wb, wh.code_z);
         const size_t o_info2 = push_blob(wb, wh.info2);
+        const size_t o_lagx = push_blob(wb, wh.lagx), o_bbase = push_blob(wb, wh.bbase);
         e = hipMalloc(&f->d_wave, wb.size());
         if (e == hipSuccess) e = hipMemcpy(f->d_wave, wb.data(), wb.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
@@ -1511,6 +1763,10 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         w.slot_lng = (const double *)(wbase + o_lng);
         w.slot_code = (const int32_t *)(wbase + o_code);
         w.code_z = (const double *)(wbase + o_cz);
+        w.has_lag = wh.has_lag;
+        w.nlag = wh.nlag;
+        w.slot_lagx = (const int32_t *)(wbase + o_lagx);
+        w.blk_base = (const int32_t *)(wbase + o_bbase);
         if (wh.coop) {
             // the paired kernel's exchange areas (one per scenario in flight) and
             // their arrival counts / generations (zeroed before every launch)
@@ -1746,7 +2002,8 @@ extern "C" int fpf_feeder_reserve(fpf_feeder *f, int max_scen) {
     // built here rather than inside the first solve (fpf_rtc.cpp: wave_rtc_function)
     if (kernel_for(f, max_scen) == FPF_KERNEL_WAVE && max_scen >= wave_rtc_min()) {
         const WaveDev &w = wave_dev_for(f, max_scen);
-        if (w.spec && !w.coop && !w.has_mask && !(w.wps && w.has_rel)) (void)wave_rtc_function(ctx->device, w, false);
+        if (w.spec && !w.coop && !w.has_mask && !w.has_lag && !(w.wps && w.has_rel))
+            (void)wave_rtc_function(ctx->device, w, false);
     }
     const bool need_scratch = kernel_for(f, max_scen) == FPF_KERNEL_GENERIC;
     if (max_scen <= f->cap) {

@@ -171,6 +171,12 @@ struct WaveDev {
     // writes its own V (out_uw elements per lane of out_smaj) -- no workgroup
     // barrier waits for the slowest wave's loads or sweeps; 0: the workgroup's IO
     int32_t stage_uw, out_uw;
+    // the sequential-order plan (fpf_api.cpp: analyse_wave_lag; FULL variant only):
+    // per slot the extra backward pair of a post-add target and the index of the
+    // previous sweep's V the slot stores (slot_lagx: hi | lo << 9 | (index + 1) << 18),
+    // per block its chain's base (blk_base: -1 V0, else that index); nlag entries
+    int32_t has_lag, nlag;
+    const int32_t *slot_lagx, *blk_base;
     double rv0[3];              // 1/|V0_p|^2 (the flat start's first load currents)
     // wave-block kernel (fpf_wblk.hip): one scenario per workgroup of wps
     // wavefronts (L = 64 wps lanes, C slots per lane) for feeders of 257..2048

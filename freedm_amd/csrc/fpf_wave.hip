@@ -59,7 +59,7 @@ int wave_out_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<in
     const int ntot = spb * 3 * nn, U = (ntot + nt - 1) / nt;
     if (U > WAVE_STAGE_U || (spb & (spb - 1))) return 0;
     const int pstr = (swz_row(nl) + 1) * srow, xc = w.ncomp + 1, noff = w.off_in_x ? 0 : 3 * w.nblk;
-    const int rs = (3 * xc + noff + 4 + REGION_EXTRA) | 1;
+    const int rs = (3 * xc + noff + 4 + REGION_EXTRA + 3 * w.nlag) | 1;
     auto at = [&](int j, int p, int k) { return k == 0 ? 3 * pstr + j * rs + 3 * xc + noff + p : p * pstr + swz_row(k - 1) * srow + j; };
     smaj.assign((size_t)U * nt, 0);
     l0.assign((size_t)U * nt, 0);
@@ -107,7 +107,7 @@ void wave_io_units(WaveDev &w) {
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
-    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4 + REGION_EXTRA) | 1);
+    const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4 + REGION_EXTRA + 3 * (size_t)w.nlag) | 1);
     const size_t stage = 16 * 3 * ((size_t)swz_row(w.nl) + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
     const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
@@ -142,7 +142,7 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     const size_t lds = wave_lds_bytes(w);
     // FULL keeps IL and Ib of the last sweep for Vpolar/PQb/PQL, and for the
     // loss of a feeder with zeroed phases (reference formula over PQL)
-    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask;
+    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask || w.has_lag;   // (the sequential-order plan: FULL only)
     WaveKernel k = nullptr;
     int id = -1;
     if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, w.wpb); id = 0; }

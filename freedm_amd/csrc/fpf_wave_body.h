@@ -163,7 +163,8 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     double2 *const stg = (double2 *)(knode + C * L);
     double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
-    const int RS = (3 * XC + noff + 4 + REGION_EXTRA) | 1;           // double2 per region (+ the guard record)
+    const int NLAG = FULL ? f.nlag : 0;                              // (the sequential-order plan: V_prev entries)
+    const int RS = (3 * XC + noff + 4 + REGION_EXTRA + 3 * NLAG) | 1;  // double2 per region (+ the guard record)
     double2 *const X = reg0 + sc * RS;
     double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
     // block offsets [3][OS]: over X's first nblk entries when off_in_x (every
@@ -458,6 +459,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     }
     if (li < 3) X[li * XC + XC - 1] = make_double2(0.0, 0.0);
     double2 *const IBO = X + 3 * XC + noff + 4;   // (FPF_WAVE_IBO_LDS) Ibo per phase
+    double2 *const LAGV = IBO + REGION_EXTRA;       // [3][nlag] V of the previous sweep (sequential-order plan)
     if (FPF_WAVE_IBO_LDS && li < 3) IBO[li] = make_double2(0.0, 0.0);
     // per-scenario results for the workgroup aggregate: [sc][loss, vmin, vmax, status]
     __shared__ double res[SPB][4];
@@ -532,6 +534,19 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
     for (int p = 0; p < 3; ++p) slp[p] = FPF_WAVE_SLD_PREF ? ldx(stg, p * PSTR + sb[0]) : mk(0, 0);
     for (int it = 0; __ballot(!done) != 0; ++it) {
+        if (FULL && f.has_lag) {
+            // (the sequential-order plan) the sources read before their own rows
+            // (:176-178 with sbus's row later) see the previous sweep's V: stored
+            // here, before this sweep updates it
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int lg = (f.slot_lagx[c * L + li] >> 18) - 1;
+                if (lg >= 0) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(LAGV, p * NLAG + lg, v[c][p]);
+                }
+            }
+        }
         WSTAMP(4 + 8 * it);
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
@@ -633,6 +648,22 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 ib[c][p] = csub(ldx(X, p * XC + si_last(si[c])), eprev);
                 eprev = e;
             }
+        }
+        if (FULL && f.has_lag) {
+            // (the sequential-order plan) a post-add target also takes its detached
+            // trees' totals (:138-146 after its own row), then node 1's Ib decides
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int lx = f.slot_lagx[c * L + li], hi = lx & 511, lo = (lx >> 9) & 511;
+                if (hi != lo) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        ib[c][p] = cadd(ib[c][p], csub(ldx(X, p * XC + hi), ldx(X, p * XC + lo)));
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p)   // node 1 is position 0: slot 0 of the segment's lane 0
+                tot[p] = mk(__shfl(ib[0][p].re, seg * L, 64), __shfl(ib[0][p].im, seg * L, 64));
         }
 
         WSTAMP(6 + 8 * it);
@@ -800,8 +831,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                             of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
                     }
                 }
+                const int bb = (FULL && f.has_lag) ? f.blk_base[li] : -1;   // (sequential-order plan: V_prev base)
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(ldx(V0S, p), of[p]));
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
             }
         } else {
             for (int b = li; b < nblk; b += L) {
@@ -811,8 +843,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
+                const int bb = (FULL && f.has_lag) ? f.blk_base[b] : -1;
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(ldx(V0S, p), of[p]));
+                for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
             }
         }
         wfence();
@@ -889,7 +922,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     mx = fmax(mx, m2);
                 }
             }
-            if (!FULL || !f.has_mask) {   // (the host runs FULL for any feeder with zeroed phases)
+            if (!FULL || !(f.has_mask || f.has_lag)) {   // (the host runs FULL for zeroed phases and the sequential-order plan)
                 // every Lnum_p + 1 = Nn: V_abc_list keeps every row, so the extremes are
                 // plain min/max; loss = s3 sum Re(drop conj(Ib))
                 x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
@@ -912,7 +945,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 x -= sl;
                 mn = INFINITY;
                 mx = -INFINITY;
-                const unsigned long long segbits = L == 64 ? ~0ull : ((1ull << L) - 1ull) << (seg * L);
+                const unsigned long long segbits = L == 64 ? ~0ull : ((1ull << (L & 63)) - 1ull) << (seg * L);
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     const int K = f.K[p];

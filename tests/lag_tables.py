@@ -1,0 +1,57 @@
+"""Dl tables the reference solves with its sequential semantics but whose rows
+do not follow the feeder tree (DPF_return7.cpp:134-195): a block listed before
+its tap's row, rows inside a block that do not chain, a branch fed from a node
+whose row comes later.  Shared by tests/test_lag_plan.py (CPU: the plan) and
+tests/test_gpu_lag.py (GPU: the fast kernel against the oracle)."""
+import numpy as np
+
+from freedm_amd import feeder as F
+
+
+def units(Dl):
+    """Block 0 (rows up to the first separator) and the [separator + block] units."""
+    sep = [i for i in range(Dl.shape[0]) if Dl[i, 0] == 0]
+    cut = [0] + sep + [Dl.shape[0]]
+    first = Dl[:cut[1]]
+    rest = [Dl[cut[i]:cut[i + 1]] for i in range(1, len(cut) - 1)]
+    return first, rest
+
+
+def shuffled_blocks(f, seed):
+    """The feeder's lateral units in a seeded order: laterals land before their
+    taps' rows (their totals are added after the tap's row; V of the tap is the
+    previous sweep's)."""
+    first, rest = units(f.Dl)
+    order = np.random.default_rng(seed).permutation(len(rest))
+    return F.Feeder(np.vstack([first] + [rest[i] for i in order]), f.Z, name=f"{f.name}-shuffled{seed}")
+
+
+def reversed_blocks(f):
+    """Every lateral unit after the last one that taps it... simply all units reversed."""
+    first, rest = units(f.Dl)
+    return F.Feeder(np.vstack([first] + rest[::-1]), f.Z, name=f"{f.name}-reversed")
+
+
+def swapped_rows(f, seed, n_swaps=3):
+    """Adjacent rows swapped inside blocks: the backward Ibl chain leaves the tree
+    and the forward sweep reads a source before its own row."""
+    Dl = f.Dl.copy()
+    rng = np.random.default_rng(seed)
+    cand = [i for i in range(1, Dl.shape[0] - 1) if Dl[i, 0] != 0 and Dl[i + 1, 0] != 0]
+    for i in rng.choice(cand, size=min(n_swaps, len(cand)), replace=False):
+        Dl[[i, i + 1]] = Dl[[i + 1, i]]
+    return F.Feeder(Dl, f.Z, name=f"{f.name}-swapped{seed}")
+
+
+def reordered_demo():
+    f = F.demo_feeder()
+    return F.Feeder(f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy(), f.Z, name="demo-reordered")
+
+
+def cases():
+    f123 = F.synthetic_feeder(123, 123)
+    f60 = F.synthetic_feeder(60, 60)
+    return {"demo-reordered": reordered_demo(), "123-shuffled1": shuffled_blocks(f123, 1),
+            "123-shuffled2": shuffled_blocks(f123, 2), "123-reversed": reversed_blocks(f123),
+            "123-swapped": swapped_rows(f123, 5), "60-shuffled-swapped": swapped_rows(shuffled_blocks(f60, 3), 7),
+            "200-shuffled-swapped": swapped_rows(shuffled_blocks(F.synthetic_feeder(200, 200), 4), 9)}

@@ -165,13 +165,12 @@ def test_auto_kernel_choice():
     assert _pf(g4["Dl"], g4["Z"], exact=1).kernel == "generic"   # exact: above the tiled kernel's size, tile 1
     f = F.demo_feeder()
     Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # 2->3 before 1->2: legal for the reference, not well formed
-    pf = _pf(Dl, f.Z)
-    assert pf.kernel == "generic" and pf.info["well_formed"] == 0
+    pf = _pf(Dl, f.Z)                                   # fast mode: the wave kernel's sequential-order plan
+    assert pf.kernel == "wave" and pf.info["well_formed"] == 0
+    assert _pf(Dl, f.Z, exact=1).kernel == "generic"    # exact mode: the generic kernel
     from freedm_amd import DPFError
     with pytest.raises(DPFError):
         _pf(Dl, f.Z, kernel="tiled")
-    with pytest.raises(DPFError):
-        _pf(Dl, f.Z, kernel="wave")
     with pytest.raises(DPFError):
         _pf(g["Dl"], g["Z"], kernel="wave", exact=1)
 
@@ -181,11 +180,14 @@ def test_malformed_order_matches_oracle():
     f = F.demo_feeder()
     Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()     # forward reads V(2) of the previous sweep
     pq = F.scenario_loads(F.Feeder(Dl, f.Z), np.arange(40))
-    r = _pf(Dl, f.Z).solve(pq)
+    r = _pf(Dl, f.Z, exact=1).solve(pq)                # the generic kernel: the oracle's bits
     c = O.dpf_batch(Dl, f.Z, pq, nthreads=4)
     assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
     np.testing.assert_array_equal(r["V_re"], c["V_re"])
     np.testing.assert_array_equal(r["V_im"], c["V_im"])
+    r = _pf(Dl, f.Z).solve(pq)                          # fast mode: the wave kernel (tests/test_gpu_lag.py)
+    assert (r["iters"] == c["iters"]).all() and (r["status"] == c["status"]).all()
+    assert _vrel(r["V_re"], r["V_im"], c["V_re"], c["V_im"]) <= 1e-10
 
 
 @pytest.mark.parametrize("spec", [False, True], ids=["interp", "rtc"])
