@@ -567,9 +567,13 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
     auto no = [&](const std::string &why) { w.ok = false; w.why = tree_why + "; sequential-order plan: " + why; };
     if (getenv("FPF_NO_WAVE_LAG")) return no("disabled (FPF_NO_WAVE_LAG)");
     const int nl = h.nl, nn = h.nn, n = nn - 1;
-    int spw = 0, C = 0;
-    if (!wave_geometry(n, &spw, &C)) return no("more than 256 branches");
-    const int L = 64 / spw;
+    int spw = 0, C = 0, wps = 0;
+    if (!wave_geometry(n, &spw, &C)) {
+        // one scenario per workgroup of wps wavefronts (fpf_wblk.hip, up to 2048 branches)
+        if (!wblk_geometry(n, &wps, &C)) return no("more than 2048 branches");
+        spw = 1;
+    }
+    const int L = wps ? 64 * wps : 64 / spw;
     std::vector<int> row_of(nn, -1), fw_of(nn, -1);
     {
         int fwi = 0;
@@ -661,7 +665,7 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
         const int hd = at[bfirst[b]];
         if (fpar[hd] < 0 && fsrc[hd] > 0 && lagid[fsrc[hd]] < 0) lagid[fsrc[hd]] = nlag++;
     }
-    if (nlag > 64) return no("too many sources of the previous sweep");
+    if (nlag > (wps ? 1024 : 64)) return no("too many sources of the previous sweep");
     // gathered positions: backward = P-subtree ends; forward = F-parents of
     // segment heads and the positions before segment heads
     std::vector<int> cb(n, -1), cf(n, -1);
@@ -752,6 +756,32 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
         w.temp.swap(ts);
     }
     w.temp_sym = sym ? 1 : 0;
+    if (wps) {
+        // TEMP = lng * Zl(code), factorised as the tree plan's wave-block tables
+        w.temp.clear();
+        w.lng.assign(S, 0.0);
+        w.code.assign(S, 0);
+        bool zsym = !getenv("FPF_WAVE_NO_SYM");
+        for (int q = 0; q < n; ++q) {
+            const int k = at[q], i = (q % C) * L + q / C;
+            w.lng[i] = h.at(row_of[k], 4);
+            w.code[i] = h.fw[fw_of[k]].code;
+            const cx *z = &h.zl[(size_t)w.code[i] * 9];
+            for (int j = 1; j < 9 && zsym; ++j)
+                if (j % 4 != 0) zsym = z[j].re == z[1].re && z[j].im == z[1].im;
+        }
+        const int ntz = zsym ? 4 : 9;
+        w.code_z.assign((size_t)h.ncode * ntz * 2, 0.0);
+        for (int cd = 0; cd < h.ncode; ++cd) {
+            const cx *z = &h.zl[(size_t)cd * 9];
+            for (int j = 0; j < ntz; ++j) {
+                const cx v = !zsym ? z[j] : (j < 3 ? csub(z[4 * j], z[1]) : z[1]);
+                w.code_z[((size_t)cd * ntz + j) * 2] = v.re;
+                w.code_z[((size_t)cd * ntz + j) * 2 + 1] = v.im;
+            }
+        }
+        w.temp_sym = zsym ? 1 : 0;
+    }
     w.bbase = bbase;
     w.n = n;
     w.spw = spw;
@@ -762,9 +792,24 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
     w.has_rel = 0;
     w.has_mask = 0;
     w.off_in_x = off_in_x ? 1 : 0;
-    w.wps = 0;
+    w.wps = wps;
     w.has_lag = 1;
     w.nlag = nlag;
+    if (wps) {
+        WaveDev probe{};
+        probe.wps = wps;
+        probe.nl = nl;
+        probe.nblk = nblk;
+        probe.bdepth = bdepth;
+        probe.ncomp = ncomp;
+        probe.temp_sym = w.temp_sym;
+        probe.ncode = h.ncode;
+        probe.nlag = nlag;
+        if (wblk_lds_bytes(probe) > WAVE_LDS_BUDGET) return no("wave-block kernel: the scenario's loads exceed LDS");
+        w.wpb = w.wpb_big_batch = wps;
+        w.ok = true;
+        return;
+    }
     WaveDev probe{};
     probe.spw = spw;
     probe.C = C;

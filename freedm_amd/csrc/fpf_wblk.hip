@@ -46,7 +46,7 @@ namespace fpf {
 size_t wblk_lds_bytes(const WaveDev &w) {
     const size_t ntz = w.temp_sym ? 4 : 9, xc = (size_t)w.ncomp + 1, nt = 64 * (size_t)w.wps;
     const size_t zc = 16 * (size_t)w.ncode * ntz;
-    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk * (w.has_rel ? 2 : 1) + 4) +
+    const size_t rest = 16 * (3 * ((size_t)w.nl + 1) + 3 * xc + 3 * (size_t)w.nblk * (w.has_rel ? 2 : 1) + 4 + 3 * (size_t)w.nlag) +
                         8 * 16 * (size_t)w.wps + 64 +
                         4 * 2 * (size_t)w.bdepth * w.nblk;
     return zc + std::max(rest, 8 * 8 * nt);   // the last workgroup's fold reuses the space after zc
@@ -80,7 +80,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
     // PQL), and the zeroed-phase paths
     // (the tables of a feeder with a live phase below a zeroed one are built for
     // the segmented forward scan: fpf_api.cpp analyse_wave)
-    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask, seg = w.has_rel != 0;
+    const bool full = o.vpolar || o.pqb || o.pql || w.has_mask || w.has_lag, seg = w.has_rel != 0;   // (has_lag: FULL only)
     WblkKernel k = nullptr;
     if (w.C == WB_C)
         k = w.wps == 2 ? pick_wblk<2, WB_C>(full, seg)

@@ -90,7 +90,9 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double2 *const OFF = X + 3 * XC;
     double2 *const OFFA = OFF + 3 * nblk;   // [3][nblk] off(b) itself (has_rel only)
     double2 *const V0S = OFF + 3 * nblk * (f.has_rel ? 2 : 1);
-    double *const wtb = (double *)(V0S + 4);
+    const int NLAG = FULL ? f.nlag : 0;              // (the sequential-order plan: V_prev entries)
+    double2 *const LAGV = V0S + 4;                   // [3][nlag]
+    double *const wtb = (double *)(V0S + 4 + 3 * NLAG);
     double *const wtf = wtb + 8 * W;
     double *const vx = wtf + 8 * W;             // [3][2] per-phase Vmin / Vmax (zeroed phases)
     int *const pairs = (int *)(vx + 8);         // [bdepth][2][nblk]
@@ -239,6 +241,19 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double dmin = INFINITY;  // closest |err2 - eps^2| of a decision in the guard's coarse band
     double err2_last = 0.0;
     for (;; ++it) {
+        if (FULL && f.has_lag) {
+            // (the sequential-order plan, fpf_api.cpp: analyse_wave_lag) the sources
+            // read before their own rows see the previous sweep's V, stored here
+            // before this sweep updates it (read after the barriers below)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int lg = (f.slot_lagx[c * L + tid] >> 18) - 1;
+                if (lg >= 0) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) stx(LAGV, p * NLAG + lg, v[c][p]);
+                }
+            }
+        }
         BSTAMP_IT(0);
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
@@ -313,6 +328,30 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 ib[c][p] = csub(ldx(X, p * XC + si_last(si[c])), eprev);
                 eprev = e;
             }
+        }
+        if (FULL && f.has_lag) {
+            // (the sequential-order plan) a post-add target also takes its detached
+            // trees' totals; node 1's Ib (position 0: thread 0's slot 0) decides
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int lx = f.slot_lagx[c * L + tid], hi = lx & 511, lo = (lx >> 9) & 511;
+                if (hi != lo) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        ib[c][p] = cadd(ib[c][p], csub(ldx(X, p * XC + hi), ldx(X, p * XC + lo)));
+                }
+            }
+            double *const ib1 = wtf + 8 * W;   // (the per-phase extremes' slot: free until after the loop)
+            if (tid == 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    ib1[2 * p] = ib[0][p].re;
+                    ib1[2 * p + 1] = ib[0][p].im;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < 3; ++p) tot[p] = mk(ib1[2 * p], ib1[2 * p + 1]);
         }
 
         BSTAMP_IT(2);
@@ -442,7 +481,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     for (int j = 0; j < WB_BD; ++j)
                         if (j < bdepth) of = cadd(of, ldx(X, op3 * XC + (bp[j] & 0xffff)));   // uniform bound
                     stx(OFF, op3 * nblk + ob3, csub(ldx(V0S, op3), of));
-                    if (FULL && f.has_rel) stx(OFFA, op3 * nblk + ob3, of);
+                    if (FULL && f.has_rel) stx(OFFA, op3 * nblk + ob3, of);   // (has_rel: never with has_lag)
                 }
             } else if (chain_regs) {
                 if (tid < nblk) {
@@ -549,7 +588,8 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     for (int j = 0; j < WB_BD; ++j)
                         if (j < bdepth)   // uniform; levels past a chain's depth read the zero entry
                             of = cadd(of, csub(ldx(X, op3 * XC + (bp[j] & 0xffff)), ldx(X, op3 * XC + (bp[j] >> 16))));
-                    stx(OFF, op3 * nblk + ob3, csub(ldx(V0S, op3), of));
+                    const int bb = (FULL && f.has_lag) ? f.blk_base[ob3] : -1;   // (sequential-order plan: V_prev base)
+                    stx(OFF, op3 * nblk + ob3, csub(bb >= 0 ? ldx(LAGV, op3 * NLAG + bb) : ldx(V0S, op3), of));
                 }
             } else if (chain_regs) {
                 if (tid < nblk) {
@@ -565,8 +605,10 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                         // all of them at once would spill)
                         if (j & 1) __builtin_amdgcn_sched_barrier(0);
                     }
+                    const int bb = (FULL && f.has_lag) ? f.blk_base[tid] : -1;
     #pragma unroll
-                    for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
+                    for (int p = 0; p < 3; ++p)
+                        stx(OFF, p * nblk + tid, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
                 }
             } else
             for (int b = tid; b < nblk; b += NT) {
@@ -576,8 +618,10 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     #pragma unroll
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
+                const int bb = (FULL && f.has_lag) ? f.blk_base[b] : -1;
     #pragma unroll
-                for (int p = 0; p < 3; ++p) stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
+                for (int p = 0; p < 3; ++p)
+                    stx(OFF, p * nblk + b, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
             }
             __syncthreads();
             BSTAMP_IT(5);
@@ -607,9 +651,10 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 }
             }
             double x;
-            if (FULL && f.has_mask) {
-                // zeroed phases: the reference's sum over PQL (the loss identity needs
-                // every phase live); the wave's part of sum Re(V conj(IL))
+            if (FULL && (f.has_mask || f.has_lag)) {
+                // zeroed phases, the sequential-order plan: the reference's sum over PQL
+                // (the loss identity needs every phase live and tree paths); the wave's
+                // part of sum Re(V conj(IL))
                 x = 0.0;
 #pragma unroll
                 for (int c = 0; c < C; ++c)
@@ -698,16 +743,19 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             mn = fmin(mn, wtf[8 * w + 6]);
             mx = fmax(mx, wtf[8 * w + 7]);
         }
-        if (FULL && f.has_mask) {
+        if (FULL && (f.has_mask || f.has_lag)) {
             // PQb(0).re - sum_k PQL(k).re, V0 conj(Ib(0)) of the last sweep
             double sb0 = 0.0;
 #pragma unroll
             for (int p = 0; p < 3; ++p) sb0 += cmul(cmul(ldx(V0S, p), mk(f.s3, 0.0)), cconj(ibo[p])).re;
             x = sb0 - f.s3 * x;
+        } else {
+            x *= f.s3;
+        }
+        if (FULL && f.has_mask) {
             mn = fmin(fmin(vx[0], vx[2]), vx[4]);
             mx = fmax(fmax(vx[1], vx[3]), vx[5]);
         } else {
-            x *= f.s3;
             mn = sqrt(mn);
             mx = sqrt(mx);
         }

@@ -55,3 +55,9 @@ def cases():
             "123-shuffled2": shuffled_blocks(f123, 2), "123-reversed": reversed_blocks(f123),
             "123-swapped": swapped_rows(f123, 5), "60-shuffled-swapped": swapped_rows(shuffled_blocks(f60, 3), 7),
             "200-shuffled-swapped": swapped_rows(shuffled_blocks(F.synthetic_feeder(200, 200), 4), 9)}
+
+
+def wblk_cases():
+    """Past 256 branches: the wave-block kernel (fpf_wblk.hip) runs the plan."""
+    return {"700-shuffled-swapped": swapped_rows(shuffled_blocks(F.synthetic_feeder(700, 700), 11), 12, n_swaps=6),
+            "2048-shuffled": shuffled_blocks(F.synthetic_feeder(2048, 2048), 13)}

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from freedm_amd import feeder as F
-from lag_tables import cases
+from lag_tables import cases, wblk_cases
 from test_gpu_parity import _close, _fast_mode_outputs_match, _vrel
 
 pytestmark = pytest.mark.gpu
@@ -42,6 +42,28 @@ def test_sequential_order_tables_on_the_wave_kernel(name):
     assert e.kernel in ("generic", "tiled")
     re_ = e.solve(pq[:, :, :16])
     np.testing.assert_array_equal(re_["V_re"], c["V_re"][..., :16])
+
+
+@pytest.mark.parametrize("name", sorted(wblk_cases()))
+def test_sequential_order_tables_on_the_wave_block_kernel(name):
+    """Past 256 branches (fpf_wblk_body.h under f.has_lag): the same bar."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = wblk_cases()[name]
+    B = 96
+    pq = F.scenario_loads(f, np.arange(B))
+    pf = PowerFlow(f)
+    assert pf.kernel == "wave" and pf.info["tile"] == 1, pf.info
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    np.testing.assert_array_equal(r["iters"], c["iters"])
+    np.testing.assert_array_equal(r["status"], c["status"])
+    assert (c["status"] == 0).all()
+    assert _vrel(r["V_re"], r["V_im"], c["V_re"], c["V_im"]) <= 1e-10
+    _fast_mode_outputs_match(r, c, c["status"] == 0)
+    _close(r["loss"], c["loss"], 1e-8)
+    np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
+    np.testing.assert_allclose(r["vmax"], c["vmax"], rtol=1e-10)
 
 
 @pytest.mark.parametrize("name", ["123-shuffled1", "123-swapped"])

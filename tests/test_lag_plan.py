@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from freedm_amd import feeder as F
-from lag_tables import cases
+from lag_tables import cases, wblk_cases
 from test_wave_plan import _plan
 
 
@@ -18,13 +18,21 @@ def test_sequential_order_tables_get_a_wave_plan(name):
     assert p["nblk"] >= 2 and p["lds"] <= 159 * 1024
 
 
+@pytest.mark.parametrize("name", sorted(wblk_cases()))
+def test_sequential_order_tables_get_a_wave_block_plan(name):
+    f = wblk_cases()[name]
+    p = _plan(f)
+    assert p["ok"] == 1 and p["spw"] == 1 and p["wpb"] >= 2, (name, p)   # (wpb: the wave-block kernel's wavefronts)
+    assert p["lds"] <= 159 * 1024
+
+
 def test_sequential_order_tables_are_not_well_formed():
     """Every case is one the tree plan declines (well_formed 0 or a chain that
     leaves the tree): the sequential-order plan is what runs it."""
     import ctypes as C
     from freedm_amd import _lib
     from freedm_amd.engine import PowerFlow  # noqa: F401  (binding only)
-    for name, f in cases().items():
+    for name, f in {**cases(), **wblk_cases()}.items():
         r = _rows_chain(f.Dl)
         assert r, name
 
