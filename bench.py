@@ -843,7 +843,7 @@ def main():
             pf4 = PowerFlow(feeder, device=local, kernel=args.kernel, exact=args.exact, layout=lay4)
             d4 = _loads_on_device(torch, dev, hosting_loads, feeder, ids4, seed4, layout=lay4)
             pf4.reserve(b4)
-            ms4, o4 = _kernel_ms(torch, pf4, d4, b4, 5, 2, stream, dev)
+            ms4, o4 = _kernel_ms(torch, pf4, d4, b4, 10, 3, stream, dev)
             conv4 = int((o4["status"] == 0).sum().item())
             ach4 = bpa * b4 / (ms4 / 1e3) / 1e9
             res["roofline_config4"] = {

@@ -139,7 +139,7 @@ struct WaveDev {
     int32_t dbg;             // diagnostic ablations (FPF_WAVE_DBG; results are wrong when set)
     int32_t wpb;             // wavefronts per workgroup (16, 8 or 4; fpf_api.cpp: analyse_wave)
     int32_t off_in_x;        // 1: block offsets stored over X's first nblk entries (nblk <= L, depth <= 4)
-    int32_t stag_lo, stag_hi, stag_n;   // workgroups [lo, hi) start stag_n x 8 k cycles late (diagnostic)
+    int32_t stag_lo, stag_hi, stag_n;   // workgroups [lo, hi) start stag_n x 1 k cycles late (diagnostic)
     int32_t temp_sym;        // 1: every branch's TEMP has one common off-diagonal zm (transposed
                              //    line / transformer): slot_temp holds (z_aa - zm) x 3, zm per slot
     int32_t spec;            // 1: large launches run the per-feeder hipRTC build (fpf_opts.specialize;

@@ -187,7 +187,7 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     // smaller ones, and a failed or non-resident build, the static kernel --
     // identical results (the light variant only: the full-output one -- Vpolar /
     // PQb / PQL, zeroed phases -- spills heavily either way and keeps the static build)
-    if (w.spec && !full && n_scen >= wave_rtc_min() && !wl.stag_n) {
+    if (w.spec && !full && n_scen >= wave_rtc_min()) {
         if (hipFunction_t fn = wave_rtc_function(dev, w, full)) {
             OutDev oa = o;
             int b = n_scen;

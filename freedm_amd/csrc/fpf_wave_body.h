@@ -123,7 +123,6 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     f.has_rel = FPF_WSPEC_HAS_REL;
     f.mxitr = FPF_WSPEC_MXITR;
     f.dbg = 0;
-    f.stag_lo = f.stag_hi = f.stag_n = 0;
 #endif
     constexpr int L = WaveGeom<SPW, C>::L, SPB = WPB * SPW;
     constexpr int NT = WPB * 64;
@@ -131,7 +130,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     if (DBG(4096)) return;
     if (o.skip && *o.skip) return;   // (the multi-area solve's device-side stop)
     if ((int)blockIdx.x >= f.stag_lo && (int)blockIdx.x < f.stag_hi)
-        for (int i = 0; i < f.stag_n; ++i) __builtin_amdgcn_s_sleep(127);
+        for (int i = 0; i < f.stag_n; ++i) __builtin_amdgcn_s_sleep(16);   // (~1 k cycles each)
     WSTAMP(0);
     // the guard's local list (OutDev::fix_dev): scenarios this workgroup flagged
     __shared__ int fix_n, fix_ids[SPB];

@@ -63,7 +63,7 @@ def main():
     torch.cuda.synchronize()
     st = buf.view(64, 128).cpu().numpy().astype(np.int64)
     phases = ["il+bw_scan", "ib_gather", "conv", "drops", "fw_scan+store", "blk_off", "v", "fin"]
-    rows, ph = [], []
+    rows, ph, ph_it = [], [], {}
     for w in range(64):
         s = st[w]
         if s[0] == 0 or s[121] == 0:
@@ -84,6 +84,7 @@ def main():
             nxt = s[tops[i + 1]] if i + 1 < n_sw else s[120]
             marks = [s[t + k] for k in range(8)] + [nxt]
             ph.append([marks[k + 1] - marks[k] for k in range(8)])
+            ph_it.setdefault(i, []).append(ph[-1])
     t0 = min(int(st[w][0]) for w in range(64) if st[w][0] != 0)
     entry = sorted(int(st[w][0]) - t0 for w in range(64) if st[w][0] != 0)
     keys = ["staging", "sld", "sweeps", "v_out", "total", "per_sweep", "n_sweeps"]
@@ -93,7 +94,9 @@ def main():
     print(json.dumps({"nn": nn, "B": B, "layout": layout, "base": base, "entry_spread": entry[::8],
                       "tile": pf.info["tile"], "waves": len(rows), "mean_cycles": mean,
                       "share": {k: mean[k] / mean["total"] for k in ("staging", "sld", "sweeps", "v_out")},
-                      "sweep_phase_cycles": {p: float(v) for p, v in zip(phases, phm)}}))
+                      "sweep_phase_cycles": {p: float(v) for p, v in zip(phases, phm)},
+                      "by_sweep": {str(i): {p: round(float(v)) for p, v in zip(phases, np.mean(np.array(x, dtype=np.float64), axis=0))}
+                                   for i, x in sorted(ph_it.items())}}))
 
 
 if __name__ == "__main__":
