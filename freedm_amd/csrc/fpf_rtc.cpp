@@ -18,8 +18,10 @@
 
 #include <algorithm>
 #include <array>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <type_traits>
 #include <map>
@@ -504,6 +506,26 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
 // the static build with the plan's uniform values defined as constants, so the
 // arithmetic -- and every result -- is the static kernel's.  Measured -4 to -5 %
 // kernel time on the 123-bus feeder (profiles/r04sp, r04rtc).
+// build switches of the wave kernel's per-plan build (experiments): FPF_WAVE_RTC_DEFS
+// = comma-separated macro names of fpf_wave_body.h, each defined as 1
+std::string wave_rtc_defs(const WaveDev &w) {
+    std::string out;
+    const char *e = getenv("FPF_WAVE_RTC_DEFS");
+    if (!e || w.wps) return out;
+    std::string s(e);
+    size_t a = 0;
+    while (a < s.size()) {
+        size_t b = s.find(',', a);
+        if (b == std::string::npos) b = s.size();
+        const std::string nm = s.substr(a, b - a);
+        bool ok = nm.size() > 9 && nm.compare(0, 9, "FPF_WAVE_") == 0;
+        for (char ch : nm) ok = ok && (isupper((unsigned char)ch) || isdigit((unsigned char)ch) || ch == '_');
+        if (ok) out += "#define " + nm + " 1\n";
+        a = b + 1;
+    }
+    return out;
+}
+
 std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
     std::ostringstream s;
     s << "#define FPF_WSPEC 1\n"
@@ -514,6 +536,7 @@ std::string wave_rtc_source(const WaveDev &w, bool full, std::string *name) {
       << "\n#define FPF_WSPEC_STAGE_UW " << w.stage_uw << "\n#define FPF_WSPEC_OUT_UW " << w.out_uw
       << "\n#define FPF_WSPEC_HAS_MASK " << w.has_mask << "\n#define FPF_WSPEC_HAS_REL " << w.has_rel
       << "\n#define FPF_WSPEC_MXITR " << w.mxitr << "\n";
+    s << wave_rtc_defs(w);
     char nm[96];
     if (w.wps) {   // the wave-block kernel (fpf_wblk_body.h); full: its FULL variant
         s << "#define FPF_WSPEC_NCODE " << w.ncode << "\n";
@@ -553,7 +576,7 @@ hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
     const char *se0 = getenv(w.wps ? "FPF_WBLK_RTC_SCHED" : "FPF_WAVE_RTC_SCHED");
     const PlanKey pk = {device, (int)full, w.nn, w.nl, w.nblk, w.bdepth, w.ncomp, w.temp_sym, w.off_in_x, w.stage_u,
                         w.out_u, w.stage_uw, w.out_uw, w.has_mask, w.has_rel, w.mxitr, w.ncode, w.wps, w.spw, w.C,
-                        w.wpb, se0 ? atoi(se0) : -1, 0, 0};
+                        w.wpb, se0 ? atoi(se0) : -1, (int32_t)std::hash<std::string>()(wave_rtc_defs(w)), 0};
     static std::map<PlanKey, hipFunction_t> by_plan;
     {
         std::lock_guard<std::mutex> lk(g_mu);

@@ -52,6 +52,14 @@ extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr, int base) {
 #endif
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
+// per-plan build switches (fpf_rtc.cpp: wave_rtc_source; FPF_WAVE_RTC_DEFS)
+// slot 0's TEMP reads issued with the Ib gathers, before the convergence test
+// (profiles/r05sw: -0.5 % config 2, -0.3 % config 4; FPF_WAVE_TEMP_LATE: after it)
+#ifdef FPF_WAVE_TEMP_LATE
+constexpr bool kTempEarly = false;
+#else
+constexpr bool kTempEarly = true;
+#endif
 constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging keeps in flight
 // the scenario-fastest batches' staging through the tables too (measured slower:
 // 44.1-44.5 vs 39.4-39.8 us on config 2, profiles/r04e); the feeder tables' loads
@@ -665,6 +673,11 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 tot[p] = mk(__shfl(ib[0][p].re, seg * L, 64), __shfl(ib[0][p].im, seg * L, 64));
         }
 
+        cx tq[4];   // slot 0's TEMP (kTempEarly: read here, with the gathers in flight)
+        if (kTempEarly && f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+        }
         WSTAMP(6 + 8 * it);
         // ---- convergence on the substation branch (:199-217): Ib(0) = the segment total;
         // max_p |Ib(0,p) - Ibo(p)| < eps compared as squares
@@ -728,9 +741,11 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             }
 #else
             // a slot's four TEMP reads issued together (2: the next slot's first)
-            cx tq[4], tn[4];
+            cx tn[4];
+            if (!kTempEarly) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+                for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+            }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
