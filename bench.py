@@ -358,7 +358,7 @@ def _instruction_efficiency(workload: str, kernel: str, flops_per_launch: float)
     """Useful fp64 flops per launch (the flop model above) / the issued VALU lane
     capacity of the launch, 2 flops (an FMA) x 64 lanes per wave64 VALU
     instruction, from the committed SQ_INSTS_VALU pass of this workload
-    (profiles/pmc_traffic.json "valu_insts_per_launch", tools/gpu_pmc_sq.sh): how
+    (profiles/pmc_traffic.json "valu_insts_per_launch", tools/runs/gpu_pmc_sq.sh): how
     much of what the kernel issues on the VALU is the path's arithmetic (the rest:
     DPP moves, address and loop arithmetic, the rounds of the scans)."""
     v = _pmc_traffic(workload, kernel, key="valu_insts_per_launch")

@@ -1,4 +1,4 @@
-"""The bench's config-5 leg alone (tools/gpu_r03n.sh profiles it): the 123-bus
+"""The bench's config-5 leg alone (tools/runs/gpu_r03n.sh profiles it): the 123-bus
 feeder in 3 areas, one config-2 batch, host buffers, tolerance 1e-12."""
 import os
 import sys

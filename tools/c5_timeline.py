@@ -1,5 +1,5 @@
 """Timeline of the last areas solve in a rocprofv3 kernel + memory-copy trace of
-tools/c5_leg.py (tools/gpu_c5.sh): every kernel and copy from the last
+tools/c5_leg.py (tools/runs/gpu_c5.sh): every kernel and copy from the last
 host-to-device copy of the batch on, with its start relative to that copy, its
 duration and the gap before it."""
 import csv

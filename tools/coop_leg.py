@@ -1,5 +1,5 @@
 """The bench's 4096-bus diagnostic leg alone (the paired wave-block kernel
-beside the exact generic kernel): tools/gpu_r03aa.sh times it."""
+beside the exact generic kernel): tools/runs/gpu_r03aa.sh times it."""
 import json
 import os
 import sys

@@ -1,4 +1,4 @@
-"""Per-dispatch means of the SQ counters collected by tools/gpu_pmc_sq.sh, per
+"""Per-dispatch means of the SQ counters collected by tools/runs/gpu_pmc_sq.sh, per
 kernel (names containing 'fpf' or 'dpf'), plus per-wave ratios."""
 import csv
 import glob

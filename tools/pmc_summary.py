@@ -2,7 +2,7 @@
 
     python tools/pmc_summary.py <tag> [kernel-name-substring] [run-dir]
 
-(run-dir: a tools/gpu_wblk.sh-style directory holding prof/run_kernel_stats.csv,
+(run-dir: a tools/runs/gpu_wblk.sh-style directory holding prof/run_kernel_stats.csv,
 pmc_<COUNTER>/pmc_counter_collection.csv and the bench line bench_*.json;
 default: the gpu_profile.sh layout gpurun_out/prof_<tag>...)
 

@@ -1,5 +1,5 @@
 """Record the VALU instruction count per launch of a workload's dominant kernel
-from an SQ counter pass (tools/gpu_pmc_sq.sh, pass 1 holds SQ_INSTS_VALU) in
+from an SQ counter pass (tools/runs/gpu_pmc_sq.sh, pass 1 holds SQ_INSTS_VALU) in
 profiles/pmc_traffic.json, where bench.py's instruction-efficiency figure reads it:
 
     python tools/pmc_valu.py <sq-tag> "<workload>" <kernel-name-substring> [<profile tag>]

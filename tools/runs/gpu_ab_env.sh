@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of the wave kernel's variants: for each "tag:ENV=.. ENV2=.." in
 # $VARIANTS, the config-4 roofline leg and config 2 (both layouts) kernel times.
-# Example: VARIANTS="base:FPF_WAVE_PERSIST=0 per:FPF_WAVE_PERSIST=1" bash tools/gpu_ab_env.sh
+# Example: VARIANTS="base:FPF_WAVE_PERSIST=0 per:FPF_WAVE_PERSIST=1" bash tools/runs/gpu_ab_env.sh
 set -o pipefail
 OUT=gpurun_out/${TAG:-ab}
 mkdir -p $OUT

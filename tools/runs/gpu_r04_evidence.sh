@@ -18,14 +18,14 @@ case ${PART:-1} in
   tail -1 gpurun_out/$P/bench_c3.log | cut -c1-300
   ;;
 2)
-  TAG=${P}_c2 ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-c4" bash tools/gpu_profile.sh || exit 1
-  TAG=${P}_c4 ARGS="--config 4 --steps 10 --warmup 2 --no-cpu-baseline" PARGS="--config 4 --steps 5 --warmup 1 --no-cpu-baseline" bash tools/gpu_profile.sh || exit 1
-  TAG=${P}_c3 ARGS="--config 3 --steps 5 --warmup 1 --no-cpu-baseline" PARGS="--config 3 --steps 3 --warmup 1 --no-cpu-baseline" bash tools/gpu_profile.sh || exit 1
+  TAG=${P}_c2 ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-c4" bash tools/runs/gpu_profile.sh || exit 1
+  TAG=${P}_c4 ARGS="--config 4 --steps 10 --warmup 2 --no-cpu-baseline" PARGS="--config 4 --steps 5 --warmup 1 --no-cpu-baseline" bash tools/runs/gpu_profile.sh || exit 1
+  TAG=${P}_c3 ARGS="--config 3 --steps 5 --warmup 1 --no-cpu-baseline" PARGS="--config 3 --steps 3 --warmup 1 --no-cpu-baseline" bash tools/runs/gpu_profile.sh || exit 1
   ;;
 3)
-  TAG=${P}_c2 ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-c4" bash tools/gpu_pmc_sq.sh || exit 1
-  TAG=${P}_c4 ARGS="--config 4 --steps 3 --warmup 1 --no-cpu-baseline" bash tools/gpu_pmc_sq.sh || exit 1
-  TAG=${P}_c3 ARGS="--config 3 --steps 2 --warmup 1 --no-cpu-baseline" bash tools/gpu_pmc_sq.sh || exit 1
+  TAG=${P}_c2 ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-c4" bash tools/runs/gpu_pmc_sq.sh || exit 1
+  TAG=${P}_c4 ARGS="--config 4 --steps 3 --warmup 1 --no-cpu-baseline" bash tools/runs/gpu_pmc_sq.sh || exit 1
+  TAG=${P}_c3 ARGS="--config 3 --steps 2 --warmup 1 --no-cpu-baseline" bash tools/runs/gpu_pmc_sq.sh || exit 1
   ;;
 esac
 echo DONE

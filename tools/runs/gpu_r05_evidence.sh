@@ -22,17 +22,17 @@ case ${PART:-1} in
   # (two streams overlap consecutive launches, each then lasting longer)
   for W in ${WHICH:-c2 c4 c3}; do
     case $W in
-      c2) TAG=${P}_c2 ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-c4 --streams 1" bash tools/gpu_profile.sh || exit 1 ;;
-      c2s2) TAG=${P}_c2s2 ARGS="--steps 20 --warmup 5 --no-cpu-baseline --no-c4" bash tools/gpu_profile.sh || exit 1 ;;
-      c4) TAG=${P}_c4 ARGS="--config 4 --steps 10 --warmup 2 --no-cpu-baseline --streams 1" PARGS="--config 4 --steps 5 --warmup 1 --no-cpu-baseline --streams 1" bash tools/gpu_profile.sh || exit 1 ;;
-      c3) TAG=${P}_c3 ARGS="--config 3 --steps 5 --warmup 1 --no-cpu-baseline --streams 1" PARGS="--config 3 --steps 3 --warmup 1 --no-cpu-baseline --streams 1" bash tools/gpu_profile.sh || exit 1 ;;
+      c2) TAG=${P}_c2 ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-c4 --streams 1" bash tools/runs/gpu_profile.sh || exit 1 ;;
+      c2s2) TAG=${P}_c2s2 ARGS="--steps 20 --warmup 5 --no-cpu-baseline --no-c4" bash tools/runs/gpu_profile.sh || exit 1 ;;
+      c4) TAG=${P}_c4 ARGS="--config 4 --steps 10 --warmup 2 --no-cpu-baseline --streams 1" PARGS="--config 4 --steps 5 --warmup 1 --no-cpu-baseline --streams 1" bash tools/runs/gpu_profile.sh || exit 1 ;;
+      c3) TAG=${P}_c3 ARGS="--config 3 --steps 5 --warmup 1 --no-cpu-baseline --streams 1" PARGS="--config 3 --steps 3 --warmup 1 --no-cpu-baseline --streams 1" bash tools/runs/gpu_profile.sh || exit 1 ;;
     esac
   done
   ;;
 3)
-  TAG=${P}_c2 ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-c4 --streams 1" bash tools/gpu_pmc_sq.sh || exit 1
-  TAG=${P}_c4 ARGS="--config 4 --steps 3 --warmup 1 --no-cpu-baseline --streams 1" bash tools/gpu_pmc_sq.sh || exit 1
-  TAG=${P}_c3 ARGS="--config 3 --steps 2 --warmup 1 --no-cpu-baseline --streams 1" bash tools/gpu_pmc_sq.sh || exit 1
+  TAG=${P}_c2 ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-c4 --streams 1" bash tools/runs/gpu_pmc_sq.sh || exit 1
+  TAG=${P}_c4 ARGS="--config 4 --steps 3 --warmup 1 --no-cpu-baseline --streams 1" bash tools/runs/gpu_pmc_sq.sh || exit 1
+  TAG=${P}_c3 ARGS="--config 3 --steps 2 --warmup 1 --no-cpu-baseline --streams 1" bash tools/runs/gpu_pmc_sq.sh || exit 1
   ;;
 esac
 echo DONE

@@ -10,4 +10,4 @@ echo "probe: $(tail -1 $OUT/probe_ilp_light.log)"
 FPF_TEST_WAVE_RTC=1 timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -k specialised tests/test_gpu_wave.py tests/test_gpu_wblk.py > $OUT/pytest_rtc.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $OUT/pytest_rtc.log; exit 1; }
 tail -3 $OUT/pytest_rtc.log
 unset FPF_DEBUG
-TAG=r05rtc/ab VARIANTS="static:FPF_WAVE_RTC=0 rtc:FPF_WAVE_RTC=1" CFGS="4:1 2:1 3:1" REPS="1 2" bash tools/gpu_ab_env.sh
+TAG=r05rtc/ab VARIANTS="static:FPF_WAVE_RTC=0 rtc:FPF_WAVE_RTC=1" CFGS="4:1 2:1 3:1" REPS="1 2" bash tools/runs/gpu_ab_env.sh

@@ -14,7 +14,7 @@ timeout -k 10 500 python3 -u bench.py > gpurun_out/${P}_bench.log 2>&1 || { echo
 tail -1 gpurun_out/${P}_bench.log | cut -c1-300
 timeout -k 10 500 python3 -u bench.py --config 3 --steps 5 --warmup 1 > gpurun_out/${P}_bench_c3.log 2>&1 || { echo "C3 FAILED"; tail -30 gpurun_out/${P}_bench_c3.log; exit 1; }
 tail -1 gpurun_out/${P}_bench_c3.log | cut -c1-300
-TAG=${P}_c2 ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-c4" bash tools/gpu_profile.sh || exit 1
-TAG=${P}_c4 ARGS="--config 4 --steps 10 --warmup 2 --no-cpu-baseline" PARGS="--config 4 --steps 5 --warmup 1 --no-cpu-baseline" bash tools/gpu_profile.sh || exit 1
-TAG=${P}_c3 ARGS="--config 3 --steps 5 --warmup 1 --no-cpu-baseline" PARGS="--config 3 --steps 3 --warmup 1 --no-cpu-baseline" bash tools/gpu_profile.sh || exit 1
+TAG=${P}_c2 ARGS="--steps 30 --warmup 5 --no-cpu-baseline --no-c4" bash tools/runs/gpu_profile.sh || exit 1
+TAG=${P}_c4 ARGS="--config 4 --steps 10 --warmup 2 --no-cpu-baseline" PARGS="--config 4 --steps 5 --warmup 1 --no-cpu-baseline" bash tools/runs/gpu_profile.sh || exit 1
+TAG=${P}_c3 ARGS="--config 3 --steps 5 --warmup 1 --no-cpu-baseline" PARGS="--config 3 --steps 3 --warmup 1 --no-cpu-baseline" bash tools/runs/gpu_profile.sh || exit 1
 echo DONE

@@ -13,4 +13,4 @@ for V in default iterative-ilp max-ilp iterative-minreg; do
 done
 done
 unset FPF_LIB_PATH
-VARIANTS="wave_default:- wave_maxilp:FPF_LIB_PATH=$A/libfreedm_pf_wave_maxilp.so" bash tools/gpu_ab.sh
+VARIANTS="wave_default:- wave_maxilp:FPF_LIB_PATH=$A/libfreedm_pf_wave_maxilp.so" bash tools/runs/gpu_ab.sh
