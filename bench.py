@@ -447,6 +447,60 @@ def _diag_4096(torch, local, stream, dev):
                     "exact kernel (every scenario)"}
 
 
+def _shuffled_units(f, seed):
+    """The feeder with its [separator + lateral block] units in a seeded order
+    (tests/lag_tables.py: laterals listed before their taps' rows -- tables the
+    tree plan declines, DPF_return7.cpp:134-195 solves them in row order)."""
+    from freedm_amd import Feeder
+    Dl = np.asarray(f.Dl)
+    cut = [0] + [i for i in range(Dl.shape[0]) if Dl[i, 0] == 0] + [Dl.shape[0]]
+    units = [Dl[cut[i]:cut[i + 1]] for i in range(1, len(cut) - 1)]
+    order = np.random.default_rng(seed).permutation(len(units))
+    return Feeder(np.vstack([Dl[:cut[1]]] + [units[i] for i in order]), f.Z, name=f"{f.name}-shuffled{seed}")
+
+
+def _diag_sequential_order(torch, local, stream, dev):
+    """Diagnostic leg: feeders whose lateral units are listed in a shuffled order
+    (the sequential-order plan, DESIGN 5.0e: the fast kernels' FULL variant) at
+    4096 scenarios (scenario major), beside the exact generic kernel -- until
+    round 5 the only kernel for such tables -- and the tree-ordered feeder's own
+    fast solve of the same loads: launch times, identical iteration counts and
+    status, max V relative difference."""
+    from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
+    out = {}
+    for name, n, seed in (("123bus_shuffled", 123, 1), ("2048bus_shuffled", 2048, 13)):
+        f0 = synthetic_feeder(n, n)
+        f = _shuffled_units(f0, seed)
+        B = 4096
+        pq = scenario_loads(f, np.arange(B), seed=B + 11)
+        d = torch.from_numpy(np.ascontiguousarray(pq.transpose(2, 0, 1))).to(dev)
+        legs = {}
+        for kind, exact in (("fast", 0), ("exact", 1)):
+            pf = PowerFlow(f, device=local, exact=exact, layout=1)
+            pf.reserve(B)
+            ms, o = _kernel_ms(torch, pf, d, B, 3, 1, stream, dev)
+            legs[kind] = (ms, o, pf.kernel, pf.info["nb"], pf.nn)
+            pf.close()
+        (msf, of, kf, nb, nn), (mse, oe, ke, _, _) = legs["fast"], legs["exact"]
+        conv = oe["status"] == 0
+        a = torch.complex(of["v_re"], of["v_im"])
+        b = torch.complex(oe["v_re"], oe["v_im"])
+        r = torch.where(conv.view(-1, 1, 1), (a - b).abs() / b.abs(), torch.zeros_like(b.real))
+        vrel = float(r.max().item())
+        del a, b, r, d
+        out[name] = {"workload": f"{nn}-bus synthetic feeder, lateral units shuffled (seed {seed}), {B} scenarios",
+                     "kernel": _wave_kernel_name(nb) if kf == "wave" else kf, "variant": "full (sequential order)",
+                     "kernel_ms": msf, "converged_scenarios_per_s": int(conv.sum().item()) / (msf / 1e3),
+                     "mean_sweeps": float(of["iters"].double().mean().item()),
+                     "exact_kernel": ke, "exact_kernel_ms": mse, "speedup_vs_exact": mse / msf,
+                     "iters_equal_exact": bool(torch.equal(of["iters"], oe["iters"])),
+                     "status_equal_exact": bool(torch.equal(of["status"], oe["status"])),
+                     "max_v_rel_diff_vs_exact": vrel,
+                     "note": "tests/test_gpu_lag.py checks these tables against the oracle"}
+        del of, oe
+    return out
+
+
 def _diag_heavy(torch, local, stream, dev):
     """Diagnostic leg: the config-2 and config-3 feeders at their full batch sizes
     under heavier, mixed loads (each scenario's loads scaled by a factor spread
@@ -902,6 +956,8 @@ def main():
             # the calibrated batches run 5 sweeps each: the same feeders under heavier,
             # mixed loads at full size, with the parity margin against the exact kernel
             res["diag_heavy"] = _diag_heavy(torch, local, stream, dev)
+            # tables whose rows do not follow the feeder tree (the sequential-order plan)
+            res["diag_sequential_order"] = _diag_sequential_order(torch, local, stream, dev)
             copy = _copy_bandwidth(torch, dev)
             res["hbm_copy_check"] = {"device_copy_gbs": copy, "spec_gbs": HBM_PEAK_GBS,
                                      "copy_frac_of_spec": copy / HBM_PEAK_GBS,

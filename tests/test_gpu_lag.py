@@ -66,14 +66,14 @@ def test_sequential_order_tables_on_the_wave_block_kernel(name):
     np.testing.assert_allclose(r["vmax"], c["vmax"], rtol=1e-10)
 
 
-@pytest.mark.parametrize("name", ["123-shuffled1", "123-swapped"])
+@pytest.mark.parametrize("name", ["123-shuffled1", "123-swapped", "700-shuffled-swapped"])
 def test_sequential_order_device_batches(name):
     """Device buffers, both layouts, a batch past the per-plan build's threshold
     (4096) and a ragged one: V and the scalars against the host-buffer solve's."""
     import torch
     from freedm_amd import PowerFlow
     from oracle import oracle as O
-    f = cases()[name]
+    f = {**cases(), **wblk_cases()}[name]
     dev = torch.device("cuda:0")
     for B in (4103, 77):
         pq = F.scenario_loads(f, np.arange(B))
