@@ -123,14 +123,24 @@ bool wave_wpb_supported(int spw, int c, int wpb) {
 
 namespace {
 typedef void (*WaveKernel)(WaveDev, int, const double *, OutDev);
+template <int SPW, int C, int WPB>
+WaveKernel pick_w(bool full, int gx) {
+    if (!full) return dpf_wave_kernel<SPW, C, false, WPB, 0>;
+    if (gx == 2) return dpf_wave_kernel<SPW, C, true, WPB, 2>;
+    if (gx == 0) return dpf_wave_kernel<SPW, C, true, WPB, 0>;
+    // (the 1-scenario, 2-slot geometry -- FPF_WAVE_GEOM experiments only -- has no
+    // zeroed-phase instantiation: the compiler's register allocator crashes on it)
+    if constexpr (SPW == 1 && C == 2) return nullptr;
+    else return dpf_wave_kernel<SPW, C, true, WPB, 1>;
+}
 template <int SPW, int C>
-WaveKernel pick(bool full, int wpb) {
+WaveKernel pick(bool full, int gen, int wpb) {
     if constexpr (SPW * C <= 2) {
-        if (wpb == 16) return full ? dpf_wave_kernel<SPW, C, true, 16> : dpf_wave_kernel<SPW, C, false, 16>;
-        if (wpb == 8) return full ? dpf_wave_kernel<SPW, C, true, 8> : dpf_wave_kernel<SPW, C, false, 8>;
+        if (wpb == 16) return pick_w<SPW, C, 16>(full, gen);
+        if (wpb == 8) return pick_w<SPW, C, 8>(full, gen);
     } else {
-        if (wpb == 8) return full ? dpf_wave_kernel<SPW, C, true, 8> : dpf_wave_kernel<SPW, C, false, 8>;
-        if (wpb == 4) return full ? dpf_wave_kernel<SPW, C, true, 4> : dpf_wave_kernel<SPW, C, false, 4>;
+        if (wpb == 8) return pick_w<SPW, C, 8>(full, gen);
+        if (wpb == 4) return pick_w<SPW, C, 4>(full, gen);
     }
     return nullptr;
 }
@@ -143,15 +153,18 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     // FULL keeps IL and Ib of the last sweep for Vpolar/PQb/PQL, and for the
     // loss of a feeder with zeroed phases (reference formula over PQL)
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask || w.has_lag;   // (the sequential-order plan: FULL only)
+    // the general paths only where the plan has them (fpf_wave_body.h: GX): zeroed
+    // phases, or the sequential-order plan (which declines zeroed phases)
+    const int gen = w.has_lag ? 2 : (w.has_mask || w.has_rel ? 1 : 0);
     WaveKernel k = nullptr;
     int id = -1;
-    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, w.wpb); id = 0; }
-    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full, w.wpb); id = 1; }
-    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full, w.wpb); id = 2; }
-    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full, w.wpb); id = 3; }
-    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full, w.wpb); id = 4; }
-    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, w.wpb); id = 5; }
-    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, w.wpb); id = 6; }
+    if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, gen, w.wpb); id = 0; }
+    else if (w.spw == 4 && w.C == 2) { k = pick<4, 2>(full, gen, w.wpb); id = 1; }
+    else if (w.spw == 4 && w.C == 4) { k = pick<4, 4>(full, gen, w.wpb); id = 2; }
+    else if (w.spw == 2 && w.C == 4) { k = pick<2, 4>(full, gen, w.wpb); id = 3; }
+    else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full, gen, w.wpb); id = 4; }
+    else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, gen, w.wpb); id = 5; }
+    else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, gen, w.wpb); id = 6; }
     if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the
     // static part) -- a per-device setting, done once per (device, variant)
@@ -161,7 +174,7 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> lk(mu);
-        const std::array<int, 4> key = {dev, id, (int)full, w.wpb};
+        const std::array<int, 4> key = {dev, id, (int)full + 2 * (full ? gen : 0), w.wpb};
         if (!attr_done.count(key)) {
             hipFuncAttributes fa{};
             hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);

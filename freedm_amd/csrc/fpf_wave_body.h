@@ -53,12 +53,13 @@ extern "C" int fpf_debug_set_wave_stamp_buffer(void *dptr, int base) {
 
 constexpr int WAVE_BD = 4;   // block-chain depth resolved from registers (deeper: LDS loop)
 // per-plan build switches (fpf_rtc.cpp: wave_rtc_source; FPF_WAVE_RTC_DEFS)
-// slot 0's TEMP reads issued with the Ib gathers, before the convergence test
-// (profiles/r05sw: -0.5 % config 2, -0.3 % config 4; FPF_WAVE_TEMP_LATE: after it)
-#ifdef FPF_WAVE_TEMP_LATE
-constexpr bool kTempEarly = false;
-#else
+// slot 0's TEMP reads issued with the Ib gathers, before the convergence test,
+// in the per-plan builds (profiles/r05sw: -0.5 % config 2, -0.3 % config 4); not
+// in the static build, whose light variant spills 139 VGPRs with them (2 without)
+#if defined(FPF_WSPEC) && !defined(FPF_WAVE_TEMP_LATE)
 constexpr bool kTempEarly = true;
+#else
+constexpr bool kTempEarly = false;
 #endif
 constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging keeps in flight
 // the scenario-fastest batches' staging through the tables too (measured slower:
@@ -109,9 +110,64 @@ constexpr bool TEMP_IN_LDS = false;
 constexpr bool TEMP_IN_LDS = true;
 #endif
 
-template <int SPW, int C, bool FULL, int WPB>
+// The loss and Vmin / Vmax of a scenario of the full variant with the general
+// paths, after its sweeps (VoltVarCtrl.cpp:1152-1161, 1201-1207): V of node k >= 1
+// at vrow[p * pstr + swz_row(k - 1) * srow], V0 and Ib(0) in v0s / ib0[p * pstr];
+// general V_abc_list (per phase the first K_p nonzero |V| in row order, zero
+// padded, V_abc_list.cpp:7-81), the loss from PQb(0) and PQL as the reference sums
+// them (slpart: this lane's part of s3 sum_k Re(V conj(IL))).  Whole segments.
+template <int L>
+__device__ __attribute__((noinline)) void full_gen_reductions(const OutDev &o, int K0, int K1, int K2, double s3, int nn,
+                                                              int s, const double2 *v0s, const double2 *ib0,
+                                                              const double2 *vrow, int pstr, int srow, double slpart,
+                                                              int seg, int lane, int li, double *rs) {
+    double mn = INFINITY, mx = -INFINITY;
+    const double sl = seg_incl<L>(slpart);
+    double x = 0.0;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) x += cmul(cmul(ldx(v0s, p), mk(s3, 0.0)), cconj(ldx(ib0, p * pstr))).re;
+    x -= sl;
+    const unsigned long long segbits = L == 64 ? ~0ull : ((1ull << (L & 63)) - 1ull) << (seg * L);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const int K = p == 0 ? K0 : (p == 1 ? K1 : K2);
+        int cnt = 0;
+        for (int k0 = 0; k0 < nn; k0 += L) {
+            const int k = k0 + li;
+            double m = 0.0;
+            if (k < nn) {
+                const cx vv = k == 0 ? ldx(v0s, p) : ldx(vrow, p * pstr + swz_row(k - 1) * srow);
+                m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
+            }
+            const bool nz = k < nn && m != 0.0;
+            const unsigned long long bal = __ballot(nz) & segbits;
+            const int rank = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+            if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
+            cnt += __popcll(bal);
+        }
+        if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
+    }
+    mn = seg_reduce_min<L>(mn);
+    mx = seg_reduce_max<L>(mx);
+    if (li == L - 1) {
+        if (o.loss) o.loss[s] = x;
+        if (o.vmin) o.vmin[s] = mn;
+        if (o.vmax) o.vmax[s] = mx;
+        rs[1] = mn;
+        rs[2] = mx;
+        rs[0] = x;
+    }
+}
+
+// FULL: the full-output variant (Vpolar / PQb / PQL); GX: the general paths
+// compiled into it -- bit 0 zeroed phases (has_mask / has_rel), bit 1 the
+// sequential-order plan (has_lag; never with zeroed phases).  One instantiation per
+// kind keeps each within the register file: all of them in one spilled ~150 VGPRs,
+// each alone 0-14 (tools/res_usage2.py)
+template <int SPW, int C, bool FULL, int WPB, int GX = FULL ? 1 : 0>
 __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, C>::template eff_minw<WPB>())) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {
+    constexpr bool FM = FULL && (GX & 1), FLG = FULL && (GX & 2), FG = FM || FLG;
 #ifdef FPF_WSPEC
     // the per-feeder hipRTC build (fpf_rtc.cpp: wave_rtc_source): the plan's
     // uniform values as constants -- loop bounds, LDS carve-up and branches fold
@@ -170,7 +226,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     double2 *const stg = (double2 *)(knode + C * L);
     double2 *const reg0 = stg + 3 * PSTR;                             // per-scenario regions
     const int noff = f.off_in_x ? 0 : 3 * nblk;                     // separate block-offset array
-    const int NLAG = FULL ? f.nlag : 0;                              // (the sequential-order plan: V_prev entries)
+    const int NLAG = FLG ? f.nlag : 0;                              // (the sequential-order plan: V_prev entries)
     const int RS = (3 * XC + noff + 4 + REGION_EXTRA + 3 * NLAG) | 1;  // double2 per region (+ the guard record)
     double2 *const X = reg0 + sc * RS;
     double2 *const V0S = X + 3 * XC + noff;   // the scenario's source voltage [3] (LDS, not registers)
@@ -540,8 +596,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     cx slp[3];   // (FPF_WAVE_SLD_PREF) slot 0's loads, read a sweep ahead
 #pragma unroll
     for (int p = 0; p < 3; ++p) slp[p] = FPF_WAVE_SLD_PREF ? ldx(stg, p * PSTR + sb[0]) : mk(0, 0);
+    double slkeep = 0.0;   // (FULL && GEN) the lane's part of s3 sum_k Re(V conj(IL)), kept from the last sweep
     for (int it = 0; __ballot(!done) != 0; ++it) {
-        if (FULL && f.has_lag) {
+        if (FLG && f.has_lag) {
             // (the sequential-order plan) the sources read before their own rows
             // (:176-178 with sbus's row later) see the previous sweep's V: stored
             // here, before this sweep updates it
@@ -564,7 +621,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(stg, p * PSTR + sb[c]), v[c][p]);
+            for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FM>(DBG(2) ? mk(0.01 * (c + 1), 0.003 * p) : ldx(stg, p * PSTR + sb[c]), v[c][p]);
 #else
         if (flat && it == 0) {
             // IL = conj(S/V0) = conj(S) V0 / |V0|^2 (V0 != 0), every Sld read once
@@ -600,7 +657,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     for (int p = 0; p < 3; ++p) sn[p] = ldx(stg, p * PSTR + sb[c + 1]);
                 }
 #pragma unroll
-                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(sl[p], v[c][p]);
+                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FM>(sl[p], v[c][p]);
                 if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
 #pragma unroll
                     for (int p = 0; p < 3; ++p) sn[p] = ldx(stg, p * PSTR + sb[c + 1]);
@@ -635,6 +692,68 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
             for (int c = 0; c < C; ++c) ib[c][p] = cadd(exl[p], ib[c][p]);   // Einc at this slot
         }
+        // ---- convergence on the substation branch (:199-217), decided once tot is
+        // known: after the scan (the full variant without the sequential-order plan:
+        // a finishing scenario's IL then leaves the registers before the gathers),
+        // else after the gathers
+        double err2 = 0.0;
+        bool conv = false, fin = false;
+        auto decide = [&]() {
+            // Ib(0) = the segment total; max_p |Ib(0,p) - Ibo(p)| < eps compared as squares
+            err2 = 0.0;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx io = FPF_WAVE_IBO_LDS ? ldx(IBO, p) : ibo[p];
+                const double dr = tot[p].re - io.re, di = tot[p].im - io.im;
+                err2 = fmax(err2, fma(dr, dr, di * di));
+                if (!FPF_WAVE_IBO_LDS) ibo[p] = tot[p];
+            }
+            if (FPF_WAVE_IBO_LDS && li == L - 1) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stx(IBO, p, tot[p]);
+            }
+            // decided in the segment's last lane, broadcast by ballot
+            const unsigned long long cbits = __ballot(li == L - 1 && err2 < eps2);
+            conv = (cbits >> (seg * L + L - 1)) & 1;
+            fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
+            if (o.flag_count) {
+                // ---- the convergence guard (fpf_opts.no_guard = 0): the decision above
+                // tests a scan-ordered Ib(0).  Where errmx lies within the rounding band
+                // of eps (fpf_api.cpp: guard_factor) the reference's sequential sum could
+                // decide the other way.  Decisions within 2^-9 of eps^2 (rare) keep their
+                // distance from eps^2 in the scenario's LDS record (no register stays
+                // live for it); the band itself is evaluated after the loop
+                const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
+                if (li == L - 1 && !done && dd <= 0x1p-9 * e2) {
+                    double2 g = V0S[3];
+                    g.y = fmin(g.y, dd);
+                    V0S[3] = g;
+                }
+            }
+            if (fin && li == L - 1 && o.errmx) o.errmx[s] = sqrt(err2);
+            if (FULL && fin) {
+                // (the full variant) the finishing scenario's IL into its own Sld rows
+                // (read for the last time at the top of this sweep; the loss reads it
+                // back in this sweep) and into the PQL output it becomes (the outputs
+                // are formed after the loop): no IL stays in registers
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if (si_valid(si[c])) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) stx(stg, p * PSTR + sb[c], il[c][p]);
+                        if (o.pql) {
+                            const int k = knode[c * L + li];
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) {
+                                const size_t o6 = out6(o, nn, B, k, p, (size_t)s);
+                                o.pql[o6] = il[c][p].re;
+                                o.pql[o6 + out6_im(o, nn, B)] = il[c][p].im;
+                            }
+                        }
+                    }
+            }
+        };
+        if (FULL && !(FLG && f.has_lag)) decide();
         wfence();
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -656,7 +775,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 eprev = e;
             }
         }
-        if (FULL && f.has_lag) {
+        if (FLG && f.has_lag) {
             // (the sequential-order plan) a post-add target also takes its detached
             // trees' totals (:138-146 after its own row), then node 1's Ib decides
 #pragma unroll
@@ -679,41 +798,27 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
         }
         WSTAMP(6 + 8 * it);
-        // ---- convergence on the substation branch (:199-217): Ib(0) = the segment total;
-        // max_p |Ib(0,p) - Ibo(p)| < eps compared as squares
-        double err2 = 0.0;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            const cx io = FPF_WAVE_IBO_LDS ? ldx(IBO, p) : ibo[p];
-            const double dr = tot[p].re - io.re, di = tot[p].im - io.im;
-            err2 = fmax(err2, fma(dr, dr, di * di));
-            if (!FPF_WAVE_IBO_LDS) ibo[p] = tot[p];
-        }
-        if (FPF_WAVE_IBO_LDS && li == L - 1) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) stx(IBO, p, tot[p]);
-        }
-        // decided in the segment's last lane, broadcast by ballot
-        const unsigned long long cbits = __ballot(li == L - 1 && err2 < eps2);
-        const bool conv = (cbits >> (seg * L + L - 1)) & 1;
-        const bool fin = DBG(512) ? !done : DBG(16) ? !done && it == 4 : !done && (conv || it == f.mxitr - 1);
-        if (o.flag_count) {
-            // ---- the convergence guard (fpf_opts.no_guard = 0): the decision above
-            // tests a scan-ordered Ib(0).  Where errmx lies within the rounding band
-            // of eps (fpf_api.cpp: guard_factor) the reference's sequential sum could
-            // decide the other way.  Decisions within 2^-9 of eps^2 (rare) keep their
-            // distance from eps^2 in the scenario's LDS record (no register stays
-            // live for it); the band itself is evaluated after the loop
-            const double e2 = f.eps * f.eps, dd = fabs(err2 - e2);
-            if (li == L - 1 && !done && dd <= 0x1p-9 * e2) {
-                double2 g = V0S[3];
-                g.y = fmin(g.y, dd);
-                V0S[3] = g;
-            }
-        }
-        if (fin && li == L - 1 && o.errmx) o.errmx[s] = sqrt(err2);
+        if (!(FULL && !(FLG && f.has_lag))) decide();
         // the loss terms are needed only in a scenario's last sweep
         const bool any_fin = __ballot(fin) != 0;
+        if (FULL && fin) {
+            // (the full variant) the finishing scenario's Ib into the PQb output it
+            // becomes: no Ib stays in registers through the forward sweep; the
+            // outputs read it back
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                if (si_valid(si[c])) {
+                    if (o.pqb) {
+                        const int k = knode[c * L + li];
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) {
+                            const size_t o6 = out6(o, nn, B, k, p, (size_t)s);
+                            o.pqb[o6] = ib[c][p].re;
+                            o.pqb[o6 + out6_im(o, nn, B)] = ib[c][p].im;
+                        }
+                    }
+                }
+        }
         WSTAMP(7 + 8 * it);
 
         // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
@@ -845,7 +950,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                             of[p] = cadd(of[p], csub(ldx(X, p * XC + (bp[j] & 0xffff)), ldx(X, p * XC + (bp[j] >> 16))));
                     }
                 }
-                const int bb = (FULL && f.has_lag) ? f.blk_base[li] : -1;   // (sequential-order plan: V_prev base)
+                const int bb = (FLG && f.has_lag) ? f.blk_base[li] : -1;   // (sequential-order plan: V_prev base)
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(OFF, p * OS + li, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
             }
@@ -857,7 +962,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
-                const int bb = (FULL && f.has_lag) ? f.blk_base[b] : -1;
+                const int bb = (FLG && f.has_lag) ? f.blk_base[b] : -1;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) stx(OFF, p * OS + b, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
             }
@@ -869,10 +974,10 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
                 const cx vr = csub(ldx(OFF, p * OS + bk[c]), g[c][p]);   // V0 - A(k)
-                if (FULL) g[c][p] = vr;
-                v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;
+                if (FM) g[c][p] = vr;
+                v[c][p] = (FM && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;
             }
-        if (FULL && f.has_rel) {
+        if (FM && f.has_rel) {
             // below a zeroed ancestor m: V(k,p) = A(m) - A(k) = Vr(k) - Vr(m), Vr = V0 - A
             // before the zeroing (held in g)
             wfence();
@@ -902,6 +1007,22 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // (VoltVarCtrl.cpp:1152-1161), Vmin/Vmax (V_abc_list.cpp:7-81,
             // VoltVarCtrl.cpp:1201-1207); whole segments
             double mn = INFINITY, mx = -INFINITY, x;
+            double slsum = 0.0;   // (full) s3 sum_k Re(V conj(IL)) of the scenario's slots
+            if (FG && (f.has_mask || f.has_lag)) {
+                // the reference's PQL form of the loss: the IL stashed in the Sld rows,
+                // all of it read before V goes over the rows below
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if (si_valid(si[c])) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) {
+                            const cx ils = ldx(stg, p * PSTR + sb[c]);
+                            slsum += f.s3 * (v[c][p].re * ils.re + v[c][p].im * ils.im);
+                        }
+                    }
+                wfence();
+                slkeep = slsum;
+            }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (si_valid(si[c])) {
@@ -909,7 +1030,6 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         stx(stg, p * PSTR + swz_row(k - 1) * SROW + sc, v[c][p]);   // over the scenario's own Sld
-                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
                         const double m2 = fma(v[c][p].re, v[c][p].re, v[c][p].im * v[c][p].im);
                         mn = fmin(mn, m2);
                         mx = fmax(mx, m2);
@@ -925,7 +1045,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 for (int p = 0; p < 3; ++p) {
                     const cx v0p = ldx(V0S, p);
                     // substation row 0: V0 (in V0S), Ib(0) = this sweep's total, no load
-                    if (FULL) emit_full(o, f.s3, nn, B, 0, p, (size_t)s, v0p, mk(0, 0), ibo[p]);
+                    // (full: node 0's outputs after the loop, from this sweep's Ib(0) kept in
+                    // the scenario's zero row of STG, which only its empty slots read)
+                    if (FULL) stx(stg, p * PSTR + swz_row(nl) * SROW + sc, ibo[p]);
                     if (o.s_in) {   // PQb row 0: (bkva/3) V0 conj(Ib(0))  (:242-244)
                         const cx sb = cmul(cmul(v0p, mk(f.s3, 0.0)), cconj(ibo[p]));
                         o.s_in[(size_t)(2 * p) * B + s] = sb.re;
@@ -936,51 +1058,12 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     mx = fmax(mx, m2);
                 }
             }
-            if (!FULL || !(f.has_mask || f.has_lag)) {   // (the host runs FULL for zeroed phases and the sequential-order plan)
+            if (!FG) {
                 // every Lnum_p + 1 = Nn: V_abc_list keeps every row, so the extremes are
                 // plain min/max; loss = s3 sum Re(drop conj(Ib))
                 x = f.s3 * seg_incl<L>(lp[0] + lp[1] + lp[2]);
                 mn = sqrt(seg_reduce_min<L>(mn));
                 mx = sqrt(seg_reduce_max<L>(mx));
-            } else {
-                // general V_abc_list: per phase the first K_p nonzero |V| in row order,
-                // zero padded; loss from PQb(0) and PQL as the reference sums them
-                wfence();
-                double sl = 0.0;
-#pragma unroll
-                for (int c = 0; c < C; ++c)
-#pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        if (si_valid(si[c])) sl += f.s3 * (v[c][p].re * il[c][p].re + v[c][p].im * il[c][p].im);
-                sl = seg_incl<L>(sl);
-                x = 0.0;
-#pragma unroll
-                for (int p = 0; p < 3; ++p) x += cmul(cmul(ldx(V0S, p), mk(f.s3, 0.0)), cconj(ibo[p])).re;
-                x -= sl;
-                mn = INFINITY;
-                mx = -INFINITY;
-                const unsigned long long segbits = L == 64 ? ~0ull : ((1ull << (L & 63)) - 1ull) << (seg * L);
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    const int K = f.K[p];
-                    int cnt = 0;
-                    for (int k0 = 0; k0 < nn; k0 += L) {
-                        const int k = k0 + li;
-                        double m = 0.0;
-                        if (k < nn) {
-                            const cx vv = k == 0 ? ldx(V0S, p) : ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
-                            m = sqrt(fma(vv.re, vv.re, vv.im * vv.im));
-                        }
-                        const bool nz = k < nn && m != 0.0;
-                        const unsigned long long bal = __ballot(nz) & segbits;
-                        const int rank = cnt + __popcll(bal & ((1ull << lane) - 1ull));
-                        if (nz && rank < K) { mn = fmin(mn, m); mx = fmax(mx, m); }
-                        cnt += __popcll(bal);
-                    }
-                    if (cnt < K) { mn = fmin(mn, 0.0); mx = fmax(mx, 0.0); }
-                }
-                mn = seg_reduce_min<L>(mn);
-                mx = seg_reduce_max<L>(mx);
             }
             if (li == L - 1) {
                 // (the output addresses formed here, not kept in registers across the loop)
@@ -988,12 +1071,14 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 __asm__ volatile("" : "+v"(sf));
                 if (o.iters) o.iters[sf] = it + 1;
                 if (o.status) o.status[sf] = conv ? 0 : 1;
-                if (o.loss) o.loss[sf] = x;
-                if (o.vmin) o.vmin[sf] = mn;
-                if (o.vmax) o.vmax[sf] = mx;
-                res[sc][1] = mn;
-                res[sc][2] = mx;
-                res[sc][0] = x;
+                if (!FG) {   // (FULL && GEN: after the loop)
+                    if (o.loss) o.loss[sf] = x;
+                    if (o.vmin) o.vmin[sf] = mn;
+                    if (o.vmax) o.vmax[sf] = mx;
+                    res[sc][1] = mn;
+                    res[sc][2] = mx;
+                    res[sc][0] = x;
+                }
                 res[sc][3] = conv ? 0.0 : 1.0;
             }
             wfence();
@@ -1001,6 +1086,37 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         done = done || fin;
     }
     WSTAMP(120);
+    if (FG && live) {
+        // (the full variant with the general paths) the loss and the extremes of the
+        // scenario's last sweep from what it left in LDS, outside the sweep loop (a
+        // call of its own: inlined here, its registers spilled ~110 VGPRs of the loop)
+        double *const rs = res[sc];
+        full_gen_reductions<L>(o, f.K[0], f.K[1], f.K[2], f.s3, nn, s, V0S, stg + swz_row(nl) * SROW + sc,
+                               stg + sc, PSTR, SROW, slkeep, seg, lane, li, rs);
+    }
+    if (FULL && live) {
+        // (the full variant) the outputs of DPF_return7.cpp:222-253 from the V this
+        // scenario stored in its last sweep and the IL / Ib its lanes stashed in PQL /
+        // PQB (complete: each lane waits for its own stores, the wave's lanes move
+        // together), node by node in output order -- consecutive lanes write
+        // consecutive nodes -- outside the sweep loop, where registers are free
+        if (o.pql || o.pqb) __builtin_amdgcn_s_waitcnt(0);
+        const size_t oim = out6_im(o, nn, B);
+        for (int i = li; i < 3 * nn; i += L) {
+            const int p = i / nn, k = i - p * nn;
+            const size_t o6 = out6(o, nn, B, k, p, (size_t)s);
+            cx vv, ils = mk(0, 0), ibs;
+            if (k == 0) {   // the substation row: V0, Ib(0) (kept in the scenario's zero row), no load
+                vv = ldx(V0S, p);
+                ibs = ldx(stg, p * PSTR + swz_row(nl) * SROW + sc);
+            } else {
+                vv = ldx(stg, p * PSTR + swz_row(k - 1) * SROW + sc);
+                if (o.pql) ils = mk(__builtin_nontemporal_load(o.pql + o6), __builtin_nontemporal_load(o.pql + o6 + oim));
+                ibs = o.pqb ? mk(__builtin_nontemporal_load(o.pqb + o6), __builtin_nontemporal_load(o.pqb + o6 + oim)) : mk(0, 0);
+            }
+            emit_full(o, f.s3, nn, B, k, p, (size_t)s, vv, ils, ibs);
+        }
+    }
 
     // ---- the guard band (fpf_api.cpp: guard_factor) for the scenarios with a decision
     // in the coarse band: errmx within tau = guard_k sum_k |IL_k|_1 of eps, where

@@ -194,6 +194,13 @@ __device__ __forceinline__ void wave_prefix_seg(const double *wt, int wv, int la
     for (int q = 0; q < 6; ++q) pre[q] = wu == 0 ? 0.0 : readlane_d(t[q], wu - 1);
 }
 
+// index of the (Re, Im) field pair of node k, phase p in a [6][Nn] output
+// (Vpolar / PQb / PQL): [field][row][B], or [B][field][row] (o.smaj)
+__device__ __forceinline__ size_t out6(const OutDev &o, int nn, int B, int k, int p, size_t s) {
+    return o.smaj ? s * 6 * nn + (size_t)(2 * p) * nn + k : ((size_t)(2 * p) * nn + k) * B + s;
+}
+__device__ __forceinline__ size_t out6_im(const OutDev &o, int nn, int B) { return o.smaj ? (size_t)nn : (size_t)nn * B; }
+
 // Outputs of node k, phase p (DPF_return7.cpp:222-253); returns (Re SL, |V|)
 __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn, int B, int k, int p, size_t s, cx v,
                                              cx il, cx ib) {
@@ -202,8 +209,7 @@ __device__ __forceinline__ double2 emit_full(const OutDev &o, double s3, int nn,
     const cx sb = cmul(sv, cconj(ib));
     const double mag = sqrt(fma(v.re, v.re, v.im * v.im));
     // [field][row][B], or [B][field][row] (o.smaj)
-    const size_t o6 = o.smaj ? s * 6 * nn + (size_t)(2 * p) * nn + k : ((size_t)(2 * p) * nn + k) * B + s;
-    const size_t o6i = o6 + (o.smaj ? (size_t)nn : (size_t)nn * B);
+    const size_t o6 = out6(o, nn, B, k, p, s), o6i = o6 + out6_im(o, nn, B);
     const size_t o3 = o.smaj ? s * 3 * nn + (size_t)p * nn + k : ((size_t)p * nn + k) * B + s;
     if (o.vpolar) { o.vpolar[o6] = mag; o.vpolar[o6i] = polar_angle(v, p); }
     if (o.pqb) { o.pqb[o6] = sb.re; o.pqb[o6i] = sb.im; }
