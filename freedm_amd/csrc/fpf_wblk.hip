@@ -68,9 +68,14 @@ bool wblk_geometry(int n, int *wps, int *c) {
 namespace {
 typedef void (*WblkKernel)(WaveDev, int, const double *, OutDev);
 template <int W, int C>
-WblkKernel pick_wblk(bool full, bool seg) {
+WblkKernel pick_wblk(bool full, bool seg, int gx) {
     // (a live phase below a zeroed one implies zeroed phases: the full variant)
-    return seg ? dpf_wblk_kernel<W, true, C, true> : (full ? dpf_wblk_kernel<W, true, C, false> : dpf_wblk_kernel<W, false, C, false>);
+    // The lean full variant for a tree feeder without zeroed phases (GX 0: no VGPR
+    // spills); every general path in one instantiation otherwise (GX 3): the
+    // zeroed-phase-only one crashes the compiler's register allocator
+    if (seg) return dpf_wblk_kernel<W, true, C, true, 1>;
+    if (!full) return dpf_wblk_kernel<W, false, C, false, 0>;
+    return gx == 0 ? dpf_wblk_kernel<W, true, C, false, 0> : dpf_wblk_kernel<W, true, C, false, 3>;
 }
 }  // namespace
 
@@ -81,11 +86,13 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
     // (the tables of a feeder with a live phase below a zeroed one are built for
     // the segmented forward scan: fpf_api.cpp analyse_wave)
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask || w.has_lag, seg = w.has_rel != 0;   // (has_lag: FULL only)
+    // the full variant's general paths only where the plan has them (fpf_wblk_body.h: GX)
+    const int gx = w.has_lag ? 2 : (w.has_mask || w.has_rel ? 1 : 0);
     WblkKernel k = nullptr;
     if (w.C == WB_C)
-        k = w.wps == 2 ? pick_wblk<2, WB_C>(full, seg)
-                       : (w.wps == 4 ? pick_wblk<4, WB_C>(full, seg) : (w.wps == 8 ? pick_wblk<8, WB_C>(full, seg) : nullptr));
-    else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full, seg) : (w.wps == 4 ? pick_wblk<4, 8>(full, seg) : nullptr);
+        k = w.wps == 2 ? pick_wblk<2, WB_C>(full, seg, gx)
+                       : (w.wps == 4 ? pick_wblk<4, WB_C>(full, seg, gx) : (w.wps == 8 ? pick_wblk<8, WB_C>(full, seg, gx) : nullptr));
+    else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full, seg, gx) : (w.wps == 4 ? pick_wblk<4, 8>(full, seg, gx) : nullptr);
     if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB: a per-device setting, once per (device, variant)
     static std::mutex mu;
@@ -94,7 +101,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> lk(mu);
-        const std::array<int, 3> key = {dev, w.wps * 16 + w.C, (int)full + 2 * (int)seg};
+        const std::array<int, 3> key = {dev, w.wps * 16 + w.C, (int)full + 2 * (int)seg + 4 * (full ? gx : 0)};
         if (!attr_done.count(key)) {
             hipFuncAttributes fa{};
             hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);

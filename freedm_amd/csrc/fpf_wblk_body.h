@@ -55,9 +55,17 @@ constexpr int WB_BD = 6;  // block-chain depth resolved from registers (deeper: 
 
 }  // namespace
 
-template <int W, bool FULL, int C, bool SEG>
+// GX (the full variant's general paths, as the wave kernel's): bit 0 zeroed
+// phases (has_mask / has_rel, SEG), bit 1 the sequential-order plan (has_lag)
+template <int W, bool FULL, int C, bool SEG, int GX = FULL ? 1 : 0>
 __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
                                                              OutDev o) {
+    constexpr bool FM = FULL && (GX & 1), FLG = FULL && (GX & 2), FG = FM || FLG;
+    // the full outputs of the lean variant (GX 0) formed after the sweep loop from
+    // IL / Ib stashed in the last sweep (no VGPR spills); the general variants emit
+    // in the last sweep as before (stashing measured slower there: 1.63 -> 1.93 ms,
+    // and faulted in the segmented one)
+    constexpr bool STASH = FULL && GX == 0 && !SEG;
 #ifdef FPF_WSPEC
     // the per-plan hipRTC build (fpf_rtc.cpp: wblk_rtc_source): the plan's
     // uniform values as constants; the host checks they match
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double2 *const OFF = X + 3 * XC;
     double2 *const OFFA = OFF + 3 * nblk;   // [3][nblk] off(b) itself (has_rel only)
     double2 *const V0S = OFF + 3 * nblk * (f.has_rel ? 2 : 1);
-    const int NLAG = FULL ? f.nlag : 0;              // (the sequential-order plan: V_prev entries)
+    const int NLAG = FLG ? f.nlag : 0;              // (the sequential-order plan: V_prev entries)
     double2 *const LAGV = V0S + 4;                   // [3][nlag]
     double *const wtb = (double *)(V0S + 4 + 3 * NLAG);
     double *const wtf = wtb + 8 * W;
@@ -175,7 +183,15 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     // t: block t % nblk, phase t / nblk): a third of the chain reads and adds per
     // thread, on every wave instead of the first nblk / 64 (round 5: the block
     // offsets were 28 % of a config-3 sweep with one block per thread, 3 phases each)
+    // (the per-plan builds only: in the static build, with the plan's values at
+    // run time, the second chain form spilled 118 VGPRs of the light variant)
+#if defined(FPF_WSPEC) || defined(FPF_WBLK_OFF3_STATIC)
     const bool off3 = chain_regs && 3 * nblk <= NT;
+#else
+    // (the general full variants keep it -- zeroed phases 1.65 vs 1.78 ms, 2048-bus x
+    // 2048 -- but not the segmented one, which faulted with it on the 2048-bus table)
+    const bool off3 = FULL && GX != 0 && !SEG && chain_regs && 3 * nblk <= NT;
+#endif
     const int op3 = off3 ? tid / nblk : 0, ob3 = off3 ? tid - op3 * nblk : tid;
     int bp[WB_BD];
 #pragma unroll
@@ -241,7 +257,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     double dmin = INFINITY;  // closest |err2 - eps^2| of a decision in the guard's coarse band
     double err2_last = 0.0;
     for (;; ++it) {
-        if (FULL && f.has_lag) {
+        if (FLG && f.has_lag) {
             // (the sequential-order plan, fpf_api.cpp: analyse_wave_lag) the sources
             // read before their own rows see the previous sweep's V, stored here
             // before this sweep updates it (read after the barriers below)
@@ -277,7 +293,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 #pragma unroll
             for (int c = 0; c < C; ++c)
 #pragma unroll
-                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FULL>(ldx(stg, p * PS + sb[c]), v[c][p]);   // 0 on a zeroed phase
+                for (int p = 0; p < 3; ++p) il[c][p] = il_fast<FM>(ldx(stg, p * PS + sb[c]), v[c][p]);   // 0 on a zeroed phase
         }
 
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of
@@ -329,7 +345,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                 eprev = e;
             }
         }
-        if (FULL && f.has_lag) {
+        if (FLG && f.has_lag) {
             // (the sequential-order plan) a post-add target also takes its detached
             // trees' totals; node 1's Ib (position 0: thread 0's slot 0) decides
 #pragma unroll
@@ -367,6 +383,24 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         conv = __builtin_amdgcn_readfirstlane(err2 < f.eps * f.eps ? 1 : 0) != 0;
         const bool fin = conv || it == f.mxitr - 1;
         if (fin) err2_last = err2;
+        if (STASH && fin) {
+            // (the full variant) IL into the slot's Sld rows (every Sld read of this
+            // sweep is behind the barriers above; the loss reads it back below) and,
+            // for the outputs formed after the loop, IL / Ib into the PQL / PQB outputs
+            // they become: neither stays in registers through the forward sweep
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                if (si_valid(si[c])) {
+                    const int k = f.slot_node[c * L + tid];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        stx(stg, p * PS + sb[c], il[c][p]);
+                        const size_t o6 = out6(o, nn, B, k, p, (size_t)s), o6i = o6 + out6_im(o, nn, B);
+                        if (o.pql) { o.pql[o6] = il[c][p].re; o.pql[o6i] = il[c][p].im; }
+                        if (o.pqb) { o.pqb[o6] = ib[c][p].re; o.pqb[o6i] = ib[c][p].im; }
+                    }
+                }
+        }
         // the convergence guard (fpf_wave.hip): err2 is the same in every lane of the
         // workgroup; a decision within 2^-9 of eps^2 keeps its distance in a register
         // (evaluated against the band after the loop)
@@ -481,7 +515,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     for (int j = 0; j < WB_BD; ++j)
                         if (j < bdepth) of = cadd(of, ldx(X, op3 * XC + (bp[j] & 0xffff)));   // uniform bound
                     stx(OFF, op3 * nblk + ob3, csub(ldx(V0S, op3), of));
-                    if (FULL && f.has_rel) stx(OFFA, op3 * nblk + ob3, of);   // (has_rel: never with has_lag)
+                    if (FM && f.has_rel) stx(OFFA, op3 * nblk + ob3, of);   // (has_rel: never with has_lag)
                 }
             } else if (chain_regs) {
                 if (tid < nblk) {
@@ -496,7 +530,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         stx(OFF, p * nblk + tid, csub(ldx(V0S, p), of[p]));
-                        if (FULL && f.has_rel) stx(OFFA, p * nblk + tid, of[p]);
+                        if (FM && f.has_rel) stx(OFFA, p * nblk + tid, of[p]);
                     }
                 }
             } else
@@ -510,7 +544,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     stx(OFF, p * nblk + b, csub(ldx(V0S, p), of[p]));
-                    if (FULL && f.has_rel) stx(OFFA, p * nblk + b, of[p]);
+                    if (FM && f.has_rel) stx(OFFA, p * nblk + b, of[p]);
                 }
             }
             __syncthreads();
@@ -519,9 +553,9 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     const cx vr = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
-                    v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
+                    v[c][p] = (FM && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
                 }
-            if (FULL && f.has_rel) {
+            if (FM && f.has_rel) {
                 // below a zeroed ancestor m: V(k,p) = A(m) - A(k) (:180-195: the path
                 // restarts from 0 at m), both small path sums; the forward entries (the
                 // block offsets are read) carry A now
@@ -588,7 +622,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                     for (int j = 0; j < WB_BD; ++j)
                         if (j < bdepth)   // uniform; levels past a chain's depth read the zero entry
                             of = cadd(of, csub(ldx(X, op3 * XC + (bp[j] & 0xffff)), ldx(X, op3 * XC + (bp[j] >> 16))));
-                    const int bb = (FULL && f.has_lag) ? f.blk_base[ob3] : -1;   // (sequential-order plan: V_prev base)
+                    const int bb = (FLG && f.has_lag) ? f.blk_base[ob3] : -1;   // (sequential-order plan: V_prev base)
                     stx(OFF, op3 * nblk + ob3, csub(bb >= 0 ? ldx(LAGV, op3 * NLAG + bb) : ldx(V0S, op3), of));
                 }
             } else if (chain_regs) {
@@ -605,7 +639,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
                         // all of them at once would spill)
                         if (j & 1) __builtin_amdgcn_sched_barrier(0);
                     }
-                    const int bb = (FULL && f.has_lag) ? f.blk_base[tid] : -1;
+                    const int bb = (FLG && f.has_lag) ? f.blk_base[tid] : -1;
     #pragma unroll
                     for (int p = 0; p < 3; ++p)
                         stx(OFF, p * nblk + tid, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
@@ -618,7 +652,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     #pragma unroll
                     for (int p = 0; p < 3; ++p) of[p] = cadd(of[p], csub(ldx(X, p * XC + pa), ldx(X, p * XC + mi)));
                 }
-                const int bb = (FULL && f.has_lag) ? f.blk_base[b] : -1;
+                const int bb = (FLG && f.has_lag) ? f.blk_base[b] : -1;
     #pragma unroll
                 for (int p = 0; p < 3; ++p)
                     stx(OFF, p * nblk + b, csub(bb >= 0 ? ldx(LAGV, p * NLAG + bb) : ldx(V0S, p), of[p]));
@@ -630,15 +664,36 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
     #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     const cx vr = csub(ldx(OFF, p * nblk + bk[c]), g[c][p]);   // V0 - A(k)
-                    v[c][p] = (FULL && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
+                    v[c][p] = (FM && ((si_mask(si[c]) >> p) & 1)) ? mk(0.0, 0.0) : vr;   // phase zeroing (:180-192)
                 }
         }
         BSTAMP_IT(6);
 
         if (fin) {
-            // ---- the last sweep: V of node k over Sld row k - 1 (every Sld read of
-            // this sweep is behind the barriers above), the full outputs, and the
-            // wave's part of the VVC loss (VoltVarCtrl.cpp:1152-1161)
+            // ---- the last sweep: the wave's part of the VVC loss
+            // (VoltVarCtrl.cpp:1152-1161), then V of node k over Sld row k - 1; the
+            // full outputs after the loop
+            double x;
+            if (FG && (f.has_mask || f.has_lag)) {
+                // zeroed phases, the sequential-order plan: the reference's sum over PQL
+                // (the loss identity needs every phase live and tree paths); the wave's
+                // part of sum Re(V conj(IL)), IL from the slot's Sld rows (SEG: still in
+                // registers)
+                x = 0.0;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        if (si_valid(si[c])) {
+                            const cx ils = STASH ? ldx(stg, p * PS + sb[c]) : il[c][p];
+                            x = fma(v[c][p].re, ils.re, fma(v[c][p].im, ils.im, x));
+                        }
+                x = seg_incl<64>(x);
+            } else {
+                x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
+            }
+            if (lane == 63) wtb[8 * wv + 6] = x;
+            if (STASH) __syncthreads();   // (every stashed IL read before V goes over the rows)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (si_valid(si[c])) {
@@ -646,34 +701,38 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
                         stx(stg, p * PS + k - 1, v[c][p]);
-                        if (FULL) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
+                        // (the general variants emit here; see STASH)
+                        if (FULL && !STASH) emit_full(o, f.s3, nn, B, k, p, (size_t)s, v[c][p], il[c][p], ib[c][p]);
                     }
                 }
             }
-            double x;
-            if (FULL && (f.has_mask || f.has_lag)) {
-                // zeroed phases, the sequential-order plan: the reference's sum over PQL
-                // (the loss identity needs every phase live and tree paths); the wave's
-                // part of sum Re(V conj(IL))
-                x = 0.0;
-#pragma unroll
-                for (int c = 0; c < C; ++c)
-#pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        if (si_valid(si[c])) x = fma(v[c][p].re, il[c][p].re, fma(v[c][p].im, il[c][p].im, x));
-                x = seg_incl<64>(x);
-            } else {
-                x = seg_incl<64>(lp[0] + lp[1] + lp[2]);
-            }
-            if (lane == 63) wtb[8 * wv + 6] = x;
             break;
         }
     }
     BSTAMP(120);
+    if (STASH && (o.pql || o.pqb)) __threadfence();   // (the stashes, for the other threads' reads below)
     __syncthreads();
+    if (STASH) {
+        // (the full variant) the outputs of DPF_return7.cpp:222-253, node by node in
+        // output order (consecutive threads, consecutive nodes): V from its row, IL / Ib
+        // from the stashes (node 0: below, from the last sweep's Ib(0))
+        const size_t oim = out6_im(o, nn, B);
+        for (int i = tid; i < 3 * nn; i += NT) {
+            const int p = i / nn, k = i - p * nn;
+            if (k == 0) continue;
+            const size_t o6 = out6(o, nn, B, k, p, (size_t)s);
+            const cx ils = o.pql ? mk(__hip_atomic_load(o.pql + o6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                      __hip_atomic_load(o.pql + o6 + oim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                 : mk(0, 0);
+            const cx ibs = o.pqb ? mk(__hip_atomic_load(o.pqb + o6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                      __hip_atomic_load(o.pqb + o6 + oim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                 : mk(0, 0);
+            emit_full(o, f.s3, nn, B, k, p, (size_t)s, ldx(stg, p * PS + k - 1), ils, ibs);
+        }
+    }
 
     // ---- Vmin/Vmax (V_abc_list.cpp:7-81, VoltVarCtrl.cpp:1201-1207)
-    if (FULL && f.has_mask) {
+    if (FM && f.has_mask) {
         // general V_abc_list: per phase the first K_p nonzero |V| in node order,
         // zero padded; one wave per phase, 64 nodes per step (ballot ranks); also
         // min over every nonzero |V|^2 of the wave's phases (the guard band)
@@ -743,7 +802,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
             mn = fmin(mn, wtf[8 * w + 6]);
             mx = fmax(mx, wtf[8 * w + 7]);
         }
-        if (FULL && (f.has_mask || f.has_lag)) {
+        if (FG && (f.has_mask || f.has_lag)) {
             // PQb(0).re - sum_k PQL(k).re, V0 conj(Ib(0)) of the last sweep
             double sb0 = 0.0;
 #pragma unroll
@@ -752,7 +811,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
         } else {
             x *= f.s3;
         }
-        if (FULL && f.has_mask) {
+        if (FM && f.has_mask) {
             mn = fmin(fmin(vx[0], vx[2]), vx[4]);
             mx = fmax(fmax(vx[1], vx[3]), vx[5]);
         } else {
@@ -775,7 +834,7 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDe
 #pragma unroll
                 for (int w = 0; w < W; ++w) {
                     sabs += wtb[8 * w + 7];
-                    m2 = fmin(m2, (FULL && f.has_mask) ? wtf[8 * w + 5] : wtf[8 * w + 6]);
+                    m2 = fmin(m2, (FM && f.has_mask) ? wtf[8 * w + 5] : wtf[8 * w + 6]);
                 }
                 const double tau = 1.25 * f.guard_k * 1.4142135623730951 * sabs / sqrt(m2);
                 near = dmin <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;

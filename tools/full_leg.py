@@ -69,6 +69,8 @@ def leg(f, full, B=4096, reps=10):
 def main():
     f = synthetic_feeder(123, 123)
     rows = [leg(f, False), leg(f, True), leg(zeroed(f), True), leg(shuffled_blocks(f, 1), True)]
+    g = synthetic_feeder(2048, 2048)   # the wave-block kernel
+    rows += [leg(g, False, B=2048, reps=3), leg(g, True, B=2048, reps=3), leg(zeroed(g), True, B=2048, reps=3)]
     print(json.dumps({"lib": os.environ.get("FPF_LIB_PATH", "default"), "legs": rows}))
 
 
