@@ -198,8 +198,9 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     // launches of at least wave_rtc_min() scenarios run the per-plan hipRTC build
     // (fpf_rtc.cpp: ~2.5 s to compile, once per plan and variant in a process);
     // smaller ones, and a failed or non-resident build, the static kernel --
-    // identical results (the light variant only: the full-output one -- Vpolar /
-    // PQb / PQL, zeroed phases -- spills heavily either way and keeps the static build)
+    // identical results (the light variant only: the full-output variants --
+    // Vpolar / PQb / PQL, zeroed phases, lag -- keep the static build, which is
+    // spill-free for them since the round-5 restructure)
     if (w.spec && !full && n_scen >= wave_rtc_min()) {
         if (hipFunction_t fn = wave_rtc_function(dev, w, full)) {
             OutDev oa = o;
