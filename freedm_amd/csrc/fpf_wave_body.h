@@ -104,10 +104,20 @@ struct WaveGeom {
 // the TEMP blocks are staged in LDS once per workgroup (a diagnostic build
 // reads them from global memory instead: L1/L2-resident, but the compiler
 // hoists the loads and spills -- 39 % slower, variants_r02a)
-#ifdef FPF_WAVE_TEMP_GLOBAL
+#if defined(FPF_WAVE_TEMP_GLOBAL) || defined(FPF_WAVE_TEMP_VMEM)
 constexpr bool TEMP_IN_LDS = false;
 #else
 constexpr bool TEMP_IN_LDS = true;
+#endif
+// (FPF_WAVE_TEMP_VMEM) the symmetric TEMP values read through the vector memory
+// pipe (L1-resident, one 8 KB table per plan) every sweep instead of from LDS: the
+// LDS pipe is as busy as the VALU in the sweeps, the vector memory
+// pipe idles there; the table pointer is made opaque per sweep so the loads are
+// not hoisted out of the loop (the round-2 global build's spills)
+#ifdef FPF_WAVE_TEMP_VMEM
+constexpr bool TEMP_VMEM = true;
+#else
+constexpr bool TEMP_VMEM = false;
 #endif
 
 // The loss and Vmin / Vmax of a scenario of the full variant with the general
@@ -596,8 +606,21 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
     cx slp[3];   // (FPF_WAVE_SLD_PREF) slot 0's loads, read a sweep ahead
 #pragma unroll
     for (int p = 0; p < 3; ++p) slp[p] = FPF_WAVE_SLD_PREF ? ldx(stg, p * PSTR + sb[0]) : mk(0, 0);
+    // (FPF_WAVE_TEMP_VMEM) the TEMP table [4][C][L] as a buffer
+    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc((void *)f.slot_temp, 0, 4 * C * L * 16, 0x00020000);
     double slkeep = 0.0;   // (FULL && GEN) the lane's part of s3 sum_k Re(V conj(IL)), kept from the last sweep
     for (int it = 0; __ballot(!done) != 0; ++it) {
+        // TEMP entry jc (= j C + c) of this lane's slot
+        int tvo = li * 16;
+        if (TEMP_VMEM) asm volatile("" : "+v"(tvo));   // opaque per sweep: the reads stay in the loop
+        auto ldt = [&](int jc) -> cx {
+            if (TEMP_VMEM) {
+                typedef double d2t __attribute__((ext_vector_type(2)));
+                const d2t t = __builtin_bit_cast(d2t, __builtin_amdgcn_raw_buffer_load_b128(trs, tvo + jc * L * 16, 0, 0));
+                return mk(t.x, t.y);
+            }
+            return ldx(tl, jc * L + li);
+        };
         if (FLG && f.has_lag) {
             // (the sequential-order plan) the sources read before their own rows
             // (:176-178 with sbus's row later) see the previous sweep's V: stored
@@ -793,9 +816,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         }
 
         cx tq[4];   // slot 0's TEMP (kTempEarly: read here, with the gathers in flight)
-        if (kTempEarly && f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
+        if (kTempEarly && f.temp_sym && (TEMP_IN_LDS || TEMP_VMEM) && !DBG(1)) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+            for (int j = 0; j < 4; ++j) tq[j] = ldt(j * C + 0);
         }
         WSTAMP(6 + 8 * it);
         if (!(FULL && !(FLG && f.has_lag))) decide();
@@ -828,18 +851,18 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         // VVC loss needs neither IL nor Ib after this point
         cx g[C][3];
         double lp[3] = {0.0, 0.0, 0.0};
-        if (f.temp_sym && TEMP_IN_LDS && !DBG(1)) {
+        if (f.temp_sym && (TEMP_IN_LDS || TEMP_VMEM) && !DBG(1)) {
             // one common off-diagonal zm: drop_a = (z_aa - zm) Ib_a + zm (Ib_1 + Ib_2 + Ib_3)
 #if FPF_WAVE_GROUP == 0
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 // (ablation 65536: wave-uniform TEMP from the kernel arguments, no LDS reads)
-                const cx m = DBG(65536) ? mk(f.lb_v * 1e-3, f.ub_v * 1e-3) : ldx(tl, (3 * C + c) * L + li);
+                const cx m = DBG(65536) ? mk(f.lb_v * 1e-3, f.ub_v * 1e-3) : ldt(3 * C + c);
                 const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
                 const cx ms = mk(fma(m.re, sm.re, -(m.im * sm.im)), fma(m.re, sm.im, m.im * sm.re));
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
-                    const cx d = DBG(65536) ? mk(f.eps * (a + 1), f.V0[0] * 1e-3) : ldx(tl, (a * C + c) * L + li);
+                    const cx d = DBG(65536) ? mk(f.eps * (a + 1), f.V0[0] * 1e-3) : ldt(a * C + c);
                     const cx b = ib[c][a];
                     g[c][a] = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
                 }
@@ -849,13 +872,13 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             cx tn[4];
             if (!kTempEarly) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) tq[j] = ldx(tl, (j * C + 0) * L + li);
+                for (int j = 0; j < 4; ++j) tq[j] = ldt(j * C + 0);
             }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (FPF_WAVE_GROUP == 2 && c + 1 < C) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) tn[j] = ldx(tl, (j * C + c + 1) * L + li);
+                    for (int j = 0; j < 4; ++j) tn[j] = ldt(j * C + c + 1);
                 }
                 const cx m = tq[3];
                 const cx sm = cadd(cadd(ib[c][0], ib[c][1]), ib[c][2]);
@@ -868,7 +891,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                 }
                 if (FPF_WAVE_GROUP == 1 && c + 1 < C) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) tn[j] = ldx(tl, (j * C + c + 1) * L + li);
+                    for (int j = 0; j < 4; ++j) tn[j] = ldt(j * C + c + 1);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) tq[j] = tn[j];
