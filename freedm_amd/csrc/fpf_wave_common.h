@@ -168,6 +168,10 @@ __device__ __forceinline__ void wave_prefix(const double *wt, int wv, int lane, 
 #pragma unroll
         for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x114, 0xf, 0xf>(t[q]);
     }
+    if (W > 8) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] += dpp_d<0x118, 0xf, 0xf>(t[q]);
+    }
     const int wu = __builtin_amdgcn_readfirstlane(wv);
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
@@ -189,6 +193,7 @@ __device__ __forceinline__ void wave_prefix_seg(const double *wt, int wv, int la
     if (W > 1) segf_step<0x111, 0xf, 0xf>(t, fl);
     if (W > 2) segf_step<0x112, 0xf, 0xf>(t, fl);
     if (W > 4) segf_step<0x114, 0xf, 0xf>(t, fl);
+    if (W > 8) segf_step<0x118, 0xf, 0xf>(t, fl);
     const int wu = __builtin_amdgcn_readfirstlane(wv);
 #pragma unroll
     for (int q = 0; q < 6; ++q) pre[q] = wu == 0 ? 0.0 : readlane_d(t[q], wu - 1);

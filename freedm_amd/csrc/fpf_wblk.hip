@@ -55,9 +55,11 @@ size_t wblk_lds_bytes(const WaveDev &w) {
 bool wblk_geometry(int n, int *wps, int *c) {
     // C = 4 slots per lane, 2 wavefronts per SIMD; FPF_WBLK_C=8 (experiments):
     // 8 slots per lane, half the wavefronts, 1 per SIMD (AGPRs hold the rest)
+    // FPF_WBLK_C=2 (experiments): 2 slots per lane, up to 16 wavefronts = 4 per SIMD
+    // (the per-plan build only: no static instantiation)
     const char *e = getenv("FPF_WBLK_C");
-    *c = (e && atoi(e) == 8) ? 8 : WB_C;
-    for (int w = 2; w <= 8; w *= 2)
+    *c = (e && atoi(e) == 8) ? 8 : (e && atoi(e) == 2) ? 2 : WB_C;
+    for (int w = 2; w <= (*c == 2 ? 16 : 8); w *= 2)
         if (n <= 64 * w * *c) {
             *wps = w;
             return true;
@@ -93,13 +95,12 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
         k = w.wps == 2 ? pick_wblk<2, WB_C>(full, seg, gx)
                        : (w.wps == 4 ? pick_wblk<4, WB_C>(full, seg, gx) : (w.wps == 8 ? pick_wblk<8, WB_C>(full, seg, gx) : nullptr));
     else if (w.C == 8) k = w.wps == 2 ? pick_wblk<2, 8>(full, seg, gx) : (w.wps == 4 ? pick_wblk<4, 8>(full, seg, gx) : nullptr);
-    if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB: a per-device setting, once per (device, variant)
     static std::mutex mu;
     static std::set<std::array<int, 3>> attr_done;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
-    {
+    if (k) {
         std::lock_guard<std::mutex> lk(mu);
         const std::array<int, 3> key = {dev, w.wps * 16 + w.C, (int)full + 2 * (int)seg + 4 * (full ? gx : 0)};
         if (!attr_done.count(key)) {
@@ -127,6 +128,7 @@ hipError_t launch_wblk(const WaveDev &w, int n_scen, const double *pq, const Out
         }
     }
 #endif
+    if (!k) return hipErrorInvalidValue;   // (FPF_WBLK_C=2: no static build)
     hipLaunchKernelGGL(k, dim3((unsigned)n_scen), dim3(64 * w.wps), wblk_lds_bytes(w), st, w, n_scen, pq, o);
     return hipGetLastError();
 }

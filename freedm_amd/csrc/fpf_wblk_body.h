@@ -58,7 +58,7 @@ constexpr int WB_BD = 6;  // block-chain depth resolved from registers (deeper: 
 // GX (the full variant's general paths, as the wave kernel's): bit 0 zeroed
 // phases (has_mask / has_rel, SEG), bit 1 the sequential-order plan (has_lag)
 template <int W, bool FULL, int C, bool SEG, int GX = FULL ? 1 : 0>
-__global__ __launch_bounds__(W * 64, C >= 8 ? 1 : 2) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
+__global__ __launch_bounds__(W * 64, C >= 8 ? 1 : (C <= 2 ? 4 : 2)) void dpf_wblk_kernel(WaveDev f, int B, const double *__restrict__ pq,
                                                              OutDev o) {
     constexpr bool FM = FULL && (GX & 1), FLG = FULL && (GX & 2), FG = FM || FLG;
     // the full outputs of the lean variant (GX 0) formed after the sweep loop from
