@@ -2154,6 +2154,24 @@ bool fpf::wave_hooks_supported(fpf_feeder *f, int n_scen) {
     return !w.wps && !w.coop;
 }
 
+// the byte ranges of a batch's output arrays intersect (fpf_outputs: they must not --
+// the fast kernels stash IL / Ib in pql / pqb before the final values)
+static bool outputs_overlap(const fpf_outputs &u, int nn, int B) {
+    const size_t b = (size_t)B, m6 = 6 * (size_t)nn * b * 8, m3 = 3 * (size_t)nn * b * 8;
+    const std::pair<const void *, size_t> r[] = {
+        {u.vpolar, m6}, {u.pqb, m6}, {u.pql, m6}, {u.v_re, m3}, {u.v_im, m3}, {u.iters, 4 * b}, {u.status, b},
+        {u.loss, 8 * b}, {u.vmin, 8 * b}, {u.vmax, 8 * b}, {u.errmx, 8 * b}, {u.guard, b}};
+    const size_t n = sizeof(r) / sizeof(r[0]);
+    for (size_t i = 0; i < n; ++i)
+        for (size_t j = i + 1; j < n; ++j) {
+            if (!r[i].first || !r[j].first) continue;
+            const uintptr_t a0 = (uintptr_t)r[i].first, a1 = a0 + r[i].second;
+            const uintptr_t b0 = (uintptr_t)r[j].first, b1 = b0 + r[j].second;
+            if (a0 < b1 && b0 < a1) return true;
+        }
+    return false;
+}
+
 int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_outputs *d_out, double *d_agg,
                                void *stream, const double *d_vsrc, double *d_s_in, int layout, unsigned *d_flag_out,
                                const int32_t *d_skip, const double *d_vinit_re, const double *d_vinit_im,
@@ -2171,6 +2189,7 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     fpf_outputs none;
     std::memset(&none, 0, sizeof(none));
     const fpf_outputs &u = d_out ? *d_out : none;
+    if (outputs_overlap(u, f->dev.nn, n_scen)) return fail(ctx, FPF_ERR_ARG, "output arrays overlap (fpf_outputs)");
     OutDev o = outdev_from(f, u, layout);
     o.vsrc = d_vsrc;
     o.s_in = d_s_in;

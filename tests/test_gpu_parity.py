@@ -482,3 +482,28 @@ def test_config3_full_size_against_oracle():
     np.testing.assert_array_equal(v_re, c["V_re"])
     np.testing.assert_array_equal(v_im, c["V_im"])
     np.testing.assert_array_equal(out["loss"][ti].cpu().numpy(), c["loss"])
+
+
+def test_overlapping_outputs_refused():
+    """fpf_outputs arrays must not overlap (include/freedm_pf.h: the fast kernels
+    stash a scenario's IL / Ib in its own pql / pqb entries): overlapping ranges
+    are refused with FPF_ERR_ARG before anything is enqueued, and a call with
+    disjoint views of one allocation still solves."""
+    import torch
+    from freedm_amd import DPFError, PowerFlow
+    f = F.synthetic_feeder(123, 123)
+    B = 64
+    pq = torch.from_numpy(F.scenario_loads(f, np.arange(B), seed=7)).to("cuda:0")
+    pf = PowerFlow(f, device=0)
+    nn = pf.nn
+    big = torch.empty((2, 6, nn, B), dtype=torch.float64, device="cuda:0")
+    with pytest.raises(DPFError):
+        pf.solve_device(pq, {"pqb": big[0], "pql": big[0]})
+    with pytest.raises(DPFError):   # a partial overlap: pql starts inside pqb
+        flat = big.reshape(-1)
+        pf.solve_device(pq, {"pqb": flat[: 6 * nn * B].view(6, nn, B),
+                             "pql": flat[nn * B: nn * B + 6 * nn * B].view(6, nn, B)})
+    out = {"pqb": big[0], "pql": big[1], "iters": torch.empty(B, dtype=torch.int32, device="cuda:0")}
+    pf.solve_device(pq, out)
+    torch.cuda.synchronize()
+    assert int(out["iters"].min()) >= 1
