@@ -51,12 +51,13 @@ def _close(a, b, rtol):
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_matches_golden(name, kernel, spec, exact):
     g = load_golden(name)
-    if kernel == "tiled" and name == "g4_2048bus" and spec:
-        pytest.skip("2048-bus: above the hipRTC size limit, covered by the interpreted tiled kernel")
+    # the 2048-bus feeder is above the tiled hipRTC build's size limit: the build
+    # is declined and the interpreted tiled kernel runs (same results)
+    declined = kernel == "tiled" and name == "g4_2048bus" and spec
     pf = _pf(g["Dl"], g["Z"], kernel=kernel, specialize=spec, exact=exact)
     assert pf.kernel == kernel
     if kernel == "tiled":
-        assert pf.info["specialized"] == int(spec), pf.rtc_error
+        assert pf.info["specialized"] == (0 if declined else int(spec)), pf.rtc_error
     r = pf.solve(g["pq"])
     # the north-star bar
     assert (r["iters"] == g["iters"]).all()
