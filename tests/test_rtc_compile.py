@@ -105,6 +105,25 @@ def test_wblk_rtc_source_compiles(nn):
     assert _compile(src, name, [b"-mllvm", b"-amdgpu-sched-strategy=iterative-ilp"]).startswith("_ZN3fpf15dpf_wblk_kernelI")
 
 
+def test_wblk_two_slot_geometry_plan_and_source(monkeypatch):
+    """The experimental wave-block geometry FPF_WBLK_C=2 (2 slots per
+    lane, 16 wavefronts for 1025..2048 branches, per-plan build only -- measured
+    slower on config 3): the plan and the per-plan source carry it, and the
+    source compiles; the default plan is unchanged without the switch."""
+    from wave_rtc_dump import wave_rtc_source
+    from test_wave_plan import _plan
+    from freedm_amd import synthetic_feeder
+    f = synthetic_feeder(2048, 2048)
+    assert (_plan(f)["C"], _plan(f)["wpb"]) == (4, 8)
+    monkeypatch.setenv("FPF_WBLK_C", "2")
+    p = _plan(f)
+    assert (p["C"], p["wpb"]) == (2, 16)
+    src = wave_rtc_source(f, 1, 0)
+    name = src.rsplit("template __global__ void ", 1)[1].split("(")[0]
+    assert name.startswith("fpf::dpf_wblk_kernel<16, false, 2,")
+    assert _compile(src, name, [b"-mllvm", b"-amdgpu-sched-strategy=iterative-ilp"]).startswith("_ZN3fpf15dpf_wblk_kernelI")
+
+
 def _notes(co: bytes) -> dict:
     import re
     import subprocess
