@@ -153,7 +153,8 @@ typedef struct fpf_feeder_info {
 /* Per-scenario outputs; every pointer may be NULL (= not produced).  Shapes
  * for FPF_LAYOUT_SCEN_FASTEST; FPF_LAYOUT_SCEN_MAJOR swaps B to the front.
  * The arrays must not overlap: the fast kernels stash a scenario's IL / Ib of
- * its last sweep in its own pql / pqb entries before writing the final values. */
+ * its last sweep in its own pql / pqb entries before writing the final values
+ * (fpf_solve_batch_device returns FPF_ERR_ARG for overlapping ranges). */
 typedef struct fpf_outputs {
     double      *vpolar;   /* [6][Nn][B]  |Va| angA |Vb| angB |Vc| angC (deg)  */
     double      *pqb;      /* [6][Nn][B]  branch P/Q (kW, kVAr)                */
