@@ -517,10 +517,14 @@ std::string wave_rtc_defs(const WaveDev &w) {
     while (a < s.size()) {
         size_t b = s.find(',', a);
         if (b == std::string::npos) b = s.size();
-        const std::string nm = s.substr(a, b - a);
-        bool ok = nm.size() > 9 && nm.compare(0, 9, "FPF_WAVE_") == 0;
+        // NAME or NAME=digits
+        const std::string item = s.substr(a, b - a);
+        const size_t eq = item.find('=');
+        const std::string nm = item.substr(0, eq), val = eq == std::string::npos ? "1" : item.substr(eq + 1);
+        bool ok = nm.size() > 9 && nm.compare(0, 9, "FPF_WAVE_") == 0 && !val.empty();
         for (char ch : nm) ok = ok && (isupper((unsigned char)ch) || isdigit((unsigned char)ch) || ch == '_');
-        if (ok) out += "#define " + nm + " 1\n";
+        for (char ch : val) ok = ok && isdigit((unsigned char)ch);
+        if (ok) out += "#define " + nm + " " + val + "\n";
         a = b + 1;
     }
     return out;

@@ -188,3 +188,18 @@ def test_rtc_compile_survives_setenv():
         for k in added:
             os.environ.pop(k, None)
     assert L.fpf_rtc_compile(src.encode(), name, 0, None, None, 0) > 1000
+
+
+def test_wave_rtc_defs_switches(monkeypatch):
+    """FPF_WAVE_RTC_DEFS (experiments): FPF_WAVE_* names become `#define NAME 1`,
+    NAME=digits `#define NAME digits`, anything else is dropped; the switches are
+    part of the source (and so of the per-plan build cache key); none by default."""
+    from wave_rtc_dump import wave_rtc_source
+    from freedm_amd import synthetic_feeder
+    f = synthetic_feeder(123, 123)
+    base = wave_rtc_source(f, 1, 0)
+    assert "#define FPF_WAVE_GROUP 2\n" not in base and "#define FPF_WAVE_TEMP_LATE 1\n" not in base
+    monkeypatch.setenv("FPF_WAVE_RTC_DEFS", "FPF_WAVE_GROUP=2,FPF_WAVE_TEMP_LATE,BOGUS=1,FPF_WAVE_X=abc,FPF_WAVE_Y=")
+    src = wave_rtc_source(f, 1, 0)
+    assert "#define FPF_WAVE_GROUP 2\n" in src and "#define FPF_WAVE_TEMP_LATE 1\n" in src
+    assert "BOGUS" not in src and "#define FPF_WAVE_X " not in src and "#define FPF_WAVE_Y" not in src
