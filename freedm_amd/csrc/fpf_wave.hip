@@ -42,6 +42,7 @@
 #include <mutex>
 #include <set>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "fpf_internal.h"
@@ -104,13 +105,25 @@ void wave_io_units(WaveDev &w) {
     }
 }
 
+// (experiments) the per-plan builds read TEMP through the vector memory pipe
+// (FPF_WAVE_RTC_DEFS names FPF_WAVE_TEMP_VMEM): no TEMP block in LDS.  Only
+// launches that run the per-plan build may be sized so (FPF_WAVE_WPB=2 has no
+// static kernel)
+static bool rtc_temp_vmem() {
+    static const bool on = [] {
+        const char *d = getenv("FPF_WAVE_RTC_DEFS");
+        return d && strstr(d, "FPF_WAVE_TEMP_VMEM");
+    }();
+    return on;
+}
+
 size_t wave_lds_bytes(const WaveDev &w) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
     const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4 + REGION_EXTRA + 3 * (size_t)w.nlag) | 1);
     const size_t stage = 16 * 3 * ((size_t)swz_row(w.nl) + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
-    const size_t temp = TEMP_IN_LDS ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
+    const size_t temp = TEMP_IN_LDS && !rtc_temp_vmem() ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
     return temp + pairs + std::max(stage + regions, agg);
 }
 
@@ -118,7 +131,8 @@ int wave_scenarios_per_block(const WaveDev &w) { return w.wps ? 1 : w.wpb * w.sp
 
 // the waves-per-workgroup choices each geometry is built for
 bool wave_wpb_supported(int spw, int c, int wpb) {
-    return spw * c <= 2 ? (wpb == 16 || wpb == 8) : (wpb == 8 || wpb == 4);
+    // (2: experiments, FPF_WAVE_WPB=2 with FPF_WAVE_TEMP_VMEM -- per-plan build only)
+    return spw * c <= 2 ? (wpb == 16 || wpb == 8) : (wpb == 8 || wpb == 4 || (wpb == 2 && rtc_temp_vmem()));
 }
 
 namespace {
@@ -165,14 +179,13 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     else if (w.spw == 1 && w.C == 4) { k = pick<1, 4>(full, gen, w.wpb); id = 4; }
     else if (w.spw == 1 && w.C == 2) { k = pick<1, 2>(full, gen, w.wpb); id = 5; }
     else if (w.spw == 2 && w.C == 2) { k = pick<2, 2>(full, gen, w.wpb); id = 6; }
-    if (!k) return hipErrorInvalidValue;
     // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per CU, minus the
     // static part) -- a per-device setting, done once per (device, variant)
     static std::mutex mu;
     static std::set<std::array<int, 4>> attr_done;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
-    {
+    if (k) {
         std::lock_guard<std::mutex> lk(mu);
         const std::array<int, 4> key = {dev, id, (int)full + 2 * (full ? gen : 0), w.wpb};
         if (!attr_done.count(key)) {
@@ -213,6 +226,7 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
         }
     }
 #endif
+    if (!k) return hipErrorInvalidValue;   // (FPF_WAVE_WPB=2: no static build)
     hipLaunchKernelGGL(k, dim3(grid), dim3(w.wpb * 64), lds, st, wl, n_scen, pq, o);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess && getenv("FPF_DEBUG")) {
