@@ -27,7 +27,8 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_gradient_at", "fpf_vvc_round",
            "fpf_vvc_gradient_batch", "fpf_feeder_check", "fpf_vvc_round_batch", "fpf_feeder_wave_rtc_source",
-           "fpf_wave_rtc_builds", "fpf_rtc_compile", "fpf_rtc_compiler"]
+           "fpf_wave_rtc_builds", "fpf_rtc_compile", "fpf_rtc_compiler", "fpf_feeder_lane_plan", "fpf_lane_launches",
+           "fpf_rtc_resident", "fpf_multi_collectives"]
 
 
 class FpfOpts(C.Structure):
@@ -128,6 +129,12 @@ def load(path: str | None = None):
         L.fpf_feeder_wave_plan.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
                                            C.POINTER(C.c_int)]
         L.fpf_feeder_wave_plan.restype = C.c_int
+    if hasattr(L, "fpf_feeder_lane_plan") or path == LIB_PATH:   # (older diagnostic builds lack it)
+        L.fpf_feeder_lane_plan.argtypes = [_dp, C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.POINTER(FpfOpts),
+                                           C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int),
+                                           C.c_int]
+        L.fpf_feeder_lane_plan.restype = C.c_int
+        L.fpf_lane_launches.restype = C.c_int
     L.fpf_selftest_division.argtypes = [C.c_int, C.c_long, C.c_ulong]
     L.fpf_selftest_division.restype = C.c_long
     if hasattr(L, "fpf_multi_create") or path == LIB_PATH:   # (older diagnostic builds lack them)

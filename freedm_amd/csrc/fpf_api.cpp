@@ -68,6 +68,11 @@ struct fpf_feeder {
     void *d_wave = nullptr;
     void *d_stage_tab = nullptr;   // the wave kernel's staging tables (both geometries)
     WaveDev wdev{}, wdev_big{};
+    // the lane kernel (fpf_lane.hip): one lane per scenario; large light-output
+    // scenario-fastest batches of the feeders it accepts (analyse_lane)
+    void *d_lane = nullptr;
+    LaneDev ldev{};
+    bool lane_ok = false;
     void *d_xch = nullptr, *d_xsync = nullptr, *d_xvm = nullptr;   // the paired wave-block kernel's exchange
     unsigned *h_xerr = nullptr;   // its sticky fault word (pinned, coherent; the kernel sets it at system scope)
     // the partials + ticket scratch is shared by every aggregating launch on
@@ -1161,6 +1166,158 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     w.ok = true;
 }
 
+// Tables of the lane kernel (fpf_lane.hip): the wave kernel's depth-first
+// order (in-block child first: subtrees and blocks are contiguous) dealt to
+// LANE_NW waves in contiguous runs of at most ns <= LANE_NS positions, each run
+// padded with dummy slots to ns.  Accepts what the wave kernel's tree plan
+// accepts, minus zeroed phases and non-symmetric TEMP, up to LANE_NW * LANE_NS
+// branches.
+struct LaneHost {
+    bool ok = false;
+    std::string why;
+    int n = 0, ns = 0, nE = 0, nG = 0, nblk = 0;
+    std::vector<int32_t> slot;   // [LANE_NW][4][ns]
+    std::vector<double> temp;   // [LANE_NW][ns][LANE_TW]
+    std::vector<int32_t> blk;    // [nblk][1 + 2 LANE_BD]
+};
+
+void analyse_lane(const HostFeeder &h, const fpf_opts &o, LaneHost &L) {
+    auto no = [&](const std::string &why) { L.ok = false; L.why = why; };
+    if (!h.wf) return no("not well formed: " + h.wf_why);
+    const int nl = h.nl, nn = h.nn, n = nn - 1;
+    if (n > LANE_NW * LANE_NS) return no("more than " + std::to_string(LANE_NW * LANE_NS) + " branches");
+    std::vector<int> par(nn, -1), chain(nn, -1);
+    std::vector<std::vector<int>> lat(nn);
+    for (int m = 0; m < nl; ++m) {
+        if (h.at(m, 0) == 0) continue;
+        const int k = (int)h.at(m, 2), src = m == 0 ? 0 : (int)h.at(m, 1);
+        par[k] = src;
+        if (m == 0) continue;
+        if (h.at(m - 1, 0) != 0) {
+            if ((int)h.at(m - 1, 2) != src) return no("the backward chains leave the feeder tree");
+            chain[src] = k;
+        } else {
+            lat[src].push_back(k);
+        }
+    }
+    for (int k = 1; k < nn; ++k)
+        if (h.node[k].mask & 7) return no("zeroed phases");
+    // depth-first order, in-block child first (analyse_wave)
+    std::vector<int> pos(nn, -1), at, blk(nn, 0), size(nn, 1), bfirst;
+    std::vector<int> st = {1};
+    bfirst.push_back(1);
+    while (!st.empty()) {
+        const int k = st.back();
+        st.pop_back();
+        pos[k] = (int)at.size();
+        at.push_back(k);
+        for (int l : lat[k]) {
+            blk[l] = (int)bfirst.size();
+            bfirst.push_back(l);
+            st.push_back(l);
+        }
+        if (chain[k] >= 0) {
+            blk[chain[k]] = blk[k];
+            st.push_back(chain[k]);
+        }
+    }
+    if ((int)at.size() != n) return no("feeder tree does not reach every node from node 1");
+    for (int q = n - 1; q > 0; --q) size[par[at[q]]] += size[at[q]];
+    const int nblk = (int)bfirst.size();
+    if (nblk > 0x3fff) return no("too many blocks");
+    // TEMP with one common off-diagonal value per branch (fast mode's symmetric form)
+    for (int q = 0; q < n; ++q) {
+        const double *t = &h.tz[(size_t)h.node[at[q]].fw * 18];
+        for (int j = 1; j < 9; ++j)
+            if (j % 4 != 0 && !(t[2 * j] == t[2] && t[2 * j + 1] == t[3])) return no("TEMP not symmetric");
+    }
+    // published entries: subtree ends (backward), taps and first - 1 of the lateral
+    // blocks (forward), in position order; the entry after both is the zero
+    std::vector<int> cb(n, -1), cf(n, -1);
+    int nE = 0, nG = 0;
+    for (int q = 0; q < n; ++q) {
+        const int e = q + size[at[q]] - 1;
+        if (cb[e] < 0) cb[e] = 0;
+    }
+    for (int q = 0; q < n; ++q)
+        if (cb[q] == 0) cb[q] = nE++;
+    for (int b = 1; b < nblk; ++b) {
+        cf[pos[par[bfirst[b]]]] = 0;
+        cf[pos[bfirst[b]] - 1] = 0;
+    }
+    for (int q = 0; q < n; ++q)
+        if (cf[q] == 0) cf[q] = nG++;
+    const int zero = std::max(nE, nG);
+    L.blk.assign((size_t)nblk * (1 + 2 * LANE_BD), 0);
+    for (int b = 1; b < nblk; ++b) {
+        int d = 0;
+        for (int j = b; j != 0; j = blk[par[bfirst[j]]], ++d) {
+            if (d >= LANE_BD) return no("block nesting deeper than " + std::to_string(LANE_BD));
+            L.blk[(size_t)b * (1 + 2 * LANE_BD) + 1 + 2 * d] = cf[pos[par[bfirst[j]]]];
+            L.blk[(size_t)b * (1 + 2 * LANE_BD) + 2 + 2 * d] = cf[pos[bfirst[j]] - 1];
+        }
+        L.blk[(size_t)b * (1 + 2 * LANE_BD)] = d;
+    }
+    // the waves' runs: the first n % NW waves one position more
+    int cmax = (n + LANE_NW - 1) / LANE_NW, ns = 4;
+    while (ns < cmax) ns += 4;
+    if (const char *e = getenv("FPF_LANE_NS")) {   // experiments: a larger instantiation
+        const int v = atoi(e);
+        if (v >= ns && v <= LANE_NS && v % 4 == 0) ns = v;
+    }
+    L.slot.assign((size_t)LANE_NW * ns * 4, 0);
+    L.temp.assign((size_t)LANE_NW * ns * LANE_TW, 0.0);
+    int q0 = 0;
+    for (int w = 0; w < LANE_NW; ++w) {
+        const int cnt = n / LANE_NW + (w < n % LANE_NW ? 1 : 0);
+        int lastb = 0;
+        for (int i = 0; i < ns; ++i) {
+            // the wave's table [4][ns] (struct of arrays: one scalar load per field)
+            int32_t sl_[4];
+            int32_t *const sl = sl_;
+            double *tp = &L.temp[((size_t)w * ns + i) * LANE_TW];
+            if (i < cnt) {
+                const int q = q0 + i, k = at[q];
+                const NodeOp &nd = h.node[k];
+                const int e = q + size[k] - 1;
+                const bool start = i == 0 || bfirst[blk[k]] == k;
+                sl[0] = nd.row;
+                sl[1] = k;
+                // bit 0: a real slot; published: the subtree ends (leaves); gathered:
+                // this subtree's end
+                sl[2] = 1 | ((cb[q] >= 0 ? cb[q] + 1 : 0) << 1) | (cb[e] << 16);
+                sl[3] = (cf[q] + 1) | (blk[k] << 16) | (start ? 1 << 30 : 0);
+                const double *t = &h.tz[(size_t)nd.fw * 18];
+                for (int a = 0; a < 3; ++a) {
+                    tp[2 * a] = t[2 * (4 * a)] - t[2];
+                    tp[2 * a + 1] = t[2 * (4 * a) + 1] - t[3];
+                }
+                tp[6] = t[2];
+                tp[7] = t[3];
+                lastb = blk[k];
+            } else {
+                // a dummy slot: row 0's loads scaled by 0, TEMP 0, gathers the zero entry
+                sl[0] = 0;
+                sl[1] = -1;
+                sl[2] = zero << 16;
+                sl[3] = (lastb << 16) | (i == 0 ? 1 << 30 : 0);
+            }
+            for (int k = 0; k < 4; ++k) L.slot[((size_t)w * 4 + k) * ns + i] = sl[k];
+        }
+        q0 += cnt;
+    }
+    L.n = n;
+    L.ns = ns;
+    L.nE = nE;
+    L.nG = nG;
+    L.nblk = nblk;
+    LaneDev probe{};
+    probe.nE = nE;
+    probe.nG = nG;
+    if (lane_lds_bytes(probe) > WAVE_LDS_BUDGET - 2048) return no("published entries exceed LDS");
+    L.ok = true;
+}
+
 // Chunked sequential programs for one tile size (see fpf_internal.h).
 void build_seq_programs(HostFeeder &h, int tile) {
     const int nn = h.nn, U = SEQ_CHUNK;
@@ -1878,6 +2035,41 @@ extern "C" int fpf_feeder_create(fpf_ctx *ctx, const double *dl, int nl, int nco
         }
         f->wdev_big = w;
         f->wdev_big.wpb = wh.wpb_big_batch;
+        // the lane kernel's plan (fpf_lane.hip): large light-output batches
+        if (!wh.wps && !wh.coop && !getenv("FPF_NO_LANE")) {
+            LaneHost lh;
+            analyse_lane(h, o, lh);
+            if (lh.ok) {
+                std::vector<char> lb;
+                const size_t o_ls = push_blob(lb, lh.slot), o_lt = push_blob(lb, lh.temp), o_lb = push_blob(lb, lh.blk);
+                e = hipMalloc(&f->d_lane, lb.size());
+                if (e == hipSuccess) e = hipMemcpy(f->d_lane, lb.data(), lb.size(), hipMemcpyHostToDevice);
+                if (e != hipSuccess) {
+                    fpf_feeder_destroy(f);
+                    return fail(ctx, FPF_ERR_HIP, std::string("lane tables upload: ") + hipGetErrorString(e));
+                }
+                LaneDev &l = f->ldev;
+                l.n = lh.n;
+                l.nn = h.nn;
+                l.nl = nl;
+                l.nE = lh.nE;
+                l.nG = lh.nG;
+                l.nblk = lh.nblk;
+                l.mxitr = o.mxitr;
+                l.ns = lh.ns;
+                for (int i = 0; i < 6; ++i) l.V0[i] = d.V0[i];
+                for (int p = 0; p < 3; ++p) l.rv0[p] = w.rv0[p];
+                l.s3 = d.s3;
+                l.eps = d.eps;
+                l.lb_v = d.lb_v;
+                l.ub_v = d.ub_v;
+                l.guard_k = w.guard_k;
+                l.slot = (const int32_t *)((char *)f->d_lane + o_ls);
+                l.temp = (const double *)((char *)f->d_lane + o_lt);
+                l.blk = (const int32_t *)((char *)f->d_lane + o_lb);
+                f->lane_ok = true;
+            }
+        }
         if (!w.wps) {
             // the table-driven staging of both launch geometries (fpf_wave.hip)
             std::vector<int32_t> sm[2], l0[2], om[2], o0[2];
@@ -1965,6 +2157,7 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     if (!f) return;
     (void)hipSetDevice(f->ctx->device);
     (void)hipFree(f->d_tables);
+    (void)hipFree(f->d_lane);
     (void)hipFree(f->d_scratch);
     (void)hipFree(f->d_iters);
     (void)hipFree(f->d_status);
@@ -2004,9 +2197,26 @@ static hipError_t agg_before(fpf_feeder *f, hipStream_t st) {
     if (f->agg_pending && f->agg_stream != st) return hipStreamWaitEvent(st, f->agg_event, 0);
     return hipSuccess;
 }
-// the wave kernel's launch geometry for a batch of n_scen scenarios
-static const WaveDev &wave_dev_for(const fpf_feeder *f, int n_scen) {
-    return n_scen >= WAVE_SMALL_WPB_MIN_SCEN ? f->wdev_big : f->wdev;
+// the wave kernel's launch geometry for a batch of n_scen scenarios: the
+// large-batch workgroups from WAVE_STATIC_BIG_MIN_SCEN on, and from
+// WAVE_SMALL_WPB_MIN_SCEN on where the per-plan build runs the launch (light
+// outputs, no zeroed phases or sequential-order plan, fpf_wave.hip: launch_wave)
+// -- the static kernel is ~6 % slower on the small workgroups there (profiles/r05wio)
+constexpr int WAVE_STATIC_BIG_MIN_SCEN = 16384;
+static const WaveDev &wave_dev_for(const fpf_feeder *f, int n_scen, bool full = false) {
+    const WaveDev &w = f->wdev;
+    const bool rtc = w.spec && !full && !w.has_mask && !w.has_lag && n_scen >= wave_rtc_min();
+    return n_scen >= WAVE_STATIC_BIG_MIN_SCEN || (rtc && n_scen >= WAVE_SMALL_WPB_MIN_SCEN) ? f->wdev_big : f->wdev;
+}
+
+// a wave-kernel launch that runs the lane kernel instead (fpf_lane.hip): its
+// plan exists, the batch is large enough (FPF_LANE), scenario fastest, light
+// outputs, the feeder's own source and flat start
+static bool lane_for(const fpf_feeder *f, int n_scen, const OutDev &o) {
+    // (the kernel's 32-bit buffer offsets: the whole batch below 4 GiB)
+    return f->lane_ok && n_scen >= lane_min_scen() && (size_t)6 * f->ldev.nl * n_scen * 8 < ((size_t)1 << 32) &&
+           !o.smaj && !o.vpolar && !o.pqb && !o.pql && !o.vsrc &&
+           !o.s_in && !o.skip && !o.vinit_re && !o.hook && !o.eps_dev && !o.check;
 }
 
 // the kernel a batch of n_scen scenarios runs on
@@ -2215,7 +2425,9 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     // own LDS (local mode) where they fit
     const bool guarded = kern == FPF_KERNEL_WAVE && f->guard && !d_vsrc && !d_s_in;
     const bool local_fix = guarded && !d_agg && !f->wdev.wps &&
-                           (size_t)96 * (f->dev.nl + f->dev.nn) <= wave_lds_bytes(wave_dev_for(f, n_scen));
+                           (size_t)96 * (f->dev.nl + f->dev.nn) <=
+                               wave_lds_bytes(wave_dev_for(f, n_scen, u.vpolar || u.pqb || u.pql)) &&
+                           (!f->lane_ok || (size_t)96 * (f->dev.nl + f->dev.nn) <= lane_lds_bytes(f->ldev));
     // launches that use state of the feeder -- the generic kernel's scratch, the
     // layout copies, an aggregate's partials and ticket, the guard's flag list and
     // fixup scratch, the paired kernel's exchange areas, the feeder's own
@@ -2257,9 +2469,13 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
     }
     static const bool fused_agg = !getenv("FPF_FUSED_AGG") || atoi(getenv("FPF_FUSED_AGG")) != 0;
     const bool fuses_agg = (kern == FPF_KERNEL_TILED && f->rtc) || kern == FPF_KERNEL_WAVE;
+    const bool lane = kern == FPF_KERNEL_WAVE && lane_for(f, n_scen, o);
     if (d_agg && fused_agg && fuses_agg) {
         // the specialised and wave kernels reduce the batch aggregate in their last workgroup
-        const int per = kern == FPF_KERNEL_WAVE ? wave_scenarios_per_block(wave_dev_for(f, n_scen)) : f->dev.tile;
+        const int per = lane ? 64
+                             : (kern == FPF_KERNEL_WAVE
+                                    ? wave_scenarios_per_block(wave_dev_for(f, n_scen, o.vpolar || o.pqb || o.pql))
+                                    : f->dev.tile);
         const size_t tiles = ((size_t)n_scen + per - 1) / per;
         if (tiles > f->partials_cap) {
             (void)hipFree(f->d_partials);
@@ -2291,9 +2507,15 @@ int fpf::solve_batch_device_ex(fpf_feeder *f, int n_scen, const double *d_pq, co
         }
     }
     if (kern == FPF_KERNEL_WAVE) {
-        WaveDev w = f->wdev.wps ? f->wdev : wave_dev_for(f, n_scen);
+        WaveDev w = f->wdev.wps ? f->wdev : wave_dev_for(f, n_scen, o.vpolar || o.pqb || o.pql);
         if (!guarded) w.guard_k = 0.0;
-        e = w.wps ? launch_wblk(w, n_scen, d_pq, o, st) : launch_wave(w, n_scen, d_pq, o, st);
+        if (lane) {
+            LaneDev l = f->ldev;
+            if (!guarded) l.guard_k = 0.0;
+            e = launch_lane(l, n_scen, d_pq, o, st);
+        } else {
+            e = w.wps ? launch_wblk(w, n_scen, d_pq, o, st) : launch_wave(w, n_scen, d_pq, o, st);
+        }
         // with an aggregate, the exact re-solve of flagged scenarios (and the
         // aggregate again) is a launch of its own after the fast solve (it exits at
         // once when none was flagged), unless the host API defers it until it has
@@ -2531,6 +2753,35 @@ extern "C" int fpf_feeder_wave_plan(const double *dl, int nl, int ncols, const d
     const int lds = !wh.ok ? 0 : (int)wave_any_lds_bytes(w);
     const int v[8] = {wh.ok ? 1 : 0, wh.spw, wh.C, wh.wpb, lds, wh.ncomp, wh.nblk, wh.bdepth};
     std::memcpy(out, v, sizeof(v));
+    return FPF_OK;
+}
+
+extern "C" int fpf_feeder_lane_plan(const double *dl, int nl, int ncols, const double *z, int z_rows, int z_cols,
+                                    const fpf_opts *opts, int out[8], int *slots, int slots_len, int *blk,
+                                    int blk_len) {
+    if (!dl || !out || nl < 1 || ncols < 12 || z_rows < 0 || (z_rows > 0 && !z)) return FPF_ERR_ARG;
+    fpf_opts o;
+    if (opts) o = *opts;
+    else fpf_opts_default(&o);
+    HostFeeder h;
+    h.nl = nl;
+    h.ncols = ncols;
+    h.dl.assign(dl, dl + (size_t)nl * ncols);
+    std::string why = build_ops(h, z, z_rows, z_cols, o);
+    if (why.empty()) why = build_lnum(h, z, z_rows, o);
+    if (!why.empty()) return FPF_ERR_TOPOLOGY;
+    analyse_tiled(h);
+    LaneHost lh;
+    analyse_lane(h, o, lh);
+    LaneDev l{};
+    l.nE = lh.nE;
+    l.nG = lh.nG;
+    const int v[8] = {lh.ok ? 1 : 0, lh.ns, LANE_NW, lh.ok ? (int)lane_lds_bytes(l) : 0, lh.nE, lh.nG, lh.nblk, lh.n};
+    std::memcpy(out, v, sizeof(v));
+    if (slots && lh.ok)
+        for (int i = 0; i < slots_len && i < (int)lh.slot.size(); ++i) slots[i] = lh.slot[i];
+    if (blk && lh.ok)
+        for (int i = 0; i < blk_len && i < (int)lh.blk.size(); ++i) blk[i] = lh.blk[i];
     return FPF_OK;
 }
 

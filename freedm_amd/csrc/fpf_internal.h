@@ -210,6 +210,35 @@ struct WaveDev {
     int32_t coop_spin;          // polls before a wait gives up (2^21; FPF_TEST_COOP_SPIN overrides, tests only)
 };
 
+// Lane kernel (fpf_lane.hip, fast mode, feeders of at most LANE_NW * LANE_NS
+// branches): one lane per scenario, 64 scenarios per workgroup of LANE_NW
+// wavefronts; the depth-first positions are dealt to the waves in contiguous
+// runs, position q of wave w in slot i (q = first_w + i), the slot's V (then its
+// scan values) in that wave's registers for the whole solve.  Every wave runs
+// the same code; what differs per slot is wave-uniform data read with scalar
+// loads.  The waves meet in LDS (per-lane columns: one scenario per lane in
+// every wave) at four barriers per sweep.
+constexpr int LANE_NW = 8, LANE_NS = 16, LANE_BD = 8, LANE_TW = 8;
+struct LaneDev {
+    int32_t n, nn, nl;       // branches, nodes, Dl rows
+    int32_t nE, nG;          // published backward (subtree-end) / forward (tap, first - 1) entries
+    int32_t nblk, mxitr;
+    double V0[6], rv0[3], s3, eps, lb_v, ub_v, guard_k;
+    // [LANE_NW][4][ns] per wave, per field, per slot (a wave's run padded with
+    // dummy slots: row 0, node -1, gather the zero entry, block of the wave's last
+    // position): Dl row; node id; backward info: bit 0 a real slot, bits 1-15
+    // published index + 1 (a subtree end), bits 16-31 the index the slot gathers
+    // (its subtree's end; the zero entry for a dummy); forward info: bits 0-15
+    // published index + 1, bits 16-29 block, bit 30 the slot starts a block or is
+    // the wave's first (its V offset is resolved there)
+    const int32_t *slot;
+    // [LANE_NW][ns][LANE_TW]: TEMP as z_aa - zm (a = 0..2), zm (complex), 0 on a
+    // dummy slot
+    const double *temp;
+    int32_t ns;              // slots per wave (4, 8, 12 or 16: the kernel instantiation)
+    const int32_t *blk;      // [nblk][1 + 2 LANE_BD]: depth, then (tap, first - 1) forward indices
+};
+
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).
 struct OutDev {
     double *vpolar, *pqb, *pql, *v_re, *v_im;
@@ -378,6 +407,9 @@ hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss
                             const double *vmin, const double *vmax, double lb_v, double ub_v,
                             double *d_agg, double *partials, unsigned *ticket, hipStream_t st);
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+hipError_t launch_lane(const LaneDev &l, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
+size_t lane_lds_bytes(const LaneDev &l);
+int lane_min_scen();   // launches from this size run the lane kernel (FPF_LANE: 0 never, 1 always, n)
 // the staging tables of a wave-kernel geometry (WaveDev::stage_smaj / stage_l0,
 // [u][NT] int2 each); returns the chunks per thread, 0 if above the kernel's limit
 int wave_stage_tables(const WaveDev &w, std::vector<int32_t> &smaj, std::vector<int32_t> &l0);

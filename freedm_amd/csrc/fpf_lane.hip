@@ -1,0 +1,624 @@
+// fpf_lane.hip -- the lane kernel (fast mode, fpf_opts.exact = 0): every sweep
+// of DPF_return7 (Broker/src/vvc/DPF_return7.cpp:104-217) with ONE LANE PER
+// SCENARIO, 64 scenarios per workgroup of LANE_NW = 8 wavefronts.
+//
+// The wave kernel (fpf_wave.hip) spreads one scenario over 32 lanes and pays for
+// it in the sweep: a fp64 DPP scan moves every double as two 32-bit halves (31 %
+// of its VALU), and ~100 LDS round trips per wave-sweep sit on the dependency
+// chain.  Here a scenario's nodes are spread over the eight
+// WAVES of a workgroup instead, and the 64 lanes of every wave are 64 scenarios:
+//   * the depth-first order of the wave kernel (in-block child first, so every
+//     subtree and every block is a contiguous range of positions) is dealt to the
+//     waves in contiguous runs; position q of wave w lives in slot i = q - first_w,
+//     its V (then its scan values) in that wave's registers for the whole solve --
+//     x[16][3] complex, 192 VGPRs, two waves per SIMD;
+//   * all of a slot's arithmetic is per lane: the load current, a sequential
+//     prefix over the wave's slots, the branch drop -- no cross-lane moves at all;
+//   * what differs between the waves (rows, TEMP, which scan values to publish or
+//     gather) is wave-uniform data, read with scalar loads: every wave runs the
+//     same code (one code body, instruction-cache friendly, no per-feeder build);
+//   * the waves meet in LDS, in per-lane columns (lane l of every wave is
+//     scenario l): the backward sweep is the prefix scan E of IL, Ib(q) =
+//     E[last(q)] - E[q - 1], with the wave totals giving each wave its carry and
+//     the subtree ends published; the forward sweep is the prefix scan G of the
+//     drops, V(q) = V0 - off(block) - G[q], off(b) = sum over b's block-ancestor
+//     chain of G[tap] - G[first - 1] (the wave kernel's algebra, fpf_wave.hip).
+//     Four barriers per sweep: wave totals of E, published E, wave totals of G,
+//     published G.
+// The loads (P, Q) are read from the caller's scenario-fastest batch every sweep
+// (64 consecutive doubles per load instruction; the re-reads hit the Infinity
+// Cache); V leaves from registers in the sweep a scenario finishes.  Converged
+// lanes sweep along (their V is already written) until the workgroup's last
+// scenario is done, as in the wave kernel.
+//
+// Scope (fpf_api.cpp: analyse_lane): well-formed tree-order feeders of at most
+// LANE_NW * LANE_NS = 128 branches, no zeroed phases, every branch's TEMP with one
+// common off-diagonal value, light outputs (V, iters, status, loss, vmin, vmax,
+// errmx, guard), scenario-fastest batches, the feeder's own source.  Everything
+// else runs the wave kernel.
+//
+// Arithmetic: the wave kernel's quantities (refined-reciprocal load currents,
+// symmetric-TEMP FMA drops, prefix-sum differences, the loss as s3 sum
+// Re(drop conj(Ib))) in another association; checked at the north-star bar
+// against the oracle (tests/test_gpu_lane.py).  The convergence guard's band
+// covers this kernel's order of Ib(0): a sequential sum over <= 16 slots, then 8
+// wave totals (<= 24 u sum |IL| against the band's 2 (Nb + 24) u).
+#include <array>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <set>
+
+#include "fpf_internal.h"
+#include "fpf_math.hpp"
+#include "fpf_wave_common.h"
+#include "fpf_generic_body.h"
+
+namespace fpf {
+
+// diagnostic ablation builds (tools/runs: FPF_LANE_ABL bits; results are wrong
+// when set): 1 the loads come from a constant instead of memory, 2 the backward
+// gathers read the slot's own value instead of LDS, 4 every scenario takes
+// exactly 5 sweeps (so that the other bits compare at equal work)
+#ifndef FPF_LANE_ABL
+#define FPF_LANE_ABL 0
+#endif
+// slots of loads in flight ahead of the load currents (registers: 12 per slot)
+#ifndef FPF_LANE_PF
+#define FPF_LANE_PF 1
+#endif
+
+namespace {
+
+typedef const __attribute__((address_space(4))) double cdbl;      // constant address space:
+typedef const __attribute__((address_space(4))) int32_t cint;     // scalar loads
+
+
+// every wave's LDS stores before it, every wave's LDS reads after it; the vector
+// memory loads in flight (the next slots' P, Q) are not waited for
+__device__ __forceinline__ void lane_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// a slot's new values stay where they are computed: without it the compiler
+// sinks each slot's V = cb - G to the loop latch (its only other use), keeping
+// every slot's block constant alive across the phase (12 registers per slot)
+__device__ __forceinline__ void pin(cx (&v)[3]) {
+    __asm__ volatile("" : "+v"(v[0].re), "+v"(v[0].im), "+v"(v[1].re), "+v"(v[1].im), "+v"(v[2].re), "+v"(v[2].im));
+}
+
+__device__ __forceinline__ cx ldc(const double2 *a, int i) {
+    const double2 v = a[i];
+    return mk(v.x, v.y);
+}
+__device__ __forceinline__ void stc(double2 *a, int i, cx v) { a[i] = make_double2(v.re, v.im); }
+
+// buffer resources on wave-uniform bases (scalar registers) with the lane's
+// 32-bit offset: no 64-bit address per load or store lives in vector registers.
+// The loads [6][Nl][B]: one resource on the batch, element (f, row) of this
+// lane's scenario at byte ((f Nl + row) B + s) 8 = a scalar offset (f Nl + row)
+// 8B plus the lane's 8s (the host keeps the batch below 4 GiB, fpf_api.cpp)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const double *base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_lane(double v, double *base, unsigned vo) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v),
+                                          rsrc_at(base), vo, 0, 0);
+}
+__device__ __forceinline__ void load_pq(double (&d)[6], __amdgpu_buffer_rsrc_t rp, int row, unsigned plane,
+                                        unsigned bb, unsigned vo) {
+    const unsigned ro = (unsigned)row * bb;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+        if (FPF_LANE_ABL & 1) d[f] = 1e-3 * (f + 1) + 1e-6 * row + 1e-9 * vo;
+        else d[f] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, vo, ro + f * plane, 0));
+    }
+}
+
+}  // namespace
+
+// one sweep's phases on the wave's NS slots (every slot is live: a wave's run of
+// positions is padded with dummy slots whose loads scale by 0 and whose TEMP is 0,
+// so their IL, Ib and drop are exactly 0 and no slot needs a branch)
+template <int NS>
+struct LaneSweep {
+    // ---- load currents (:106-130) and the wave's local prefix E of IL; the flat
+    // start's first sweep is the same arithmetic on x = V0 (DPF_return7.cpp:92-96),
+    // plus the guard's sum |S|_1 (a branch on one register only).  The loads run
+    // FPF_LANE_PF slots ahead (sn[k]: slot i + 1 + k); the rows come from the
+    // wave's row table, read once per phase
+    __device__ __forceinline__ static void currents(cx (&x)[NS][3], double &sabs, bool flat, double (&sn)[FPF_LANE_PF][6],
+                                                    __amdgpu_buffer_rsrc_t rp, cint *tab, unsigned plane, unsigned bb,
+                                                    unsigned so, double inv_s3) {
+        int row[NS], ei[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) row[i] = tab[i];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) ei[i] = tab[2 * NS + i];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            double sc[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) sc[k] = sn[0][k];
+#pragma unroll
+            for (int j = 0; j + 1 < FPF_LANE_PF; ++j)
+#pragma unroll
+                for (int k = 0; k < 6; ++k) sn[j][k] = sn[j + 1][k];
+            if (i + FPF_LANE_PF < NS) load_pq(sn[FPF_LANE_PF - 1], rp, row[i + FPF_LANE_PF], plane, bb, so);
+            const double isc = (ei[i] & 1) ? inv_s3 : 0.0;   // (uniform) 0 on a dummy slot
+            if (flat) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) sabs = fma(fabs(sc[k]), isc, sabs);
+            }
+            __asm__ volatile("" : "+v"(sabs));
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const double P = sc[2 * p], Q = sc[2 * p + 1];
+                // IL = conj(S/V) = conj(S) V / |V|^2, one refined reciprocal
+                const cx v = x[i][p];
+                const double d2 = fma(v.re, v.re, v.im * v.im);
+                double r = __builtin_amdgcn_rcp(d2);
+                r = fma(r, fma(-d2, r, 1.0), r) * isc;
+                const cx il = mk(fma(P, v.re, Q * v.im) * r, fma(P, v.im, -(Q * v.re)) * r);
+                x[i][p] = i == 0 ? il : cadd(x[i - 1][p], il);
+            }
+            pin(x[i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // ---- backward sweep (:134-160) Ib = E[last] - E[q - 1] on the globalised E
+    // (x = carry + local prefix), slots in descending order so that E[q - 1] is
+    // still in place; the branch drops lng (Ib . Zl) (:163-178) over it; then their
+    // local prefix G in ascending order.  FIN (a scenario finishes in this sweep):
+    // also its part of the loss, sum Re(drop conj(Ib)) (s3 times it is PQb(0).re -
+    // sum_k PQL(k).re on a feeder without zeroed phases, fpf_wave_body.h)
+    __device__ __forceinline__ static void drops(cx (&x)[NS][3], double &lp, bool any_fin, const double2 *cw,
+                                                 const double2 *EG, cint *tab, cdbl *tmp, int lane) {
+        int ei[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) ei[i] = tab[2 * NS + i];
+        cx el[3], en[3];
+        {
+            const int li = (ei[NS - 1] >> 16) & 0xffff;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) en[p] = ldc(EG, (li * 3 + p) * 64 + lane);
+        }
+#pragma unroll
+        for (int i = NS - 1; i >= 0; --i) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) el[p] = en[p];
+            if (i > 0) {   // the next slot's gather, in flight during this slot's arithmetic
+                const int li = (ei[i - 1] >> 16) & 0xffff;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) en[p] = (FPF_LANE_ABL & 2) ? x[i - 1][p] : ldc(EG, (li * 3 + p) * 64 + lane);
+            }
+            cx ib[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ib[p] = csub(el[p], i > 0 ? x[i - 1][p] : ldc(cw, p * 64 + lane));   // (E[-1] = the carry)
+            cdbl *const t = tmp + i * LANE_TW;
+            const cx zm = mk(t[6], t[7]);
+            const cx sm = cadd(cadd(ib[0], ib[1]), ib[2]);
+            const cx ms = mk(fma(zm.re, sm.re, -(zm.im * sm.im)), fma(zm.re, sm.im, zm.im * sm.re));
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const cx d = mk(t[2 * p], t[2 * p + 1]);
+                const cx b = ib[p];
+                const cx g = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
+                x[i][p] = g;
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) lp = fma(x[i][p].re, ib[p].re, fma(x[i][p].im, ib[p].im, lp));
+            pin(x[i]);
+            __asm__ volatile("" : "+v"(lp));   // (else summed where it is stored, keeping every Ib alive)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 1; i < NS; ++i) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) x[i][p] = cadd(x[i - 1][p], x[i][p]);
+            pin(x[i]);
+        }
+    }
+
+    // ---- forward sweep (:163-195): V = (V0 - off(block) - carry) - G, the block
+    // offset resolved where a block starts (and at the wave's first slot); FIN: the
+    // finishing scenarios' V out (rows [3][Nn][B]) and their extremes
+    __device__ __forceinline__ static void voltages(cx (&x)[NS][3], const double2 *vw, const double2 *EG, cint *tab,
+                                                    cint *blk, int lane) {
+        int gv[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) gv[i] = tab[3 * NS + i];
+        cx cb[3];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const int gi = gv[i];
+            if (gi & (1 << 30)) {   // (uniform; always at slot 0)
+                cint *const bt = blk + ((gi >> 16) & 0x3fff) * (1 + 2 * LANE_BD);
+                const int dep = bt[0];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) cb[p] = ldc(vw, p * 64 + lane);   // V0 - the carry of G
+#pragma nounroll
+                for (int j = 0; j < dep; ++j) {
+                    const int ta = bt[1 + 2 * j], fm = bt[2 + 2 * j];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) cb[p] = cadd(cb[p], ldc(EG, (fm * 3 + p) * 64 + lane));
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) cb[p] = csub(cb[p], ldc(EG, (ta * 3 + p) * 64 + lane));
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) x[i][p] = csub(cb[p], x[i][p]);
+            pin(x[i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // ---- a scenario's last sweep: its V out (node rows of [3][Nn][B]) and the
+    // extremes of the wave's slots (V_abc_list.cpp:7-81 with every row kept)
+    __device__ __forceinline__ static void finish(const cx (&x)[NS][3], double &mn, double &mx, bool fin, cint *tab,
+                                                  const OutDev &o, int nn, unsigned B, unsigned so) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const double m2 = fma(x[i][p].re, x[i][p].re, x[i][p].im * x[i][p].im);
+                mn = fmin(mn, m2);
+                mx = fmax(mx, m2);
+            }
+            const int node = tab[NS + i];
+            if (fin && node >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const size_t r = ((size_t)p * nn + node) * B;
+                    if (o.v_re) st_lane(x[i][p].re, o.v_re + r, so);
+                    if (o.v_im) st_lane(x[i][p].im, o.v_im + r, so);
+                }
+            }
+        }
+    }
+};
+
+template <int NS>
+__global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, int B, const double *__restrict__ pq,
+                                                                   OutDev o) {
+    constexpr int NW = LANE_NW;
+    typedef LaneSweep<NS> SW;
+    extern __shared__ double2 lds[];
+    double2 *const WT = lds;                               // [NW][3][64] wave totals (E, then G)
+    double2 *const IBO = WT + NW * 3 * 64;                 // [3][64] Ib(0) of the last sweep
+    double *const RES = (double *)(IBO + 3 * 64);          // [NW][4][64] per wave: loss part, min / max |V|^2, sum |S|_1
+    double2 *const EG = (double2 *)(RES + NW * 4 * 64);    // [max(nE, nG) + 1][3][64] published E, then G; last: 0
+    __shared__ int fix_n, fix_ids[64];
+    __shared__ double res[64][4];
+    __shared__ int last_wg;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int s = (int)blockIdx.x * 64 + lane;
+    const bool live = s < B;
+    const unsigned so = 8u * (unsigned)(live ? s : B - 1);   // byte offset (lanes past the batch read its last scenario)
+    const unsigned bb = 8u * (unsigned)B;                     // bytes per Dl row of a field plane
+    const int nl = f.nl, nn = f.nn;
+    cint *const tab0 = (cint *)f.slot + 4 * w * NS;   // [4][NS]: rows, nodes, backward, forward info
+    cdbl *const tmp0 = (cdbl *)f.temp + (size_t)w * NS * LANE_TW;
+    // one buffer resource on the batch [6][Nl][B] (P1 Q1 P2 Q2 P3 Q3 planes)
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void *)pq, 0, (int)0xffffffffu, 0x00020000);
+    const unsigned plane = (unsigned)nl * bb;   // bytes per field plane
+    const double inv_s3 = 1.0 / f.s3;
+    const double eps2 = f.eps * f.eps;
+    cx v0[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) v0[p] = mk(f.V0[2 * p], f.V0[2 * p + 1]);
+
+    if (threadIdx.x == 0) fix_n = 0;
+    if ((int)threadIdx.x < 3 * 64) {
+        IBO[threadIdx.x] = make_double2(0.0, 0.0);
+        EG[max(f.nE, f.nG) * 3 * 64 + threadIdx.x] = make_double2(0.0, 0.0);   // the permanent zero entry
+    }
+    for (int i = threadIdx.x; i < NW * 4 * 64; i += NW * 64) {
+        const int q = (i >> 6) & 3;
+        RES[i] = q == 1 ? INFINITY : (q == 2 ? -INFINITY : 0.0);
+    }
+
+    cx x[NS][3];   // the slots' state: V, then E, Ib -> G, then V again
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) x[i][p] = v0[p];
+    bool done = !live;
+    double gmin = INFINITY;   // (wave 0) closest |errmx^2 - eps^2| of a decision in the coarse band
+    int stat = 1;             // (wave 0) the scenario's status
+    double sn[FPF_LANE_PF][6];   // the next slots' P, Q
+#pragma unroll
+    for (int j = 0; j < FPF_LANE_PF; ++j) load_pq(sn[j], rp, tab0[j], plane, bb, so);
+    for (int it = 0;; ++it) {
+        // the slot tables' base opaque per sweep: their scalar loads stay inside the
+        // loop instead of hundreds of scalar registers hoisted (and spilled) across it
+        cint *tab = tab0;
+        cdbl *tmp = tmp0;
+        cint *blk = (cint *)f.blk;
+        __asm__ volatile("" : "+s"(tab), "+s"(tmp), "+s"(blk));
+        double sabs = 0.0;
+        SW::currents(x, sabs, it == 0, sn, rp, tab, plane, bb, so, inv_s3);
+        if (it == 0) RES[(w * 4 + 3) * 64 + lane] = sabs;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
+        lane_barrier();   // B1: the wave totals of E
+
+        // ---- the carry of this wave and Ib(0) = the total, summed in wave order (the
+        // same association in every wave, so every wave takes the same decisions)
+        cx carry[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+#pragma nounroll
+        for (int u = 0; u < w; ++u)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) carry[p] = cadd(carry[p], ldc(WT, (u * 3 + p) * 64 + lane));
+        cx tot[3] = {carry[0], carry[1], carry[2]};
+#pragma nounroll
+        for (int u = w; u < NW; ++u)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) tot[p] = cadd(tot[p], ldc(WT, (u * 3 + p) * 64 + lane));
+        // ---- convergence on the substation branch (:199-217)
+        double err2 = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const cx io = ldc(IBO, p * 64 + lane);
+            const double dr = tot[p].re - io.re, di = tot[p].im - io.im;
+            err2 = fmax(err2, fma(dr, dr, di * di));
+        }
+        const bool conv = (FPF_LANE_ABL & 4) ? false : err2 < eps2;
+        const bool fin = !done && (conv || it == ((FPF_LANE_ABL & 4) ? 4 : f.mxitr - 1));
+        if (w == 0 && o.flag_count) {
+            // the guard record (fpf_wave_body.h): decisions within 2^-9 of eps^2
+            const double dd = fabs(err2 - eps2);
+            if (!done && dd <= 0x1p-9 * eps2) gmin = fmin(gmin, dd);
+        }
+        const bool any_fin = __ballot(fin) != 0;
+        // E made global (x = carry + the local prefix) and published at the subtree
+        // ends (the leaves; every slot gathers one)
+        int ev[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) ev[i] = tab[2 * NS + i];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) x[i][p] = cadd(carry[p], x[i][p]);
+            pin(x[i]);
+            const int pe = ((ev[i] >> 1) & 0x7fff) - 1;
+            if (pe >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stc(EG, (pe * 3 + p) * 64 + lane, x[i][p]);
+            }
+        }
+        lane_barrier();   // B2: published E (every wave has read IBO and the wave totals)
+        if (w == 0) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) stc(IBO, p * 64 + lane, tot[p]);
+        }
+        // the wave's carry parked in its WT entry for the backward sweep's slot 0
+        // (12 registers fewer through it)
+        double2 *const cw = WT + w * 3 * 64;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) stc(cw, p * 64 + lane, carry[p]);
+
+        double lp = 0.0;
+        SW::drops(x, lp, any_fin, cw, EG, tab, tmp, lane);
+        // WT is free again (every wave read it before B2)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
+        if (fin) RES[(w * 4 + 0) * 64 + lane] = lp;
+#pragma unroll
+        for (int j = 0; j < FPF_LANE_PF; ++j)   // the next sweep's first loads, in flight across the barriers
+            load_pq(sn[j], rp, tab[j], plane, bb, so);
+        lane_barrier();   // B3: the wave totals of G (every wave has read its gathered E)
+
+        cx carryg[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+#pragma nounroll
+        for (int u = 0; u < w; ++u)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) carryg[p] = cadd(carryg[p], ldc(WT, (u * 3 + p) * 64 + lane));
+        // publish G at the taps and before the lateral blocks
+        int gv[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) gv[i] = tab[3 * NS + i];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const int pg = (gv[i] & 0xffff) - 1;
+            if (pg >= 0) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) stc(EG, (pg * 3 + p) * 64 + lane, cadd(carryg[p], x[i][p]));
+            }
+        }
+        lane_barrier();   // B4: published G
+
+        // V0 - the carry of G, parked in the wave's WT entry (every wave has read the
+        // G totals before B4)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) stc(cw, p * 64 + lane, csub(v0[p], carryg[p]));
+        SW::voltages(x, cw, EG, tab, blk, lane);
+        double mn = INFINITY, mx = -INFINITY;
+        if (any_fin) SW::finish(x, mn, mx, fin, tab, o, nn, (unsigned)B, so);
+        if (fin) {
+            RES[(w * 4 + 1) * 64 + lane] = mn;
+            RES[(w * 4 + 2) * 64 + lane] = mx;
+            if (w == 0) {
+                stat = conv ? FPF_CONVERGED : FPF_NONCONVERGED;
+                if (o.iters) o.iters[s] = it + 1;
+                if (o.status) o.status[s] = (int8_t)stat;
+                if (o.errmx) o.errmx[s] = sqrt(err2);
+            }
+        }
+        done = done || fin;
+        if (__ballot(!done) == 0) break;   // (the same in every wave)
+    }
+    lane_barrier();   // RES complete
+
+    // ---- per scenario (wave 0): loss (VoltVarCtrl.cpp:1152-1161), Vmin / Vmax
+    // (V_abc_list.cpp:7-81 with every row kept, VoltVarCtrl.cpp:1201-1207), the
+    // guard band, the substation row of V
+    const int nsb = min(64, B - (int)blockIdx.x * 64);
+    if (w == 0) {
+        double ls = 0.0, sa = 0.0, mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const double m2 = fma(v0[p].re, v0[p].re, v0[p].im * v0[p].im);
+            mn = fmin(mn, m2);
+            mx = fmax(mx, m2);
+        }
+        for (int u = 0; u < NW; ++u) {
+            ls += RES[(u * 4 + 0) * 64 + lane];
+            mn = fmin(mn, RES[(u * 4 + 1) * 64 + lane]);
+            mx = fmax(mx, RES[(u * 4 + 2) * 64 + lane]);
+            sa += RES[(u * 4 + 3) * 64 + lane];
+        }
+        const double loss = f.s3 * ls, vmin = sqrt(mn), vmax = sqrt(mx);
+        if (live) {
+            if (o.loss) o.loss[s] = loss;
+            if (o.vmin) o.vmin[s] = vmin;
+            if (o.vmax) o.vmax[s] = vmax;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const size_t r = (size_t)p * nn * (unsigned)B + (unsigned)s;
+                if (o.v_re) __builtin_nontemporal_store(v0[p].re, o.v_re + r);
+                if (o.v_im) __builtin_nontemporal_store(v0[p].im, o.v_im + r);
+            }
+        }
+        res[lane][0] = loss;
+        res[lane][1] = vmin;
+        res[lane][2] = vmax;
+        res[lane][3] = stat == FPF_CONVERGED ? 0.0 : 1.0;
+        // the guard band (fpf_wave_body.h): errmx within tau = guard_k sum_k |IL_k|_1
+        // of eps at a decision, sum_k |IL_k|_1 <= 1.25 sqrt2 sum_k |S_k|_1 / min_k |V_k|
+        if (o.flag_count && live) {
+            const bool cand = gmin < INFINITY;
+            const double tau = 1.25 * f.guard_k * 1.4142135623730951 * sa / sqrt(mn);
+            const bool near = cand && gmin <= 2.0 * f.eps * (1.0 + 0x1p-9) * tau;
+            if (near) guard_flag(o, s, &fix_n, fix_ids);
+            if (o.guard) o.guard[s] = near ? 1 : 0;
+        } else if (live && o.guard) {
+            o.guard[s] = 0;
+        }
+    }
+
+    // ---- fused batch aggregate (the wave kernel's: per-workgroup partial in
+    // scenario order, ticket, the last workgroup folds in workgroup order)
+    constexpr int NT = NW * 64;
+    const bool agg = o.agg != nullptr;
+    if (agg) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double ls = 0, mn = INFINITY, mx = -INFINITY, nc = 0, nnc = 0, no = 0, nu = 0;
+            for (int j = 0; j < nsb; ++j) {
+                if (res[j][3] == 0.0) {
+                    ls += res[j][0];
+                    mn = fmin(mn, res[j][1]);
+                    mx = fmax(mx, res[j][2]);
+                    nc += 1;
+                    if (res[j][2] > f.ub_v) no += 1;
+                    if (res[j][1] < f.lb_v) nu += 1;
+                } else {
+                    nnc += 1;
+                }
+            }
+            const double part[8] = {ls, mn, mx, nc, nnc, no, nu, (double)nsb};
+            double *dst = o.partials + 8 * (size_t)blockIdx.x;
+            for (int q = 0; q < 8; ++q) __hip_atomic_store(dst + q, part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned t = __hip_atomic_fetch_add(o.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_wg = t == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last_wg) {
+            double a[8] = {0, INFINITY, -INFINITY, 0, 0, 0, 0, 0};
+            for (unsigned b = threadIdx.x; b < gridDim.x; b += NT) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const double r = __hip_atomic_load(o.partials + 8 * (size_t)b + q, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                    a[q] = q == 1 ? fmin(a[q], r) : (q == 2 ? fmax(a[q], r) : a[q] + r);
+                }
+            }
+            double *sh = (double *)lds;   // [8][NT] (the sweep's LDS is dead)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sh[q * NT + threadIdx.x] = a[q];
+            __syncthreads();
+            for (int h = NT / 2; h > 0; h >>= 1) {
+                if ((int)threadIdx.x < h) {
+                    const int t = threadIdx.x;
+                    sh[0 * NT + t] += sh[0 * NT + t + h];
+                    sh[1 * NT + t] = fmin(sh[1 * NT + t], sh[1 * NT + t + h]);
+                    sh[2 * NT + t] = fmax(sh[2 * NT + t], sh[2 * NT + t + h]);
+#pragma unroll
+                    for (int q = 3; q < 8; ++q) sh[q * NT + t] += sh[q * NT + t + h];
+                }
+                __syncthreads();
+            }
+            if (threadIdx.x < 8) o.agg[threadIdx.x] = sh[threadIdx.x * NT];
+            if (threadIdx.x == 0) __hip_atomic_store(o.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0 && o.flag_out)
+                *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (o.fix_dev) {
+        // the guard's local mode (a solve without an aggregate): the scenarios this
+        // workgroup flagged are re-solved on the exact body by its first wave, after
+        // every store of the fast results has landed (fpf_wave_body.h)
+        __shared__ OutDev osh;
+        __syncthreads();
+        if (fix_n > 0) {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == 0) osh = o;
+            __syncthreads();
+            if (w == 0) g3::g3_fixup_local(o.fix_dev, B, pq, (double *)lds, &osh, fix_ids, fix_n);
+        }
+    }
+}
+
+size_t lane_lds_bytes(const LaneDev &l) {
+    const size_t col = 3 * 64 * 16;   // one published entry: 3 phases x 64 lanes x complex
+    return (size_t)LANE_NW * col + 3 * 64 * 16 + (size_t)LANE_NW * 4 * 64 * 8 + (size_t)(std::max(l.nE, l.nG) + 1) * col;
+}
+
+int lane_min_scen() {
+    const char *e = getenv("FPF_LANE");
+    if (!e) return 1 << 30;   // (until measured: off by default)
+    const int v = atoi(e);
+    return v <= 0 ? (1 << 30) : v;
+}
+
+static std::atomic<int> g_lane_launches{0};
+extern "C" int fpf_lane_launches(void) { return g_lane_launches.load(); }
+
+hipError_t launch_lane(const LaneDev &l, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
+    void (*k)(LaneDev, int, const double *, OutDev) = nullptr;
+    switch (l.ns) {
+        case 4: k = dpf_lane_kernel<4>; break;
+        case 8: k = dpf_lane_kernel<8>; break;
+        case 12: k = dpf_lane_kernel<12>; break;
+        case 16: k = dpf_lane_kernel<16>; break;
+        default: return hipErrorInvalidValue;
+    }
+    const size_t lds = lane_lds_bytes(l);
+    static std::mutex mu;
+    static std::set<std::array<int, 2>> attr_done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!attr_done.count({dev, l.ns})) {
+            hipFuncAttributes fa{};
+            hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - (int)fa.sharedSizeBytes);
+            if (e != hipSuccess) return e;
+            attr_done.insert({dev, l.ns});
+        }
+    }
+    const unsigned grid = (unsigned)((n_scen + 63) / 64);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(LANE_NW * 64), lds, st, l, n_scen, pq, o);
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) g_lane_launches.fetch_add(1);
+    return e;
+}
+
+}  // namespace fpf

@@ -3,8 +3,10 @@
 // per device (shard_range of freedm_amd/dist.py), every device solves its
 // shard on its own stream with its own copy of the feeder tables, and the
 // per-device batch aggregates are combined by RCCL over xGMI -- the path's
-// only collective: a sum of the 8 aggregate doubles, a min
-// of vmin and a max of vmax.  Per-scenario results never cross devices; they
+// only collective: one all-gather of every device's 8
+// aggregate doubles, folded in device order on the host (fpf_aggregate_fold,
+// the fold of the one-process-per-GPU form, dist.py: bit-identical aggregates).
+// Per-scenario results never cross devices; they
 // return to the caller's host arrays at their global scenario index.
 //
 // The reference caller is single-threaded C++ (VoltVarCtrl.cpp:1141 on the
@@ -25,6 +27,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -83,7 +86,8 @@ struct fpf_multi {
     std::vector<fpf_feeder *> feeder;
     std::vector<ncclComm_t> comm;
     std::vector<hipStream_t> stream;
-    // per device: d_agg[20] = aggregate (8) | summed (8) | min, max reduced
+    // per device: d_agg[8 + 8 n] = the shard's aggregate (8) | every device's, gathered
+    // in device order (8 n) by the one collective
     std::vector<double *> d_agg;
     // per device: the shard's per-scenario scalars (the aggregate reads status /
     // loss / vmin / vmax; iters, errmx, guard as asked) and their pinned copy
@@ -148,6 +152,10 @@ extern "C" long fpf_multi_schedule(int n_gpus, long n_scen, long chunk, long *op
     }
     return (long)v.size();
 }
+
+// collective calls fpf_multi_solve has issued in this process (one per solve)
+static std::atomic<long> g_multi_collectives{0};
+extern "C" long fpf_multi_collectives(void) { return g_multi_collectives.load(); }
 
 extern "C" void fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate *out) {
     if (!out) return;
@@ -233,7 +241,7 @@ extern "C" int fpf_multi_create(int n_gpus, const double *dl, int nl, int ncols,
             return rc;
         }
         if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&m->stream[d], hipStreamNonBlocking) != hipSuccess ||
-            hipMalloc(&m->d_agg[d], 20 * sizeof(double)) != hipSuccess ||
+            hipMalloc(&m->d_agg[d], (8 + 8 * (size_t)n_gpus) * sizeof(double)) != hipSuccess ||
             hipEventCreateWithFlags(&m->ev[0][d], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&m->ev[1][d], hipEventDisableTiming) != hipSuccess) {
             g_create_err = "fpf_multi_create: device " + std::to_string(d) + ": stream / buffer allocation failed";
@@ -399,18 +407,22 @@ extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const
         }
         MHIP(m, hipMemcpyAsync(m->h_scal[d], sc, soff[7], hipMemcpyDeviceToHost, st));
     }
-    // the one collective: [loss_sum .. n_scen] summed, vmin min'd, vmax max'd
+    // the one collective: an all-gather of every device's 8-double aggregate (one
+    // ncclAllGather per communicator rank, grouped), folded on the host in device
+    // order by fpf_aggregate_fold -- the same rows and the same fold as the
+    // one-process-per-GPU form (dist.py: gather_aggregates + fold_aggregates), so
+    // the two forms give bit-identical aggregates
     MNCCL(m, ncclGroupStart());
     for (int d = 0; d < m->n; ++d) {
         MHIP(m, hipSetDevice(d));
-        MNCCL(m, ncclAllReduce(m->d_agg[d], m->d_agg[d] + 8, 8, ncclDouble, ncclSum, m->comm[d], m->stream[d]));
-        MNCCL(m, ncclAllReduce(m->d_agg[d] + 1, m->d_agg[d] + 16, 1, ncclDouble, ncclMin, m->comm[d], m->stream[d]));
-        MNCCL(m, ncclAllReduce(m->d_agg[d] + 2, m->d_agg[d] + 17, 1, ncclDouble, ncclMax, m->comm[d], m->stream[d]));
+        MNCCL(m, ncclAllGather(m->d_agg[d], m->d_agg[d] + 8, 8, ncclDouble, m->comm[d], m->stream[d]));
     }
     MNCCL(m, ncclGroupEnd());
-    double h[20];
+    g_multi_collectives.fetch_add(1);
+    std::vector<fpf_aggregate> rows((size_t)m->n);
     MHIP(m, hipSetDevice(0));
-    MHIP(m, hipMemcpyAsync(h, m->d_agg[0], sizeof(h), hipMemcpyDeviceToHost, m->stream[0]));
+    MHIP(m, hipMemcpyAsync(rows.data(), m->d_agg[0] + 8, 8 * sizeof(double) * (size_t)m->n, hipMemcpyDeviceToHost,
+                           m->stream[0]));
     for (int d = 0; d < m->n; ++d) {
         MHIP(m, hipSetDevice(d));
         MHIP(m, hipStreamSynchronize(m->stream[d]));
@@ -425,14 +437,7 @@ extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const
         if (fr) return mfail(m, fr, std::string("device ") + std::to_string(d) + ": " + fpf_last_error(m->ctx[d]));
     }
     fpf_aggregate a;
-    a.loss_sum = h[8];
-    a.vmin = h[16];
-    a.vmax = h[17];
-    a.n_conv = h[11];
-    a.n_nonconv = h[12];
-    a.n_over = h[13];
-    a.n_under = h[14];
-    a.n_scen = h[15];
+    fpf_aggregate_fold(rows.data(), m->n, &a);
     if (agg) *agg = a;
     return (int)a.n_nonconv;
 }

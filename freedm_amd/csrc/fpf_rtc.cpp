@@ -332,7 +332,7 @@ const RtcApi &rtc_api() {
 // the compiled code object's kernel descriptor (AMDHSA ABI): registers per
 // lane (VGPRs + AGPRs, COMPUTE_PGM_RSRC1 granule 8 on gfx950) and the fixed
 // private segment; false if the object has no such kernel
-bool co_kernel_desc(const std::string &co, const std::string &kname, int *regs, int *scratch) {
+bool co_kernel_desc(const std::string &co, const std::string &kname, int *regs, int *scratch, int *group = nullptr) {
     const auto *eh = reinterpret_cast<const Elf64_Ehdr *>(co.data());
     if (co.size() < sizeof(Elf64_Ehdr) || memcmp(eh->e_ident, ELFMAG, SELFMAG) || eh->e_shoff + (size_t)eh->e_shnum *
         sizeof(Elf64_Shdr) > co.size())
@@ -348,11 +348,13 @@ bool co_kernel_desc(const std::string &co, const std::string &kname, int *regs, 
             const Elf64_Shdr &sec = sh[sym[j].st_shndx];
             const size_t off = sec.sh_offset + (sym[j].st_value - sec.sh_addr);
             if (off + 64 > co.size()) return false;
-            uint32_t rsrc1, pss;
-            memcpy(&pss, co.data() + off + 4, 4);     // kernel_descriptor_t: +0 group, +4 private segment
+            uint32_t rsrc1, pss, gss;
+            memcpy(&gss, co.data() + off + 0, 4);     // kernel_descriptor_t: +0 group, +4 private segment
+            memcpy(&pss, co.data() + off + 4, 4);
             memcpy(&rsrc1, co.data() + off + 48, 4);  // +48 compute_pgm_rsrc1
             *regs = ((int)(rsrc1 & 63) + 1) * 8;
             *scratch = (int)pss;
+            if (group) *group = (int)gss;
             return true;
         }
     }
@@ -407,10 +409,17 @@ int compile_co(const std::string &src, const char *file, const char *fname, cons
 }
 
 // can a workgroup of nt threads be resident at all: its waves share a CU's 4
-// SIMDs, each with 512 registers per lane
-bool rtc_resident(const std::string &co, const std::string &kname, int nt, std::string *err) {
-    int regs = 0, scratch = 0;
-    if (!co_kernel_desc(co, kname, &regs, &scratch)) {
+// SIMDs, each with 512 registers per lane, and its static LDS (the descriptor's
+// group segment) fits the CU's 160 KiB.  max_priv >= 0 (the hot per-plan wave
+// builds, which exist to be faster than the static kernel): a private segment
+// above max_priv bytes per lane is declined too -- the static kernel runs instead
+// of a build that spills its sweep state.  (The light builds' private segment
+// is not zero: it holds the call frame of the guard's exact re-solve,
+// g3_fixup_local, a non-inlined call -- 112 bytes on the 123-bus plan.)
+constexpr int WAVE_RTC_MAX_PRIV = 256;
+bool rtc_resident(const std::string &co, const std::string &kname, int nt, std::string *err, int max_priv = -1) {
+    int regs = 0, scratch = 0, group = 0;
+    if (!co_kernel_desc(co, kname, &regs, &scratch, &group)) {
         *err = "no kernel descriptor for " + kname;
         return false;
     }
@@ -418,6 +427,14 @@ bool rtc_resident(const std::string &co, const std::string &kname, int nt, std::
     if (regs * waves_per_simd > 512) {
         *err = "the build needs " + std::to_string(regs) + " registers per lane: a workgroup of " +
                std::to_string(nt) + " threads cannot be resident (" + rtc_api().where + ")";
+        return false;
+    }
+    if (group > 160 * 1024) {
+        *err = "the build's static LDS (" + std::to_string(group) + " bytes) exceeds a CU's 160 KiB";
+        return false;
+    }
+    if (max_priv >= 0 && scratch > max_priv) {
+        *err = "the build spills (" + std::to_string(scratch) + " bytes of private segment per lane)";
         return false;
     }
     return true;
@@ -464,6 +481,19 @@ extern "C" long fpf_rtc_compile(const char *src, const char *name_expr, int ilp,
 }
 
 extern "C" const char *fpf_rtc_compiler(void) { return rtc_api().where.c_str(); }
+
+extern "C" int fpf_rtc_resident(const char *code, size_t size, const char *kernel, int nt, int max_priv, int *regs,
+                                int *group, int *priv) {
+    if (!code || !kernel || nt < 1) return FPF_ERR_ARG;
+    const std::string co(code, size);
+    int r = 0, sc = 0, g = 0;
+    if (!co_kernel_desc(co, kernel, &r, &sc, &g)) return FPF_ERR_ARG;
+    if (regs) *regs = r;
+    if (group) *group = g;
+    if (priv) *priv = sc;
+    std::string err;
+    return rtc_resident(co, kernel, nt, &err, max_priv < 0 ? -1 : max_priv) ? 1 : 0;
+}
 
 int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
     const std::string src = rtc_source(sp);
@@ -576,12 +606,16 @@ hipFunction_t wave_rtc_function(int device, const WaveDev &w, bool full) {
     // every launch looks its build up: by the plan values the source is made of
     // (forming the ~300 KB source and comparing it as the key cost ~10 us a launch),
     // then, for a plan not seen yet, by the source itself
-    typedef std::array<int32_t, 24> PlanKey;
+    // (the key's fields are every value wave_rtc_source writes into the source --
+    // FPF_WSPEC_* and the template arguments -- plus the scheduler switch and the
+    // FPF_WAVE_RTC_DEFS text itself; keep it in step with wave_rtc_source)
+    typedef std::array<int32_t, 23> PlanKey;
     const char *se0 = getenv(w.wps ? "FPF_WBLK_RTC_SCHED" : "FPF_WAVE_RTC_SCHED");
-    const PlanKey pk = {device, (int)full, w.nn, w.nl, w.nblk, w.bdepth, w.ncomp, w.temp_sym, w.off_in_x, w.stage_u,
-                        w.out_u, w.stage_uw, w.out_uw, w.has_mask, w.has_rel, w.mxitr, w.ncode, w.wps, w.spw, w.C,
-                        w.wpb, se0 ? atoi(se0) : -1, (int32_t)std::hash<std::string>()(wave_rtc_defs(w)), 0};
-    static std::map<PlanKey, hipFunction_t> by_plan;
+    const PlanKey pk0 = {device, (int)full, w.nn, w.nl, w.nblk, w.bdepth, w.ncomp, w.temp_sym, w.off_in_x, w.stage_u,
+                         w.out_u, w.stage_uw, w.out_uw, w.has_mask, w.has_rel, w.mxitr, w.ncode, w.wps, w.spw, w.C,
+                         w.wpb, se0 ? atoi(se0) : -1, 0};
+    const std::pair<PlanKey, std::string> pk(pk0, wave_rtc_defs(w));
+    static std::map<std::pair<PlanKey, std::string>, hipFunction_t> by_plan;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = by_plan.find(pk);
@@ -620,7 +654,7 @@ hipFunction_t wave_rtc_function_src(int device, const WaveDev &w, bool full) {
     if (!(se && atoi(se) == 0)) opts = {"-mllvm", "-amdgpu-sched-strategy=iterative-ilp"};
     const int nt = 64 * (w.wps ? w.wps : w.wpb);
     if (compile_co(src, "fpf_rtc_wave.hip", nullptr, name.c_str(), opts, &code, &lowered, &err) == 0 &&
-        rtc_resident(code, lowered, nt, &err) && load_co(code, lowered, &k, &err) == 0) {
+        rtc_resident(code, lowered, nt, &err, full ? -1 : WAVE_RTC_MAX_PRIV) && load_co(code, lowered, &k, &err) == 0) {
         int stat = 0;
         if (hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.fn) == hipSuccess &&
             hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - stat) ==

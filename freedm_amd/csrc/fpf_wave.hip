@@ -117,15 +117,22 @@ static bool rtc_temp_vmem() {
     return on;
 }
 
-size_t wave_lds_bytes(const WaveDev &w) {
+// the dynamic LDS of one launch: temp_in_lds is the launched build's own choice
+// (the static kernels always stage TEMP in LDS; a per-plan build compiled with
+// FPF_WAVE_TEMP_VMEM does not)
+static size_t wave_lds_bytes_as(const WaveDev &w, bool temp_in_lds) {
     const size_t L = 64 / (size_t)w.spw, xc = (size_t)w.ncomp + 1, spb = (size_t)w.wpb * w.spw;
     const size_t pairs = ((2 * (size_t)w.bdepth * w.nblk + 3) & ~(size_t)3) * 4 + 4 * (size_t)w.C * L;
     const size_t regions = 16 * spb * ((3 * xc + (w.off_in_x ? 0 : 3 * (size_t)w.nblk) + 4 + REGION_EXTRA + 3 * (size_t)w.nlag) | 1);
     const size_t stage = 16 * 3 * ((size_t)swz_row(w.nl) + 1) * (spb + 1);   // STG: Sld in place, then V
     const size_t agg = 8 * 8 * (size_t)w.wpb * 64;                     // the last workgroup's fold
-    const size_t temp = TEMP_IN_LDS && !rtc_temp_vmem() ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
+    const size_t temp = temp_in_lds ? 16 * ((w.temp_sym ? 4 : 9) * (size_t)w.C * L) : 0;
     return temp + pairs + std::max(stage + regions, agg);
 }
+
+// the plan's figure (the large launches' build: the per-plan one when the
+// experiment switch moves TEMP out of LDS)
+size_t wave_lds_bytes(const WaveDev &w) { return wave_lds_bytes_as(w, TEMP_IN_LDS && !rtc_temp_vmem()); }
 
 int wave_scenarios_per_block(const WaveDev &w) { return w.wps ? 1 : w.wpb * w.spw; }   // wps: fpf_wblk.hip
 
@@ -163,7 +170,8 @@ WaveKernel pick(bool full, int gen, int wpb) {
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
     const int per_block = wave_scenarios_per_block(w);
     const unsigned grid = (unsigned)((n_scen + per_block - 1) / per_block);
-    const size_t lds = wave_lds_bytes(w);
+    // (the static kernels' size; the per-plan build's below)
+    const size_t lds = wave_lds_bytes_as(w, TEMP_IN_LDS);
     // FULL keeps IL and Ib of the last sweep for Vpolar/PQb/PQL, and for the
     // loss of a feeder with zeroed phases (reference formula over PQL)
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask || w.has_lag;   // (the sequential-order plan: FULL only)
@@ -220,8 +228,9 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
             int b = n_scen;
             const double *p = pq;
             void *args[] = {&wl, &b, &p, &oa};
-            hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)w.wpb * 64, 1, 1, (unsigned)lds, st, args,
-                                                 nullptr);
+            const size_t lds_rtc = wave_lds_bytes_as(w, TEMP_IN_LDS && !rtc_temp_vmem());
+            hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)w.wpb * 64, 1, 1, (unsigned)lds_rtc, st,
+                                                 args, nullptr);
             return e;
         }
     }

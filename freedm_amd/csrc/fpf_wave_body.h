@@ -326,7 +326,9 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // the tile's chunk c (scenarios 0 .. SPW-1), shifted to this wave's columns
             const int nchw = wnw * 3 * nl, SUW = f.stage_uw;
             const int2 *tab = (const int2 *)f.stage_smaj;
-            const d2v *src = (const d2v *)(pq + (size_t)(s0 + wsc0) * 6 * nl);
+            // (a wave with no live scenario -- the tail of a partial last tile --
+            // reads the tile's first chunk, which is inside the batch, not past it)
+            const d2v *src = (const d2v *)(pq + (size_t)(s0 + (wnw > 0 ? wsc0 : 0)) * 6 * nl);
 #pragma unroll
             for (int u = 0; u < US; ++u) {
                 if (u < SUW) {

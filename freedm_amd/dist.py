@@ -116,6 +116,10 @@ def timed_study(run_steps, study_aggregate, sync=None, group=None, clock=time.pe
         host.copy_(rows.reshape(-1), non_blocking=True)
         if sync is not None:
             sync()   # (waits for the rank's device work and the copy)
+        else:
+            # (no caller-supplied sync: wait for the copy itself before reading it)
+            import torch
+            torch.cuda.current_stream(rows.device).synchronize()
         rh = host.numpy()
     else:
         rh = rows.cpu().numpy()   # (waits for the rank's device work)

@@ -272,9 +272,15 @@ int         fpf_multi_shard(int rank, int n_gpus, long n_total, long *lo, long *
  * = {kind (0 issue, 1 collect), device, lo, hi}; at most max_ops entries are
  * written; returns the number of operations or FPF_ERR_ARG. */
 long        fpf_multi_schedule(int n_gpus, long n_scen, long chunk, long *ops, long max_ops);
-/* The combine the all-reduce performs, on the host (no device needed):
- * sums of fields 0 and 3..7, min of vmin, max of vmax; n = 0 gives the identity. */
+/* The combine of the per-device aggregates, on the host (no device needed):
+ * fpf_multi_solve all-gathers every device's aggregate (its one collective) and
+ * folds the rows with this, in device order -- sums of fields 0 and 3..7
+ * accumulated row after row, min of vmin, max of vmax; n = 0 gives the
+ * identity.  The one-process-per-GPU form (freedm_amd/dist.py) folds the same
+ * rows the same way, so both give the same bits. */
 void        fpf_aggregate_fold(const fpf_aggregate *parts, int n, fpf_aggregate *out);
+/* Diagnostics: collectives fpf_multi_solve has issued in this process (one per solve). */
+long        fpf_multi_collectives(void);
 
 /* ---- Multi-area solve (BASELINE config 5, the Broker_s1..s3 areas;
  * Broker_s1/src/vvc/VoltVarCtrl.cpp:327-395).  node_area[k] (k = 1..nn-1;
@@ -333,6 +339,26 @@ int         fpf_wave_rtc_builds(void);
 long        fpf_rtc_compile(const char *src, const char *name_expr, int ilp, int *regs,
                             char *buf, size_t buf_size);
 const char *fpf_rtc_compiler(void);
+/* Diagnostics (no device needed): the residency check the library applies to a
+ * hipRTC build before loading it -- registers per lane x waves per SIMD <= 512,
+ * static LDS (group segment) <= 160 KiB, and with max_priv >= 0 a private
+ * segment of at most max_priv bytes per lane (the hot light-output wave builds:
+ * 256, room for the call frame of the guard's exact re-solve but not for a
+ * spilled sweep state; -1: no limit).  code/size: a gfx950 code object (as
+ * fpf_rtc_compile writes it), kernel: its lowered kernel name, nt: threads per
+ * workgroup.  regs / group / priv (may be NULL): the descriptor's registers per
+ * lane, group segment and private segment bytes.  Returns 1 resident, 0 not,
+ * FPF_ERR_ARG (no such kernel descriptor).
+ *
+ * The hipRTC the library compiles with is the ROCm image's own, loaded with
+ * dlmopen into a private link-map namespace with its own libc; that libc's
+ * environ is pointed at the process's environment array before every compile
+ * (fpf_rtc.cpp: RtcApi::sync_env).  A compile therefore must not run while
+ * another thread calls setenv / putenv, and nothing in the compiler may
+ * modify the environment (it would reallocate the process's array with the
+ * other libc's allocator); the library serialises its own compiles. */
+int         fpf_rtc_resident(const char *code, size_t size, const char *kernel, int nt, int max_priv,
+                             int *regs, int *group, int *priv);
 
 /* Diagnostics (no device needed): the wave kernel's plan for this feeder.
  * out[0..7] = {accepted (1/0), scenarios per wavefront, slots per lane,
@@ -346,6 +372,23 @@ const char *fpf_rtc_compiler(void);
 int         fpf_feeder_wave_plan(const double *dl, int nl, int ncols,
                                  const double *z, int z_rows, int z_cols,
                                  const fpf_opts *opts, int out[8]);
+
+/* Diagnostics (no device needed): the lane kernel's plan for this feeder (one
+ * lane per scenario, the feeder's positions dealt to the waves of a workgroup;
+ * run by light-output scenario-fastest wave batches of >= n scenarios with
+ * FPF_LANE=n).  out[0..7] = {accepted (1/0), slots per wave, waves per workgroup,
+ * LDS bytes per workgroup, published backward entries, published forward
+ * entries, blocks, branches}; slots (may be NULL): the first slots_len ints of
+ * the per-slot table [waves][4][slots] = {Dl row, node (-1: dummy), backward
+ * info, forward info}; blk (may be NULL): the first blk_len ints of the block
+ * table [blocks][1 + 2 x 8] = {depth, (tap, first - 1) forward entries}.
+ * Returns FPF_OK or FPF_ERR_*. */
+int         fpf_feeder_lane_plan(const double *dl, int nl, int ncols,
+                                 const double *z, int z_rows, int z_cols,
+                                 const fpf_opts *opts, int out[8], int *slots, int slots_len,
+                                 int *blk, int blk_len);
+/* Diagnostics: launches of the lane kernel in this process. */
+int         fpf_lane_launches(void);
 
 /* Device-memory batch aggregate over per-scenario results (deterministic
  * reduction); same layout as fpf_aggregate.  Lets a caller aggregate several

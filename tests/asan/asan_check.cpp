@@ -74,6 +74,10 @@ int main(int argc, char **argv) {
         const int nl = h[0], nc = h[1], zr = h[2], zc = h[3];
         int plan[8];
         const int rp = fpf_feeder_wave_plan(dl.data(), nl, nc, z.data(), zr, zc, &o, plan);
+        int lplan[8];
+        std::vector<int> lslots(8 * 16 * 4), lblk(4096 * 17);
+        const int rl = fpf_feeder_lane_plan(dl.data(), nl, nc, z.data(), zr, zc, &o, lplan, lslots.data(), (int)lslots.size(),
+                                            lblk.data(), (int)lblk.size());
         const long need = fpf_feeder_rtc_source(dl.data(), nl, nc, z.data(), zr, zc, &o, nullptr, 0);
         std::vector<char> src(need > 0 ? (size_t)need : 1);
         const long got = need > 0 ? fpf_feeder_rtc_source(dl.data(), nl, nc, z.data(), zr, zc, &o, src.data(), src.size()) : need;
@@ -103,8 +107,8 @@ int main(int argc, char **argv) {
             rv = ref_vvc_main(dl.data(), nl, nc, z.data(), zr, zc, &ro, 0.1, 1.1, mm, ld, g.data(), nodes.data(), nloads,
                               lf.data(), lr.data(), dlo.data(), res.data());
         }
-        printf("%s: nl %d plan rc %d ok %d | rtc src %ld/%ld | ref solve %d batch %d vvc %d\n", argv[a], nl, rp,
-               rp == 0 ? plan[0] : -1, got, need, rs, rb, rv);
+        printf("%s: nl %d plan rc %d ok %d lane %d/%d | rtc src %ld/%ld | ref solve %d batch %d vvc %d\n", argv[a], nl, rp,
+               rp == 0 ? plan[0] : -1, rl, rl == 0 ? lplan[0] : -1, got, need, rs, rb, rv);
     }
     printf(failures ? "FAILURES %d\n" : "asan_check ok\n", failures);
     return failures ? 1 : 0;

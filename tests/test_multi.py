@@ -1,12 +1,15 @@
 """Multi-GPU study inside the C ABI (fpf_multi_*, freedm_amd/csrc/fpf_multi.cpp).
 
 CPU: the partition (fpf_multi_shard) equals freedm_amd.dist.shard_range, and
-the host fold of aggregates (fpf_aggregate_fold, the combine the RCCL
-all-reduce performs) equals dist.fold_aggregates -- identity included.
+the host fold of aggregates (fpf_aggregate_fold: the rows fpf_multi_solve's one
+RCCL all-gather brings together, folded in device order) equals
+dist.fold_aggregates bit for bit -- identity included -- so the in-process and
+the one-process-per-GPU forms give the same aggregate.
 GPU: fpf_multi with one device gives fpf_solve_batch's results bit for bit,
-and its aggregate is the fold of the per-scenario results; ragged batches
-smaller than the device count leave empty shards that still join the
-all-reduce (n_gpus above the box's one GPU is the driver's 8-GPU run).
+its aggregate is the fold of the per-scenario results, and each solve issues
+exactly one collective; ragged batches smaller than the device count leave
+empty shards that still join the all-gather (n_gpus above the box's one GPU is
+the driver's 8-GPU run).
 """
 import ctypes as C
 
@@ -44,8 +47,7 @@ def test_aggregate_fold_matches_dist():
     L.fpf_aggregate_fold(parts, 6, C.byref(out))
     ref = D.fold_aggregates(rows)
     got = np.array([getattr(out, k) for k in D.AGG_FIELDS])
-    np.testing.assert_array_equal(got[1:], ref[1:])
-    assert got[0] == pytest.approx(ref[0], rel=1e-15)
+    np.testing.assert_array_equal(got, ref)   # the same sequential sums: the same bits
     L.fpf_aggregate_fold(parts, 0, C.byref(out))
     assert (out.vmin, out.vmax, out.n_scen) == (np.inf, -np.inf, 0.0)
 
@@ -58,7 +60,11 @@ def test_multi_one_gpu_equals_single(name, B):
     pq = F.scenario_loads(f, np.arange(B))
     single = PowerFlow(f, device=0).solve(pq)
     m = MultiPowerFlow(f, n_gpus=1)
+    L = _lib.load()
+    L.fpf_multi_collectives.restype = C.c_long
+    c0 = L.fpf_multi_collectives()
     r = m.solve(pq)
+    assert L.fpf_multi_collectives() == c0 + 1   # one all-gather per solve
     for k in ("V_re", "V_im", "Vpolar", "PQb", "PQL", "iters", "status", "loss", "vmin", "vmax"):
         np.testing.assert_array_equal(r[k], single[k], err_msg=k)
     ag = r["aggregate"]
@@ -66,6 +72,8 @@ def test_multi_one_gpu_equals_single(name, B):
     assert ag["n_scen"] == B and ag["n_conv"] == ref[3] and ag["vmin"] == ref[1] and ag["vmax"] == ref[2]
     assert ag["loss_sum"] == pytest.approx(ref[0], rel=1e-12)
     assert ag == single["aggregate"]
+    fold = D.fold_aggregates(np.array([[single["aggregate"][k] for k in D.AGG_FIELDS]]))
+    np.testing.assert_array_equal(np.array([ag[k] for k in D.AGG_FIELDS]), fold)
     m.close()
 
 

@@ -203,3 +203,53 @@ def test_wave_rtc_defs_switches(monkeypatch):
     src = wave_rtc_source(f, 1, 0)
     assert "#define FPF_WAVE_GROUP 2\n" in src and "#define FPF_WAVE_TEMP_LATE 1\n" in src
     assert "BOGUS" not in src and "#define FPF_WAVE_X " not in src and "#define FPF_WAVE_Y" not in src
+
+
+def test_rtc_resident_checks_lds_and_scratch():
+    """The residency check a per-plan build passes before it is loaded
+    (fpf_rtc.cpp: rtc_resident): registers, the static LDS of the group segment
+    (<= 160 KiB) and, for the hot light-output wave builds, a private segment of
+    at most 256 bytes per lane -- the call frame of the guard's exact re-solve
+    fits, a spilled sweep state does not (the build is declined and the static
+    kernel runs).  The config-2 plan's light build passes; a kernel that spills a
+    private array passes only without the bound."""
+    from wave_rtc_dump import wave_rtc_source
+    from freedm_amd import _lib, synthetic_feeder
+    L = _lib.load()
+    L.fpf_rtc_resident.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.fpf_rtc_resident.restype = C.c_int
+
+    def build(src, name, ilp=0):
+        n = L.fpf_rtc_compile(src.encode(), name, ilp, None, None, 0)
+        assert n > 100
+        buf = C.create_string_buffer(n)
+        L.fpf_rtc_compile(src.encode(), name, ilp, None, buf, n)
+        return buf.raw
+
+    def check(co, kname, nt, max_priv):
+        regs, group, priv = C.c_int(-1), C.c_int(-1), C.c_int(-1)
+        low = next(s for s in _symbols(co) if kname in s)
+        rc = L.fpf_rtc_resident(co, len(co), low.encode(), nt, max_priv, C.byref(regs), C.byref(group), C.byref(priv))
+        return rc, regs.value, group.value, priv.value
+
+    src = wave_rtc_source(synthetic_feeder(123, 123), 1, 0)
+    name = src.rsplit("template __global__ void ", 1)[1].split("(")[0].encode()
+    co = build(src, name, 1)
+    rc, regs, group, priv = check(co, "dpf_wave_kernel", 256, 256)
+    assert rc == 1 and 0 <= priv <= 256 and 0 < group <= 160 * 1024 and regs <= 256, (rc, regs, group, priv)
+    spill = ("template <int N> __global__ void spill(double *o, const int *ix) {\n"
+             "  double a[N]; for (int i = 0; i < N; ++i) a[i] = o[i * 7 + threadIdx.x];\n"
+             "  __shared__ double s[64]; s[threadIdx.x & 63] = a[ix[threadIdx.x]];\n"
+             "  __syncthreads(); o[threadIdx.x] = s[(threadIdx.x + 1) & 63]; }\n"
+             "template __global__ void spill<512>(double *, const int *);\n")
+    co2 = build(spill, b"spill<512>")
+    rc2, _, group2, priv2 = check(co2, "spill", 64, 256)
+    assert priv2 > 256 and rc2 == 0 and group2 >= 512, (rc2, group2, priv2)
+    assert check(co2, "spill", 64, -1)[0] == 1
+
+
+def _symbols(co):
+    """The kernel symbols of a code object (their .kd descriptors, from the string table)."""
+    import re
+    return sorted({m.decode()[:-3] for m in re.findall(rb"_Z[A-Za-z0-9_]*\.kd", co)})
