@@ -635,7 +635,8 @@ def launch_ranks(n: int, argv: list) -> int:
 
 def _wave_rtc_builds():
     """per-plan hipRTC wave kernels built in this process (fpf_opts.specialize:
-    the wave launches of >= 2048 scenarios run them, fpf_rtc.cpp)"""
+    the wave launches of >= 4096 scenarios run them, FPF_WAVE_RTC overrides;
+    fpf_rtc.cpp: WAVE_RTC_DEFAULT_MIN)"""
     import ctypes
     from freedm_amd import _lib
     L = _lib.load()

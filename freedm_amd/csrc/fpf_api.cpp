@@ -2213,9 +2213,10 @@ static const WaveDev &wave_dev_for(const fpf_feeder *f, int n_scen, bool full = 
 // plan exists, the batch is large enough (FPF_LANE), scenario fastest, light
 // outputs, the feeder's own source and flat start
 static bool lane_for(const fpf_feeder *f, int n_scen, const OutDev &o) {
-    // (the kernel's 32-bit buffer offsets: the whole batch below 4 GiB)
+    // (the kernel's 32-bit buffer offsets: the whole batch below 4 GiB; V's two
+    // planes both or neither)
     return f->lane_ok && n_scen >= lane_min_scen() && (size_t)6 * f->ldev.nl * n_scen * 8 < ((size_t)1 << 32) &&
-           !o.smaj && !o.vpolar && !o.pqb && !o.pql && !o.vsrc &&
+           !o.v_re == !o.v_im && !o.smaj && !o.vpolar && !o.pqb && !o.pql && !o.vsrc &&
            !o.s_in && !o.skip && !o.vinit_re && !o.hook && !o.eps_dev && !o.check;
 }
 

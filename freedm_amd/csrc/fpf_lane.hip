@@ -27,9 +27,11 @@
 //     published G.
 // The loads (P, Q) are read from the caller's scenario-fastest batch every sweep
 // (64 consecutive doubles per load instruction; the re-reads hit the Infinity
-// Cache); V leaves from registers in the sweep a scenario finishes.  Converged
-// lanes sweep along (their V is already written) until the workgroup's last
-// scenario is done, as in the wave kernel.
+// Cache).  A lane whose scenario has finished is frozen -- every update of a
+// sweep runs under a divergent !done branch -- so its registers keep the V of its
+// last sweep until the workgroup's last scenario is done; then every lane's V
+// leaves in whole 512-byte rows (stored in the sweep each scenario finished, the
+// rows went out in part-lines twice: +0.2 ms on config 4, profiles/r06_lane).
 //
 // Scope (fpf_api.cpp: analyse_lane): well-formed tree-order feeders of at most
 // LANE_NW * LANE_NS = 128 branches, no zeroed phases, every branch's TEMP with one
@@ -66,11 +68,21 @@ namespace fpf {
 #define FPF_LANE_ABL 0
 #endif
 // slots of loads in flight ahead of the load currents (registers: 12 per slot)
+#ifndef FPF_LANE_LD3
+#define FPF_LANE_LD3 0
+#endif
+#ifndef FPF_LANE_FREEZE
+#define FPF_LANE_FREEZE 1
+#endif
 #ifndef FPF_LANE_PF
 #define FPF_LANE_PF 1
 #endif
 
 namespace {
+
+// (the frozen-lane branches; FPF_LANE_FREEZE=0: every lane sweeps until the
+// workgroup is done and writes its V in the sweep it finishes)
+#define FZ(d) (FPF_LANE_FREEZE ? (d) : false)
 
 typedef const __attribute__((address_space(4))) double cdbl;      // constant address space:
 typedef const __attribute__((address_space(4))) int32_t cint;     // scalar loads
@@ -91,6 +103,14 @@ __device__ __forceinline__ cx ldc(const double2 *a, int i) {
     const double2 v = a[i];
     return mk(v.x, v.y);
 }
+// a wave's three phase entries (stride 64): the three reads issued together, one
+// wait (else the compiler reuses one register quad and waits after each)
+__device__ __forceinline__ void ld3(cx (&t)[3], const double2 *a, int i) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) t[p] = ldc(a, i + p * 64);
+    if (FPF_LANE_LD3)
+        __asm__ volatile("" : "+v"(t[0].re), "+v"(t[0].im), "+v"(t[1].re), "+v"(t[1].im), "+v"(t[2].re), "+v"(t[2].im));
+}
 __device__ __forceinline__ void stc(double2 *a, int i, cx v) { a[i] = make_double2(v.re, v.im); }
 
 // buffer resources on wave-uniform bases (scalar registers) with the lane's
@@ -101,9 +121,14 @@ __device__ __forceinline__ void stc(double2 *a, int i, cx v) { a[i] = make_doubl
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const double *base) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ void st_lane(double v, double *base, unsigned vo) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v),
-                                          rsrc_at(base), vo, 0, 0);
+__device__ __forceinline__ __attribute__((ext_vector_type(2))) unsigned bits2(double v) {
+    return __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v);
+}
+// a wave-uniform pointer parked in LDS (read where it is used, into scalar registers)
+__device__ __forceinline__ double *lds_ptr(const uint64_t *a, int k) {
+    const uint64_t v = a[k];
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (double *)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ void load_pq(double (&d)[6], __amdgpu_buffer_rsrc_t rp, int row, unsigned plane,
                                         unsigned bb, unsigned vo) {
@@ -144,7 +169,13 @@ struct LaneSweep {
             for (int j = 0; j + 1 < FPF_LANE_PF; ++j)
 #pragma unroll
                 for (int k = 0; k < 6; ++k) sn[j][k] = sn[j + 1][k];
-            if (i + FPF_LANE_PF < NS) load_pq(sn[FPF_LANE_PF - 1], rp, row[i + FPF_LANE_PF], plane, bb, so);
+            if (i + FPF_LANE_PF < NS) {
+                // (the row opaque here: else all NS x 6 load offsets are computed up
+                // front, in scalar registers that spill)
+                int r = row[i + FPF_LANE_PF];
+                __asm__ volatile("" : "+s"(r));
+                load_pq(sn[FPF_LANE_PF - 1], rp, r, plane, bb, so);
+            }
             const double isc = (ei[i] & 1) ? inv_s3 : 0.0;   // (uniform) 0 on a dummy slot
             if (flat) {
 #pragma unroll
@@ -170,39 +201,57 @@ struct LaneSweep {
     // ---- backward sweep (:134-160) Ib = E[last] - E[q - 1] on the globalised E
     // (x = carry + local prefix), slots in descending order so that E[q - 1] is
     // still in place; the branch drops lng (Ib . Zl) (:163-178) over it; then their
-    // local prefix G in ascending order.  FIN (a scenario finishes in this sweep):
-    // also its part of the loss, sum Re(drop conj(Ib)) (s3 times it is PQb(0).re -
-    // sum_k PQL(k).re on a feeder without zeroed phases, fpf_wave_body.h)
-    __device__ __forceinline__ static void drops(cx (&x)[NS][3], double &lp, bool any_fin, const double2 *cw,
+    // local prefix G in ascending order; also the lane's part of the loss, sum
+    // Re(drop conj(Ib)) (s3 times it is PQb(0).re - sum_k PQL(k).re on a feeder
+    // without zeroed phases, fpf_wave_body.h), kept in the sweep a scenario finishes
+    __device__ __forceinline__ static void drops(cx (&x)[NS][3], double &lp, const double2 *cw,
                                                  const double2 *EG, cint *tab, cdbl *tmp, int lane) {
         int ei[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) ei[i] = tab[2 * NS + i];
+        // the next slot's gathers (LDS) and TEMP (scalar loads) are issued at the top
+        // of a slot and first used in the next one: one wait (lgkmcnt(0): scalar
+        // loads return out of order, so any wait on them waits for every LDS read as
+        // well) per slot, after the slot's arithmetic instead of before it
         cx el[3], en[3];
+        double tc[LANE_TW], tn[LANE_TW];
         {
             const int li = (ei[NS - 1] >> 16) & 0xffff;
 #pragma unroll
             for (int p = 0; p < 3; ++p) en[p] = ldc(EG, (li * 3 + p) * 64 + lane);
+#pragma unroll
+            for (int k = 0; k < LANE_TW; ++k) tn[k] = tmp[(NS - 1) * LANE_TW + k];
         }
 #pragma unroll
         for (int i = NS - 1; i >= 0; --i) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) el[p] = en[p];
-            if (i > 0) {   // the next slot's gather, in flight during this slot's arithmetic
+#pragma unroll
+            for (int k = 0; k < LANE_TW; ++k) tc[k] = tn[k];
+            // (consumed here: the wait for them comes before the next slot's loads)
+            __asm__ volatile("" : "+s"(tc[0]), "+s"(tc[1]), "+s"(tc[2]), "+s"(tc[3]), "+s"(tc[4]), "+s"(tc[5]),
+                             "+s"(tc[6]), "+s"(tc[7]));
+            pin(el);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i > 0) {
                 const int li = (ei[i - 1] >> 16) & 0xffff;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) en[p] = (FPF_LANE_ABL & 2) ? x[i - 1][p] : ldc(EG, (li * 3 + p) * 64 + lane);
+                cdbl *tq = tmp + (i - 1) * LANE_TW;
+                __asm__ volatile("" : "+s"(tq));   // (issued here, not hoisted to the phase start)
+#pragma unroll
+                for (int k = 0; k < LANE_TW; ++k) tn[k] = tq[k];
             }
+            __builtin_amdgcn_sched_barrier(0);   // (the loads first)
             cx ib[3];
 #pragma unroll
             for (int p = 0; p < 3; ++p) ib[p] = csub(el[p], i > 0 ? x[i - 1][p] : ldc(cw, p * 64 + lane));   // (E[-1] = the carry)
-            cdbl *const t = tmp + i * LANE_TW;
-            const cx zm = mk(t[6], t[7]);
+            const cx zm = mk(tc[6], tc[7]);
             const cx sm = cadd(cadd(ib[0], ib[1]), ib[2]);
             const cx ms = mk(fma(zm.re, sm.re, -(zm.im * sm.im)), fma(zm.re, sm.im, zm.im * sm.re));
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const cx d = mk(t[2 * p], t[2 * p + 1]);
+                const cx d = mk(tc[2 * p], tc[2 * p + 1]);
                 const cx b = ib[p];
                 const cx g = mk(fma(d.re, b.re, fma(-d.im, b.im, ms.re)), fma(d.re, b.im, fma(d.im, b.re, ms.im)));
                 x[i][p] = g;
@@ -222,8 +271,7 @@ struct LaneSweep {
     }
 
     // ---- forward sweep (:163-195): V = (V0 - off(block) - carry) - G, the block
-    // offset resolved where a block starts (and at the wave's first slot); FIN: the
-    // finishing scenarios' V out (rows [3][Nn][B]) and their extremes
+    // offset resolved where a block starts (and at the wave's first slot)
     __device__ __forceinline__ static void voltages(cx (&x)[NS][3], const double2 *vw, const double2 *EG, cint *tab,
                                                     cint *blk, int lane) {
         int gv[NS];
@@ -254,10 +302,13 @@ struct LaneSweep {
         }
     }
 
-    // ---- a scenario's last sweep: its V out (node rows of [3][Nn][B]) and the
-    // extremes of the wave's slots (V_abc_list.cpp:7-81 with every row kept)
+    // ---- after the loop: V out (node rows of [3][Nn][B]) and the
+    // extremes of the wave's slots (V_abc_list.cpp:7-81 with every row kept).  The
+    // output bases come from LDS (optr) as buffer resources, each row's offset
+    // (p Nn + node) 8B a scalar: the kernel's arguments are not kept in scalar
+    // registers across the loop (they were spilled and reloaded per store)
     __device__ __forceinline__ static void finish(const cx (&x)[NS][3], double &mn, double &mx, bool fin, cint *tab,
-                                                  const OutDev &o, int nn, unsigned B, unsigned so) {
+                                                  const uint64_t *optr, unsigned nn, unsigned bb, unsigned so) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
 #pragma unroll
@@ -266,15 +317,24 @@ struct LaneSweep {
                 mn = fmin(mn, m2);
                 mx = fmax(mx, m2);
             }
-            const int node = tab[NS + i];
-            if (fin && node >= 0) {
+        }
+        double *const vre = lds_ptr(optr, 0), *const vim = lds_ptr(optr, 1);
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)vre, 0, (int)0xffffffffu, 0x00020000);
+        const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)vim, 0, (int)0xffffffffu, 0x00020000);
+        if (!fin || !vre) return;   // (the host passes both planes or neither)
+        const unsigned ps = nn * bb;   // bytes per phase plane
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    const size_t r = ((size_t)p * nn + node) * B;
-                    if (o.v_re) st_lane(x[i][p].re, o.v_re + r, so);
-                    if (o.v_im) st_lane(x[i][p].im, o.v_im + r, so);
+        for (int i = 0; i < NS; ++i) {
+            const int node = tab[NS + i];
+            if (node >= 0) {
+                unsigned ro = (unsigned)node * bb;
+#pragma unroll
+                for (int p = 0; p < 3; ++p, ro += ps) {
+                    __builtin_amdgcn_raw_buffer_store_b64(bits2(x[i][p].re), rr, so, ro, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(bits2(x[i][p].im), ri, so, ro, 0);
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 };
@@ -292,6 +352,7 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
     __shared__ int fix_n, fix_ids[64];
     __shared__ double res[64][4];
     __shared__ int last_wg;
+    __shared__ uint64_t optr[5];   // v_re, v_im, iters, status, errmx (read where used)
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int s = (int)blockIdx.x * 64 + lane;
@@ -311,6 +372,14 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
     for (int p = 0; p < 3; ++p) v0[p] = mk(f.V0[2 * p], f.V0[2 * p + 1]);
 
     if (threadIdx.x == 0) fix_n = 0;
+    if (threadIdx.x == 0) {
+        optr[0] = (uint64_t)o.v_re;
+        optr[1] = (uint64_t)o.v_im;
+        optr[2] = (uint64_t)o.iters;
+        optr[3] = (uint64_t)o.status;
+        optr[4] = (uint64_t)o.errmx;
+    }
+    const bool guard_on = o.flag_count != nullptr;
     if ((int)threadIdx.x < 3 * 64) {
         IBO[threadIdx.x] = make_double2(0.0, 0.0);
         EG[max(f.nE, f.nG) * 3 * 64 + threadIdx.x] = make_double2(0.0, 0.0);   // the permanent zero entry
@@ -338,25 +407,36 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         cdbl *tmp = tmp0;
         cint *blk = (cint *)f.blk;
         __asm__ volatile("" : "+s"(tab), "+s"(tmp), "+s"(blk));
-        double sabs = 0.0;
-        SW::currents(x, sabs, it == 0, sn, rp, tab, plane, bb, so, inv_s3);
-        if (it == 0) RES[(w * 4 + 3) * 64 + lane] = sabs;
+        // a finished lane's state is frozen (every update below is under !done, a
+        // divergent branch: its registers keep the V of its last sweep until the
+        // loop ends, when every lane's V leaves in whole lines)
+        if (!FZ(done)) {
+            double sabs = 0.0;
+            SW::currents(x, sabs, it == 0, sn, rp, tab, plane, bb, so, inv_s3);
+            if (it == 0) RES[(w * 4 + 3) * 64 + lane] = sabs;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
+            for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
+        }
         lane_barrier();   // B1: the wave totals of E
 
         // ---- the carry of this wave and Ib(0) = the total, summed in wave order (the
         // same association in every wave, so every wave takes the same decisions)
         cx carry[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
 #pragma nounroll
-        for (int u = 0; u < w; ++u)
+        for (int u = 0; u < w; ++u) {
+            cx t[3];
+            ld3(t, WT, u * 3 * 64 + lane);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) carry[p] = cadd(carry[p], ldc(WT, (u * 3 + p) * 64 + lane));
+            for (int p = 0; p < 3; ++p) carry[p] = cadd(carry[p], t[p]);
+        }
         cx tot[3] = {carry[0], carry[1], carry[2]};
 #pragma nounroll
-        for (int u = w; u < NW; ++u)
+        for (int u = w; u < NW; ++u) {
+            cx t[3];
+            ld3(t, WT, u * 3 * 64 + lane);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) tot[p] = cadd(tot[p], ldc(WT, (u * 3 + p) * 64 + lane));
+            for (int p = 0; p < 3; ++p) tot[p] = cadd(tot[p], t[p]);
+        }
         // ---- convergence on the substation branch (:199-217)
         double err2 = 0.0;
 #pragma unroll
@@ -367,26 +447,27 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         }
         const bool conv = (FPF_LANE_ABL & 4) ? false : err2 < eps2;
         const bool fin = !done && (conv || it == ((FPF_LANE_ABL & 4) ? 4 : f.mxitr - 1));
-        if (w == 0 && o.flag_count) {
+        if (w == 0 && guard_on) {
             // the guard record (fpf_wave_body.h): decisions within 2^-9 of eps^2
             const double dd = fabs(err2 - eps2);
             if (!done && dd <= 0x1p-9 * eps2) gmin = fmin(gmin, dd);
         }
-        const bool any_fin = __ballot(fin) != 0;
         // E made global (x = carry + the local prefix) and published at the subtree
         // ends (the leaves; every slot gathers one)
-        int ev[NS];
+        if (!FZ(done)) {
+            int ev[NS];
 #pragma unroll
-        for (int i = 0; i < NS; ++i) ev[i] = tab[2 * NS + i];
+            for (int i = 0; i < NS; ++i) ev[i] = tab[2 * NS + i];
 #pragma unroll
-        for (int i = 0; i < NS; ++i) {
+            for (int i = 0; i < NS; ++i) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) x[i][p] = cadd(carry[p], x[i][p]);
-            pin(x[i]);
-            const int pe = ((ev[i] >> 1) & 0x7fff) - 1;
-            if (pe >= 0) {
+                for (int p = 0; p < 3; ++p) x[i][p] = cadd(carry[p], x[i][p]);
+                pin(x[i]);
+                const int pe = ((ev[i] >> 1) & 0x7fff) - 1;
+                if (pe >= 0) {
 #pragma unroll
-                for (int p = 0; p < 3; ++p) stc(EG, (pe * 3 + p) * 64 + lane, x[i][p]);
+                    for (int p = 0; p < 3; ++p) stc(EG, (pe * 3 + p) * 64 + lane, x[i][p]);
+                }
             }
         }
         lane_barrier();   // B2: published E (every wave has read IBO and the wave totals)
@@ -400,12 +481,14 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
 #pragma unroll
         for (int p = 0; p < 3; ++p) stc(cw, p * 64 + lane, carry[p]);
 
-        double lp = 0.0;
-        SW::drops(x, lp, any_fin, cw, EG, tab, tmp, lane);
-        // WT is free again (every wave read it before B2)
+        if (!FZ(done)) {
+            double lp = 0.0;
+            SW::drops(x, lp, cw, EG, tab, tmp, lane);
+            // WT is free again (every wave read it before B2)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
-        if (fin) RES[(w * 4 + 0) * 64 + lane] = lp;
+            for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
+            if (fin) RES[(w * 4 + 0) * 64 + lane] = lp;
+        }
 #pragma unroll
         for (int j = 0; j < FPF_LANE_PF; ++j)   // the next sweep's first loads, in flight across the barriers
             load_pq(sn[j], rp, tab[j], plane, bb, so);
@@ -413,9 +496,12 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
 
         cx carryg[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
 #pragma nounroll
-        for (int u = 0; u < w; ++u)
+        for (int u = 0; u < w; ++u) {
+            cx t[3];
+            ld3(t, WT, u * 3 * 64 + lane);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) carryg[p] = cadd(carryg[p], ldc(WT, (u * 3 + p) * 64 + lane));
+            for (int p = 0; p < 3; ++p) carryg[p] = cadd(carryg[p], t[p]);
+        }
         // publish G at the taps and before the lateral blocks
         int gv[NS];
 #pragma unroll
@@ -434,21 +520,39 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         // G totals before B4)
 #pragma unroll
         for (int p = 0; p < 3; ++p) stc(cw, p * 64 + lane, csub(v0[p], carryg[p]));
-        SW::voltages(x, cw, EG, tab, blk, lane);
-        double mn = INFINITY, mx = -INFINITY;
-        if (any_fin) SW::finish(x, mn, mx, fin, tab, o, nn, (unsigned)B, so);
+        if (!FZ(done)) SW::voltages(x, cw, EG, tab, blk, lane);
+        if (!FPF_LANE_FREEZE && __ballot(fin) != 0) {
+            // (not frozen: V out in the sweep a lane finishes, rows in part-lines)
+            double mn = INFINITY, mx = -INFINITY;
+            SW::finish(x, mn, mx, fin, tab, optr, (unsigned)nn, bb, so);
+            if (fin) {
+                RES[(w * 4 + 1) * 64 + lane] = mn;
+                RES[(w * 4 + 2) * 64 + lane] = mx;
+            }
+        }
         if (fin) {
-            RES[(w * 4 + 1) * 64 + lane] = mn;
-            RES[(w * 4 + 2) * 64 + lane] = mx;
             if (w == 0) {
                 stat = conv ? FPF_CONVERGED : FPF_NONCONVERGED;
-                if (o.iters) o.iters[s] = it + 1;
-                if (o.status) o.status[s] = (int8_t)stat;
-                if (o.errmx) o.errmx[s] = sqrt(err2);
+                int32_t *const pit = (int32_t *)lds_ptr(optr, 2);
+                int8_t *const pst = (int8_t *)lds_ptr(optr, 3);
+                double *const per = lds_ptr(optr, 4);
+                if (pit) pit[s] = it + 1;
+                if (pst) pst[s] = (int8_t)stat;
+                if (per) per[s] = sqrt(err2);
             }
         }
         done = done || fin;
         if (__ballot(!done) == 0) break;   // (the same in every wave)
+    }
+    if (FPF_LANE_FREEZE) {
+        // every lane's V (frozen at its last sweep) out in whole lines, and the
+        // extremes of the wave's slots
+        double mn = INFINITY, mx = -INFINITY;
+        cint *tab = tab0;
+        __asm__ volatile("" : "+s"(tab));
+        SW::finish(x, mn, mx, live, tab, optr, (unsigned)nn, bb, so);
+        RES[(w * 4 + 1) * 64 + lane] = mn;
+        RES[(w * 4 + 2) * 64 + lane] = mx;
     }
     lane_barrier();   // RES complete
 

@@ -172,6 +172,14 @@ def test_lane_declines_and_wave_runs(monkeypatch):
     pq = F.scenario_loads(f, np.arange(70))
     n0 = _launches()
     PowerFlow(f).solve(pq)   # full outputs (Vpolar, PQb, PQL)
+    r = _solve_light(PowerFlow(f), pq)
+    assert _launches() == n0 + 1   # (light outputs with both V planes: the lane kernel)
+    n0 = _launches()
+    import torch
+    one = {"v_re": torch.zeros((3, PowerFlow(f).nn, 70), dtype=torch.float64, device="cuda:0")}
+    PowerFlow(f).solve_device(torch.from_numpy(pq).to("cuda:0"), one)   # one V plane: the wave kernel
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(one["v_re"].cpu().numpy(), r["v_re"], rtol=1e-12, atol=1e-14)
     PowerFlow(f, layout=1).solve(np.ascontiguousarray(pq.transpose(2, 0, 1)), full=False)
     assert _launches() == n0
 
@@ -189,6 +197,7 @@ def test_lane_two_streams(monkeypatch):
     dev = torch.device("cuda:0")
     d = [torch.from_numpy(x).to(dev) for x in xs]
     outs = [{"v_re": torch.zeros((3, pf.nn, 640), dtype=torch.float64, device=dev),
+             "v_im": torch.zeros((3, pf.nn, 640), dtype=torch.float64, device=dev),
              "iters": torch.zeros(640, dtype=torch.int32, device=dev),
              "status": torch.zeros(640, dtype=torch.int8, device=dev),
              "loss": torch.zeros(640, dtype=torch.float64, device=dev),
@@ -196,11 +205,14 @@ def test_lane_two_streams(monkeypatch):
              "vmax": torch.zeros(640, dtype=torch.float64, device=dev)} for _ in range(2)]
     s = [torch.cuda.Stream(), torch.cuda.Stream()]
     torch.cuda.synchronize()
+    n0 = _launches()
     for _ in range(3):
         for k in range(2):
             pf.solve_device(d[k], outs[k], stream=s[k])
     torch.cuda.synchronize()
+    assert _launches() == n0 + 6
     for k in range(2):
         np.testing.assert_array_equal(outs[k]["v_re"].cpu().numpy(), ref[k]["v_re"])
+        np.testing.assert_array_equal(outs[k]["v_im"].cpu().numpy(), ref[k]["v_im"])
         np.testing.assert_array_equal(outs[k]["iters"].cpu().numpy(), ref[k]["iters"])
         np.testing.assert_array_equal(outs[k]["loss"].cpu().numpy(), ref[k]["loss"])
