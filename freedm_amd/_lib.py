@@ -27,7 +27,7 @@ EXPORTS = ["fpf_abi_version", "fpf_opts_default", "fpf_ctx_create", "fpf_ctx_des
            "fpf_multi_shard", "fpf_multi_schedule", "fpf_aggregate_fold", "fpf_areas_create", "fpf_areas_destroy", "fpf_areas_last_error",
            "fpf_areas_info", "fpf_areas_solve", "fpf_vvc_gradient", "fpf_vvc_gradient_at", "fpf_vvc_round",
            "fpf_vvc_gradient_batch", "fpf_feeder_check", "fpf_vvc_round_batch", "fpf_feeder_wave_rtc_source",
-           "fpf_wave_rtc_builds", "fpf_rtc_compile", "fpf_rtc_compiler", "fpf_feeder_lane_plan", "fpf_lane_launches",
+           "fpf_wave_rtc_builds", "fpf_rtc_compile", "fpf_rtc_compiler", "fpf_feeder_lane_plan", "fpf_lane_launches", "fpf_lane_dma_launches",
            "fpf_rtc_resident", "fpf_multi_collectives"]
 
 
@@ -135,6 +135,7 @@ def load(path: str | None = None):
                                            C.c_int]
         L.fpf_feeder_lane_plan.restype = C.c_int
         L.fpf_lane_launches.restype = C.c_int
+        L.fpf_lane_dma_launches.restype = C.c_int
     L.fpf_selftest_division.argtypes = [C.c_int, C.c_long, C.c_ulong]
     L.fpf_selftest_division.restype = C.c_long
     if hasattr(L, "fpf_multi_create") or path == LIB_PATH:   # (older diagnostic builds lack them)

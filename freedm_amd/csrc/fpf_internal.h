@@ -408,7 +408,9 @@ hipError_t launch_aggregate(int n_scen, const int8_t *status, const double *loss
                             double *d_agg, double *partials, unsigned *ticket, hipStream_t st);
 hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
 hipError_t launch_lane(const LaneDev &l, int n_scen, const double *pq, const OutDev &o, hipStream_t st);
-size_t lane_lds_bytes(const LaneDev &l);
+// the lane kernel's dynamic LDS: with the loads' DMA rings (dma) or without (the
+// plan's check and the guard's local re-solve use the smaller, dma = false)
+size_t lane_lds_bytes(const LaneDev &l, bool dma = false);
 int lane_min_scen();   // launches from this size run the lane kernel (FPF_LANE: 0 never, 1 always, n)
 // the staging tables of a wave-kernel geometry (WaveDev::stage_smaj / stage_l0,
 // [u][NT] int2 each); returns the chunks per thread, 0 if above the kernel's limit

@@ -50,6 +50,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <set>
 
@@ -71,8 +72,11 @@ namespace fpf {
 #ifndef FPF_LANE_LD3
 #define FPF_LANE_LD3 0
 #endif
-#ifndef FPF_LANE_FREEZE
-#define FPF_LANE_FREEZE 1
+#ifndef FPF_LANE_IL3
+#define FPF_LANE_IL3 1
+#endif
+#ifndef FPF_LANE_SB
+#define FPF_LANE_SB 1   // (bit 1: a scheduling barrier between the load currents' slots)
 #endif
 #ifndef FPF_LANE_PF
 #define FPF_LANE_PF 1
@@ -80,9 +84,26 @@ namespace fpf {
 
 namespace {
 
-// (the frozen-lane branches; FPF_LANE_FREEZE=0: every lane sweeps until the
-// workgroup is done and writes its V in the sweep it finishes)
-#define FZ(d) (FPF_LANE_FREEZE ? (d) : false)
+#ifdef FPF_LANE_STAMPS
+// diagnostic build only (tools/lane_stamps.py): lane 0 of each wave of the eight
+// workgroups from fpf_lane_stamp_base on records s_memtime, [64][128]: 0 entry,
+// 1 loop start, 4 + 10 it + k in sweep it < 12 (k: 0 top, 1 currents, 2 B1, 3
+// carry + E published, 4 B2, 5 drops, 6 B3, 7 G published, 8 B4, 9 voltages),
+// 120 after the loop, 121 V out, 122 end
+__device__ unsigned long long *fpf_lane_stamp_buf = nullptr;
+__device__ unsigned fpf_lane_stamp_base = 0;
+#define LSTAMP(idx)                                                                                    \
+    do {                                                                                               \
+        const unsigned g_ = (blockIdx.x - fpf_lane_stamp_base) * LANE_NW + (threadIdx.x >> 6);        \
+        if (fpf_lane_stamp_buf && (threadIdx.x & 63) == 0 && blockIdx.x >= fpf_lane_stamp_base &&     \
+            g_ < 64u && (idx) < 128)                                                                   \
+            fpf_lane_stamp_buf[g_ * 128 + (idx)] = __builtin_amdgcn_s_memtime();                       \
+    } while (0)
+#define LSTAMP_IT(k) LSTAMP(it < 12 ? 4 + 10 * it + (k) : 999)
+#else
+#define LSTAMP(idx) ((void)0)
+#define LSTAMP_IT(k) ((void)0)
+#endif
 
 typedef const __attribute__((address_space(4))) double cdbl;      // constant address space:
 typedef const __attribute__((address_space(4))) int32_t cint;     // scalar loads
@@ -118,9 +139,6 @@ __device__ __forceinline__ void stc(double2 *a, int i, cx v) { a[i] = make_doubl
 // The loads [6][Nl][B]: one resource on the batch, element (f, row) of this
 // lane's scenario at byte ((f Nl + row) B + s) 8 = a scalar offset (f Nl + row)
 // 8B plus the lane's 8s (the host keeps the batch below 4 GiB, fpf_api.cpp)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const double *base) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 0x7fffffff, 0x00020000);
-}
 __device__ __forceinline__ __attribute__((ext_vector_type(2))) unsigned bits2(double v) {
     return __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v);
 }
@@ -140,6 +158,54 @@ __device__ __forceinline__ void load_pq(double (&d)[6], __amdgpu_buffer_rsrc_t r
     }
 }
 
+// ---- the loads through LDS-DMA (the DMA variant: no VGPR holds a load in flight,
+// so they run three slots ahead).  A wave's ring has two entries of [6][64]
+// doubles (one slot's P1 Q1 P2 Q2 P3 Q3 of its 64 scenarios); a slot is three
+// 16-byte pieces per lane -- lanes 0-31 field 2k, lanes 32-63 field 2k + 1, lane
+// l scenarios s0 + 2 (l % 32) and + 1 -- each piece one wave instruction writing
+// 1 KiB of LDS at M0 + 16 lane.  hipcc does not count these loads: the waits for
+// them are explicit (vm_wait) and the ring entry is overwritten only after the
+// wave's own reads of it are done (lgkmcnt(0) in the same statement).
+typedef unsigned __attribute__((ext_vector_type(4))) u4;
+// (issued with every lane on: a lane's piece carries its neighbours' scenarios,
+// and the load currents run under the divergent !done branch)
+__device__ __forceinline__ void dma_piece(u4 rsrc, unsigned vo, unsigned so, unsigned lds_addr) {
+    unsigned keep;
+    unsigned long long ex;
+    __asm__ volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, -1\n\t"
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, %5 offen lds\n\t"
+        "s_mov_b32 m0, %0\n\t"
+        "s_mov_b64 exec, %1"
+        : "=&s"(keep), "=&s"(ex)
+        : "v"(vo), "s"(rsrc), "s"(lds_addr), "s"(so)
+        : "memory");
+}
+// one slot's three pieces: row offset row B 8, field pair k at + 2 k plane
+__device__ __forceinline__ void dma_slot(u4 rsrc, unsigned vo, int row, unsigned bb, unsigned plane2, unsigned lds_addr) {
+    if (FPF_LANE_ABL & 1) return;
+    int r = row;
+    __asm__ volatile("" : "+s"(r));   // (the offsets here, not hoisted)
+    const unsigned ro = (unsigned)r * bb;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dma_piece(rsrc, vo, ro + k * plane2, lds_addr + k * 1024);
+}
+// every vector memory operation but the newest three (one slot's pieces) done, or all
+__device__ __forceinline__ void vm_wait(bool leave3) {
+    if (leave3) __asm__ volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// a slot's six values of this lane's scenario from a ring entry
+__device__ __forceinline__ void ring_read(double (&d)[6], const double *e, int lane, int row, unsigned vo) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) d[f] = (FPF_LANE_ABL & 1) ? 1e-3 * (f + 1) + 1e-6 * row + 1e-9 * vo : e[f * 64 + lane];
+}
+
 }  // namespace
 
 // one sweep's phases on the wave's NS slots (every slot is live: a wave's run of
@@ -147,6 +213,30 @@ __device__ __forceinline__ void load_pq(double (&d)[6], __amdgpu_buffer_rsrc_t r
 // so their IL, Ib and drop are exactly 0 and no slot needs a branch)
 template <int NS>
 struct LaneSweep {
+    // a slot's load currents IL = conj(S/V) = conj(S) V / |V|^2 (one refined
+    // reciprocal per phase) added to the wave's local prefix.  FPF_LANE_IL3: the
+    // three phases' chains in lockstep, stage by stage (the scheduler otherwise
+    // runs them one after another at this register pressure: ~11 dependent fp64
+    // steps each)
+    __device__ __forceinline__ static void slot_currents(cx (&x)[NS][3], int i, const double (&sc)[6], double isc) {
+        double d2[3], r[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) d2[p] = fma(x[i][p].re, x[i][p].re, x[i][p].im * x[i][p].im);
+        if (FPF_LANE_IL3) __asm__ volatile("" : "+v"(d2[0]), "+v"(d2[1]), "+v"(d2[2]));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) r[p] = (FPF_LANE_ABL & 8) ? d2[p] : __builtin_amdgcn_rcp(d2[p]);
+        if (FPF_LANE_IL3) __asm__ volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) r[p] = fma(r[p], fma(-d2[p], r[p], 1.0), r[p]) * isc;
+        if (FPF_LANE_IL3) __asm__ volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const double P = sc[2 * p], Q = sc[2 * p + 1];
+            const cx v = x[i][p];
+            const cx il = mk(fma(P, v.re, Q * v.im) * r[p], fma(P, v.im, -(Q * v.re)) * r[p]);
+            x[i][p] = i == 0 ? il : cadd(x[i - 1][p], il);
+        }
+    }
     // ---- load currents (:106-130) and the wave's local prefix E of IL; the flat
     // start's first sweep is the same arithmetic on x = V0 (DPF_return7.cpp:92-96),
     // plus the guard's sum |S|_1 (a branch on one register only).  The loads run
@@ -182,19 +272,46 @@ struct LaneSweep {
                 for (int k = 0; k < 6; ++k) sabs = fma(fabs(sc[k]), isc, sabs);
             }
             __asm__ volatile("" : "+v"(sabs));
+            slot_currents(x, i, sc, isc);
+            pin(x[i]);
+            if (FPF_LANE_SB & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // ---- the same on the DMA ring: on entry slots 0 and 1 are in flight (entries 0
+    // and 1); slot j + 3 is issued in slot j into the entry slot j + 1 was read from
+    __device__ __forceinline__ static void currents_dma(cx (&x)[NS][3], double &sabs, bool flat, u4 rsrc, unsigned vo,
+                                                        cint *tab, unsigned bb, unsigned plane2, unsigned ring_lds,
+                                                        const double *ring, int lane, double inv_s3) {
+        int row[NS], ei[NS];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                const double P = sc[2 * p], Q = sc[2 * p + 1];
-                // IL = conj(S/V) = conj(S) V / |V|^2, one refined reciprocal
-                const cx v = x[i][p];
-                const double d2 = fma(v.re, v.re, v.im * v.im);
-                double r = __builtin_amdgcn_rcp(d2);
-                r = fma(r, fma(-d2, r, 1.0), r) * isc;
-                const cx il = mk(fma(P, v.re, Q * v.im) * r, fma(P, v.im, -(Q * v.re)) * r);
-                x[i][p] = i == 0 ? il : cadd(x[i - 1][p], il);
+        for (int i = 0; i < NS; ++i) row[i] = tab[i];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) ei[i] = tab[2 * NS + i];
+        double sn[6];
+        vm_wait(NS > 1);   // slot 0 landed (slot 1 may not have)
+        ring_read(sn, ring, lane, row[0], vo);
+        if (NS > 2) dma_slot(rsrc, vo, row[2], bb, plane2, ring_lds);   // (waits for the reads of entry 0)
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            double sc[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) sc[k] = sn[k];
+            if (i + 1 < NS) {
+                vm_wait(i + 2 < NS);   // slot i + 1 landed (slot i + 2 may not have)
+                ring_read(sn, ring + ((i + 1) & 1) * 384, lane, row[i + 1], vo);
             }
+            __builtin_amdgcn_sched_barrier(0);
+            const double isc = (ei[i] & 1) ? inv_s3 : 0.0;   // (uniform) 0 on a dummy slot
+            if (flat) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) sabs = fma(fabs(sc[k]), isc, sabs);
+            }
+            __asm__ volatile("" : "+v"(sabs));
+            slot_currents(x, i, sc, isc);
             pin(x[i]);
             __builtin_amdgcn_sched_barrier(0);
+            if (i + 3 < NS) dma_slot(rsrc, vo, row[i + 3], bb, plane2, ring_lds + ((i + 1) & 1) * 3072);
         }
     }
 
@@ -339,16 +456,19 @@ struct LaneSweep {
     }
 };
 
-template <int NS>
+template <int NS, bool DMA>
 __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, int B, const double *__restrict__ pq,
                                                                    OutDev o) {
     constexpr int NW = LANE_NW;
     typedef LaneSweep<NS> SW;
     extern __shared__ double2 lds[];
-    double2 *const WT = lds;                               // [NW][3][64] wave totals (E, then G)
+    // DMA: [NW][2][6][64] the waves' load rings (48 KiB, first: M0 addresses stay
+    // small), after the loop [NW][2][64] min / max |V|^2; else only the latter
+    double *const MM = (double *)lds;
+    double2 *const WT = (double2 *)(MM + (DMA ? NW * 2 * 384 : NW * 2 * 64));   // [NW][3][64] wave totals (E, then G)
     double2 *const IBO = WT + NW * 3 * 64;                 // [3][64] Ib(0) of the last sweep
-    double *const RES = (double *)(IBO + 3 * 64);          // [NW][4][64] per wave: loss part, min / max |V|^2, sum |S|_1
-    double2 *const EG = (double2 *)(RES + NW * 4 * 64);    // [max(nE, nG) + 1][3][64] published E, then G; last: 0
+    double *const LS = (double *)(IBO + 3 * 64);           // [NW][2][64] per wave: loss part, sum |S|_1
+    double2 *const EG = (double2 *)(LS + NW * 2 * 64);     // [max(nE, nG) + 1][3][64] published E, then G; last: 0
     __shared__ int fix_n, fix_ids[64];
     __shared__ double res[64][4];
     __shared__ int last_wg;
@@ -371,6 +491,7 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
 #pragma unroll
     for (int p = 0; p < 3; ++p) v0[p] = mk(f.V0[2 * p], f.V0[2 * p + 1]);
 
+    LSTAMP(0);
     if (threadIdx.x == 0) fix_n = 0;
     if (threadIdx.x == 0) {
         optr[0] = (uint64_t)o.v_re;
@@ -384,10 +505,7 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         IBO[threadIdx.x] = make_double2(0.0, 0.0);
         EG[max(f.nE, f.nG) * 3 * 64 + threadIdx.x] = make_double2(0.0, 0.0);   // the permanent zero entry
     }
-    for (int i = threadIdx.x; i < NW * 4 * 64; i += NW * 64) {
-        const int q = (i >> 6) & 3;
-        RES[i] = q == 1 ? INFINITY : (q == 2 ? -INFINITY : 0.0);
-    }
+    for (int i = threadIdx.x; i < NW * 2 * 64; i += NW * 64) LS[i] = 0.0;
 
     cx x[NS][3];   // the slots' state: V, then E, Ib -> G, then V again
 #pragma unroll
@@ -397,10 +515,24 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
     bool done = !live;
     double gmin = INFINITY;   // (wave 0) closest |errmx^2 - eps^2| of a decision in the coarse band
     int stat = 1;             // (wave 0) the scenario's status
-    double sn[FPF_LANE_PF][6];   // the next slots' P, Q
+    double sn[FPF_LANE_PF][6];   // (no DMA) the next slots' P, Q
+    // (DMA) the batch resource with its exact size (pieces past the batch read 0),
+    // this lane's piece offset, this wave's ring
+    const u4 rq = {(unsigned)(uintptr_t)pq, (unsigned)((uintptr_t)pq >> 32), 6u * plane, 0x00020000u};
+    const unsigned vdma = (lane >= 32 ? plane : 0u) + 8u * (unsigned)(blockIdx.x * 64 + 2 * (lane & 31));
+    const unsigned ring_lds =
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) double *)MM + (unsigned)w * 2u * 3072u;
+    const double *const ring = MM + w * 2 * 384;
+    if (DMA) {
+        dma_slot(rq, vdma, tab0[0], bb, 2 * plane, ring_lds);
+        dma_slot(rq, vdma, tab0[1], bb, 2 * plane, ring_lds + 3072);
+    } else {
 #pragma unroll
-    for (int j = 0; j < FPF_LANE_PF; ++j) load_pq(sn[j], rp, tab0[j], plane, bb, so);
+        for (int j = 0; j < FPF_LANE_PF; ++j) load_pq(sn[j], rp, tab0[j], plane, bb, so);
+    }
+    LSTAMP(1);
     for (int it = 0;; ++it) {
+        LSTAMP_IT(0);
         // the slot tables' base opaque per sweep: their scalar loads stay inside the
         // loop instead of hundreds of scalar registers hoisted (and spilled) across it
         cint *tab = tab0;
@@ -410,14 +542,17 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         // a finished lane's state is frozen (every update below is under !done, a
         // divergent branch: its registers keep the V of its last sweep until the
         // loop ends, when every lane's V leaves in whole lines)
-        if (!FZ(done)) {
+        if (!done) {
             double sabs = 0.0;
-            SW::currents(x, sabs, it == 0, sn, rp, tab, plane, bb, so, inv_s3);
-            if (it == 0) RES[(w * 4 + 3) * 64 + lane] = sabs;
+            if (DMA) SW::currents_dma(x, sabs, it == 0, rq, vdma, tab, bb, 2 * plane, ring_lds, ring, lane, inv_s3);
+            else SW::currents(x, sabs, it == 0, sn, rp, tab, plane, bb, so, inv_s3);
+            if (it == 0) LS[(w * 2 + 1) * 64 + lane] = sabs;
 #pragma unroll
             for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
         }
+        LSTAMP_IT(1);
         lane_barrier();   // B1: the wave totals of E
+        LSTAMP_IT(2);
 
         // ---- the carry of this wave and Ib(0) = the total, summed in wave order (the
         // same association in every wave, so every wave takes the same decisions)
@@ -454,7 +589,7 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         }
         // E made global (x = carry + the local prefix) and published at the subtree
         // ends (the leaves; every slot gathers one)
-        if (!FZ(done)) {
+        if (!done) {
             int ev[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) ev[i] = tab[2 * NS + i];
@@ -470,7 +605,9 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
                 }
             }
         }
+        LSTAMP_IT(3);
         lane_barrier();   // B2: published E (every wave has read IBO and the wave totals)
+        LSTAMP_IT(4);
         if (w == 0) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) stc(IBO, p * 64 + lane, tot[p]);
@@ -481,18 +618,26 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
 #pragma unroll
         for (int p = 0; p < 3; ++p) stc(cw, p * 64 + lane, carry[p]);
 
-        if (!FZ(done)) {
+        if (!done) {
             double lp = 0.0;
             SW::drops(x, lp, cw, EG, tab, tmp, lane);
             // WT is free again (every wave read it before B2)
 #pragma unroll
             for (int p = 0; p < 3; ++p) stc(WT, (w * 3 + p) * 64 + lane, x[NS - 1][p]);
-            if (fin) RES[(w * 4 + 0) * 64 + lane] = lp;
+            if (fin) LS[(w * 2 + 0) * 64 + lane] = lp;
         }
+        // the next sweep's first loads, in flight across the barriers (DMA: slots 0
+        // and 1 into the ring, free since the last slots' reads)
+        if (DMA) {
+            dma_slot(rq, vdma, tab[0], bb, 2 * plane, ring_lds);
+            dma_slot(rq, vdma, tab[1], bb, 2 * plane, ring_lds + 3072);
+        } else {
 #pragma unroll
-        for (int j = 0; j < FPF_LANE_PF; ++j)   // the next sweep's first loads, in flight across the barriers
-            load_pq(sn[j], rp, tab[j], plane, bb, so);
+            for (int j = 0; j < FPF_LANE_PF; ++j) load_pq(sn[j], rp, tab[j], plane, bb, so);
+        }
+        LSTAMP_IT(5);
         lane_barrier();   // B3: the wave totals of G (every wave has read its gathered E)
+        LSTAMP_IT(6);
 
         cx carryg[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
 #pragma nounroll
@@ -514,22 +659,16 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
                 for (int p = 0; p < 3; ++p) stc(EG, (pg * 3 + p) * 64 + lane, cadd(carryg[p], x[i][p]));
             }
         }
+        LSTAMP_IT(7);
         lane_barrier();   // B4: published G
+        LSTAMP_IT(8);
 
         // V0 - the carry of G, parked in the wave's WT entry (every wave has read the
         // G totals before B4)
 #pragma unroll
         for (int p = 0; p < 3; ++p) stc(cw, p * 64 + lane, csub(v0[p], carryg[p]));
-        if (!FZ(done)) SW::voltages(x, cw, EG, tab, blk, lane);
-        if (!FPF_LANE_FREEZE && __ballot(fin) != 0) {
-            // (not frozen: V out in the sweep a lane finishes, rows in part-lines)
-            double mn = INFINITY, mx = -INFINITY;
-            SW::finish(x, mn, mx, fin, tab, optr, (unsigned)nn, bb, so);
-            if (fin) {
-                RES[(w * 4 + 1) * 64 + lane] = mn;
-                RES[(w * 4 + 2) * 64 + lane] = mx;
-            }
-        }
+        if (!done) SW::voltages(x, cw, EG, tab, blk, lane);
+        LSTAMP_IT(9);
         if (fin) {
             if (w == 0) {
                 stat = conv ? FPF_CONVERGED : FPF_NONCONVERGED;
@@ -544,17 +683,20 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
         done = done || fin;
         if (__ballot(!done) == 0) break;   // (the same in every wave)
     }
-    if (FPF_LANE_FREEZE) {
+    LSTAMP(120);
+    if (DMA) vm_wait(false);   // (the ring's last pieces, issued for a sweep that did not come)
+    {
         // every lane's V (frozen at its last sweep) out in whole lines, and the
         // extremes of the wave's slots
         double mn = INFINITY, mx = -INFINITY;
         cint *tab = tab0;
         __asm__ volatile("" : "+s"(tab));
         SW::finish(x, mn, mx, live, tab, optr, (unsigned)nn, bb, so);
-        RES[(w * 4 + 1) * 64 + lane] = mn;
-        RES[(w * 4 + 2) * 64 + lane] = mx;
+        MM[(w * 2 + 0) * 64 + lane] = mn;
+        MM[(w * 2 + 1) * 64 + lane] = mx;
     }
-    lane_barrier();   // RES complete
+    LSTAMP(121);
+    lane_barrier();   // MM, LS complete
 
     // ---- per scenario (wave 0): loss (VoltVarCtrl.cpp:1152-1161), Vmin / Vmax
     // (V_abc_list.cpp:7-81 with every row kept, VoltVarCtrl.cpp:1201-1207), the
@@ -569,10 +711,10 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
             mx = fmax(mx, m2);
         }
         for (int u = 0; u < NW; ++u) {
-            ls += RES[(u * 4 + 0) * 64 + lane];
-            mn = fmin(mn, RES[(u * 4 + 1) * 64 + lane]);
-            mx = fmax(mx, RES[(u * 4 + 2) * 64 + lane]);
-            sa += RES[(u * 4 + 3) * 64 + lane];
+            ls += LS[(u * 2 + 0) * 64 + lane];
+            mn = fmin(mn, MM[(u * 2 + 0) * 64 + lane]);
+            mx = fmax(mx, MM[(u * 2 + 1) * 64 + lane]);
+            sa += LS[(u * 2 + 1) * 64 + lane];
         }
         const double loss = f.s3 * ls, vmin = sqrt(mn), vmax = sqrt(mx);
         if (live) {
@@ -662,6 +804,7 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
                 *o.flag_out = __hip_atomic_load(o.flag_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    LSTAMP(122);
     if (o.fix_dev) {
         // the guard's local mode (a solve without an aggregate): the scenarios this
         // workgroup flagged are re-solved on the exact body by its first wave, after
@@ -677,9 +820,19 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
     }
 }
 
-size_t lane_lds_bytes(const LaneDev &l) {
+#ifdef FPF_LANE_STAMPS
+extern "C" int fpf_debug_set_lane_stamp_buffer(void *dptr, unsigned base) {
+    unsigned long long *p = (unsigned long long *)dptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fpf_lane_stamp_base), &base, sizeof(base)) != hipSuccess) return -3;
+    return hipMemcpyToSymbol(HIP_SYMBOL(fpf_lane_stamp_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#endif
+
+size_t lane_lds_bytes(const LaneDev &l, bool dma) {
     const size_t col = 3 * 64 * 16;   // one published entry: 3 phases x 64 lanes x complex
-    return (size_t)LANE_NW * col + 3 * 64 * 16 + (size_t)LANE_NW * 4 * 64 * 8 + (size_t)(std::max(l.nE, l.nG) + 1) * col;
+    const size_t first = dma ? (size_t)LANE_NW * 2 * 384 * 8 : (size_t)LANE_NW * 2 * 64 * 8;   // rings / extremes
+    return first + (size_t)LANE_NW * col + 3 * 64 * 16 + (size_t)LANE_NW * 2 * 64 * 8 +
+           (size_t)(std::max(l.nE, l.nG) + 1) * col;
 }
 
 int lane_min_scen() {
@@ -689,39 +842,68 @@ int lane_min_scen() {
     return v <= 0 ? (1 << 30) : v;
 }
 
-static std::atomic<int> g_lane_launches{0};
+static std::atomic<int> g_lane_launches{0}, g_lane_dma_launches{0};
 extern "C" int fpf_lane_launches(void) { return g_lane_launches.load(); }
+extern "C" int fpf_lane_dma_launches(void) { return g_lane_dma_launches.load(); }
+
+// FPF_LANE_DMA=0 keeps the loads in registers (diagnostics; read per call)
+static bool lane_dma_allowed() {
+    const char *e = getenv("FPF_LANE_DMA");
+    return !(e && *e && atoi(e) == 0);
+}
 
 hipError_t launch_lane(const LaneDev &l, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {
-    void (*k)(LaneDev, int, const double *, OutDev) = nullptr;
+    typedef void (*KFn)(LaneDev, int, const double *, OutDev);
+    KFn kr = nullptr, kd = nullptr;
     switch (l.ns) {
-        case 4: k = dpf_lane_kernel<4>; break;
-        case 8: k = dpf_lane_kernel<8>; break;
-        case 12: k = dpf_lane_kernel<12>; break;
-        case 16: k = dpf_lane_kernel<16>; break;
+        case 4: kr = dpf_lane_kernel<4, false>; kd = dpf_lane_kernel<4, true>; break;
+        case 8: kr = dpf_lane_kernel<8, false>; kd = dpf_lane_kernel<8, true>; break;
+        case 12: kr = dpf_lane_kernel<12, false>; kd = dpf_lane_kernel<12, true>; break;
+        case 16: kr = dpf_lane_kernel<16, false>; kd = dpf_lane_kernel<16, true>; break;
         default: return hipErrorInvalidValue;
     }
-    const size_t lds = lane_lds_bytes(l);
     static std::mutex mu;
-    static std::set<std::array<int, 2>> attr_done;
+    static std::map<std::array<int, 3>, int> static_lds;   // (device, ns, dma) -> the kernel's static LDS
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
-    {
+    auto prepare = [&](KFn k, int dma, int *stat) -> hipError_t {
         std::lock_guard<std::mutex> lk(mu);
-        if (!attr_done.count({dev, l.ns})) {
+        auto it = static_lds.find({dev, l.ns, dma});
+        if (it == static_lds.end()) {
             hipFuncAttributes fa{};
             hipError_t e = hipFuncGetAttributes(&fa, (const void *)k);
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024 - (int)fa.sharedSizeBytes);
             if (e != hipSuccess) return e;
-            attr_done.insert({dev, l.ns});
+            it = static_lds.emplace(std::array<int, 3>{dev, l.ns, dma}, (int)fa.sharedSizeBytes).first;
         }
+        *stat = it->second;
+        return hipSuccess;
+    };
+    // the DMA ring when it fits beside the kernel's static LDS and the batch has an
+    // even number of scenarios (a lane's 16-byte piece is two scenarios: an odd
+    // batch's last piece would reach past the end of the buffer)
+    KFn k = kr;
+    size_t lds = lane_lds_bytes(l, false);
+    int stat = 0;
+    if (lane_dma_allowed() && n_scen % 2 == 0) {
+        if (prepare(kd, 1, &stat) == hipSuccess && lane_lds_bytes(l, true) + (size_t)stat <= (size_t)160 * 1024) {
+            k = kd;
+            lds = lane_lds_bytes(l, true);
+        }
+    }
+    if (k == kr) {
+        const hipError_t e = prepare(kr, 0, &stat);
+        if (e != hipSuccess) return e;
     }
     const unsigned grid = (unsigned)((n_scen + 63) / 64);
     hipLaunchKernelGGL(k, dim3(grid), dim3(LANE_NW * 64), lds, st, l, n_scen, pq, o);
     const hipError_t e = hipGetLastError();
-    if (e == hipSuccess) g_lane_launches.fetch_add(1);
+    if (e == hipSuccess) {
+        g_lane_launches.fetch_add(1);
+        if (k == kd) g_lane_dma_launches.fetch_add(1);
+    }
     return e;
 }
 

@@ -387,8 +387,11 @@ int         fpf_feeder_lane_plan(const double *dl, int nl, int ncols,
                                  const double *z, int z_rows, int z_cols,
                                  const fpf_opts *opts, int out[8], int *slots, int slots_len,
                                  int *blk, int blk_len);
-/* Diagnostics: launches of the lane kernel in this process. */
+/* Diagnostics: launches of the lane kernel in this process; of those, the
+ * launches that read the loads through the LDS-DMA ring (even batches whose
+ * ring fits in LDS; FPF_LANE_DMA=0 turns it off). */
 int         fpf_lane_launches(void);
+int         fpf_lane_dma_launches(void);
 
 /* Device-memory batch aggregate over per-scenario results (deterministic
  * reduction); same layout as fpf_aggregate.  Lets a caller aggregate several

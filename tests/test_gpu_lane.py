@@ -22,6 +22,11 @@ def _launches():
     return int(L.fpf_lane_launches())
 
 
+def _dma_launches():
+    from freedm_amd import _lib
+    return int(_lib.load().fpf_lane_dma_launches())
+
+
 def _vrel(a, b):
     return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))
 
@@ -77,9 +82,11 @@ def test_lane_matches_oracle(name, B, monkeypatch):
     f = _feeder(name)
     pq = F.scenario_loads(f, np.arange(500, 500 + B))
     pf = PowerFlow(f)
-    n0 = _launches()
+    n0, d0 = _launches(), _dma_launches()
     r = _solve_light(pf, pq)
     assert _launches() == n0 + 1, "the lane kernel did not run"
+    # (even batches read the loads through the LDS-DMA ring, odd ones from registers)
+    assert _dma_launches() == d0 + (1 if B % 2 == 0 else 0)
     _check_oracle(f, pq, r)
     assert not r["guard"].any()
 
@@ -109,6 +116,25 @@ def test_lane_matches_wave_kernel(monkeypatch):
     assert lr["agg"][1] == pytest.approx(w["agg"][1], rel=1e-13)
     assert lr["agg"][2] == pytest.approx(w["agg"][2], rel=1e-13)
     assert lr["agg"][7] == pq.shape[2]
+
+
+def test_lane_dma_ring_equals_register_loads(monkeypatch):
+    """The same even batch with the loads through the LDS-DMA ring and through
+    registers (FPF_LANE_DMA=0): the same arithmetic on the same values, so every
+    output is bit-identical; ragged last workgroup (B % 64 != 0)."""
+    from freedm_amd import PowerFlow
+    monkeypatch.setenv("FPF_LANE", "1")
+    f = F.synthetic_feeder(123, 123)
+    pq = F.hosting_loads(f, np.arange(3000), seed=77)
+    pf = PowerFlow(f)
+    d0 = _dma_launches()
+    a = _solve_light(pf, pq, agg=True)
+    assert _dma_launches() == d0 + 1
+    monkeypatch.setenv("FPF_LANE_DMA", "0")
+    b = _solve_light(pf, pq, agg=True)
+    assert _dma_launches() == d0 + 1
+    for k in ("v_re", "v_im", "iters", "status", "loss", "vmin", "vmax", "errmx", "agg"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 def test_lane_nonconverged_and_mxitr(monkeypatch):
