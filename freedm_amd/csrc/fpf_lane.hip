@@ -73,7 +73,7 @@ namespace fpf {
 #define FPF_LANE_LD3 0
 #endif
 #ifndef FPF_LANE_IL3
-#define FPF_LANE_IL3 1
+#define FPF_LANE_IL3 0   // (measured: no faster, and the register-load variant spills; profiles/r06_lane)
 #endif
 #ifndef FPF_LANE_SB
 #define FPF_LANE_SB 1   // (bit 1: a scheduling barrier between the load currents' slots)
@@ -846,10 +846,13 @@ static std::atomic<int> g_lane_launches{0}, g_lane_dma_launches{0};
 extern "C" int fpf_lane_launches(void) { return g_lane_launches.load(); }
 extern "C" int fpf_lane_dma_launches(void) { return g_lane_dma_launches.load(); }
 
-// FPF_LANE_DMA=0 keeps the loads in registers (diagnostics; read per call)
+// FPF_LANE_DMA=1: the loads through the LDS-DMA ring (read per call).  Off by
+// default: config 4 0.920 ms with it against 0.913 ms without (profiles/r06_lane:
+// the ring hides the loads' latency, but the load-current phase takes as long --
+// its time is not the loads' latency)
 static bool lane_dma_allowed() {
     const char *e = getenv("FPF_LANE_DMA");
-    return !(e && *e && atoi(e) == 0);
+    return e && *e && atoi(e) != 0;
 }
 
 hipError_t launch_lane(const LaneDev &l, int n_scen, const double *pq, const OutDev &o, hipStream_t st) {

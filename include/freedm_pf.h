@@ -388,8 +388,8 @@ int         fpf_feeder_lane_plan(const double *dl, int nl, int ncols,
                                  const fpf_opts *opts, int out[8], int *slots, int slots_len,
                                  int *blk, int blk_len);
 /* Diagnostics: launches of the lane kernel in this process; of those, the
- * launches that read the loads through the LDS-DMA ring (even batches whose
- * ring fits in LDS; FPF_LANE_DMA=0 turns it off). */
+ * launches that read the loads through the LDS-DMA ring (FPF_LANE_DMA=1, even
+ * batches whose ring fits in LDS). */
 int         fpf_lane_launches(void);
 int         fpf_lane_dma_launches(void);
 

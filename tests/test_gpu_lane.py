@@ -85,8 +85,7 @@ def test_lane_matches_oracle(name, B, monkeypatch):
     n0, d0 = _launches(), _dma_launches()
     r = _solve_light(pf, pq)
     assert _launches() == n0 + 1, "the lane kernel did not run"
-    # (even batches read the loads through the LDS-DMA ring, odd ones from registers)
-    assert _dma_launches() == d0 + (1 if B % 2 == 0 else 0)
+    assert _dma_launches() == d0   # (the LDS-DMA ring only on request, FPF_LANE_DMA=1)
     _check_oracle(f, pq, r)
     assert not r["guard"].any()
 
@@ -119,16 +118,20 @@ def test_lane_matches_wave_kernel(monkeypatch):
 
 
 def test_lane_dma_ring_equals_register_loads(monkeypatch):
-    """The same even batch with the loads through the LDS-DMA ring and through
-    registers (FPF_LANE_DMA=0): the same arithmetic on the same values, so every
-    output is bit-identical; ragged last workgroup (B % 64 != 0)."""
+    """The same even batch with the loads through the LDS-DMA ring (FPF_LANE_DMA=1)
+    and through registers: the same arithmetic on the same values, so every output
+    is bit-identical; ragged last workgroup (B % 64 != 0); an odd batch keeps the
+    register loads (a lane's 16-byte piece is two scenarios)."""
     from freedm_amd import PowerFlow
     monkeypatch.setenv("FPF_LANE", "1")
+    monkeypatch.setenv("FPF_LANE_DMA", "1")
     f = F.synthetic_feeder(123, 123)
     pq = F.hosting_loads(f, np.arange(3000), seed=77)
     pf = PowerFlow(f)
     d0 = _dma_launches()
     a = _solve_light(pf, pq, agg=True)
+    assert _dma_launches() == d0 + 1
+    _solve_light(pf, np.ascontiguousarray(pq[:, :, :2999]))
     assert _dma_launches() == d0 + 1
     monkeypatch.setenv("FPF_LANE_DMA", "0")
     b = _solve_light(pf, pq, agg=True)
