@@ -237,6 +237,7 @@ struct LaneDev {
     const double *temp;
     int32_t ns;              // slots per wave (4, 8, 12 or 16: the kernel instantiation)
     const int32_t *blk;      // [nblk][1 + 2 LANE_BD]: depth, then (tap, first - 1) forward indices
+    int32_t stagger;         // cycles the first-round workgroups of every other CU wait (launch_lane)
 };
 
 // Device views of the caller's output buffers ([col][row][B], scenario fastest).

@@ -492,6 +492,14 @@ __global__ __launch_bounds__(LANE_NW * 64, 2) void dpf_lane_kernel(LaneDev f, in
     for (int p = 0; p < 3; ++p) v0[p] = mk(f.V0[2 * p], f.V0[2 * p + 1]);
 
     LSTAMP(0);
+    if (f.stagger > 0 && blockIdx.x < 256u && ((blockIdx.x >> 3) & 1u)) {
+        // every other CU of each XCD (blocks go round robin over the 8 XCDs) starts
+        // its first workgroup late, its later ones follow on: the CUs' load-current
+        // phases -- each workgroup's 377 KB of loads re-read in a burst -- then
+        // fall at different times instead of all at once (FPF_LANE_STAGGER)
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)f.stagger) __builtin_amdgcn_s_sleep(8);
+    }
     if (threadIdx.x == 0) fix_n = 0;
     if (threadIdx.x == 0) {
         optr[0] = (uint64_t)o.v_re;
@@ -901,7 +909,12 @@ hipError_t launch_lane(const LaneDev &l, int n_scen, const double *pq, const Out
         if (e != hipSuccess) return e;
     }
     const unsigned grid = (unsigned)((n_scen + 63) / 64);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(LANE_NW * 64), lds, st, l, n_scen, pq, o);
+    LaneDev la = l;
+    {
+        const char *e = getenv("FPF_LANE_STAGGER");   // (read per call)
+        la.stagger = e && *e ? std::max(0, atoi(e)) : 0;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(LANE_NW * 64), lds, st, la, n_scen, pq, o);
     const hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
         g_lane_launches.fetch_add(1);
