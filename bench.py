@@ -459,17 +459,36 @@ def _shuffled_units(f, seed):
     return Feeder(np.vstack([Dl[:cut[1]]] + [units[i] for i in order]), f.Z, name=f"{f.name}-shuffled{seed}")
 
 
+def _zeroed_units(f):
+    """Phase c zeroed (a two-phase line code, no phase-c load) on every second
+    lateral unit that no other unit taps (tests/lag_tables.py: zeroed)."""
+    from freedm_amd import Feeder
+    Dl = np.array(f.Dl, copy=True)
+    Z = np.vstack([f.Z, np.diag([f.Z[0, 0], f.Z[1, 1], 0])])
+    code = Z.shape[0] // 3
+    sep = [i for i in range(Dl.shape[0]) if Dl[i, 0] == 0] + [Dl.shape[0]]
+    taps = {int(Dl[i + 1, 1]) for i in sep[:-1] if i + 1 < Dl.shape[0]}
+    leaves = [u for u in range(len(sep) - 1) if not any(int(Dl[r, 2]) in taps for r in range(sep[u] + 1, sep[u + 1]))]
+    for u in leaves[::2]:
+        Dl[sep[u] + 1:sep[u + 1], 3] = code
+        Dl[sep[u] + 1:sep[u + 1], 10:12] = 0.0
+    return Feeder(Dl, Z, name=f"{f.name}-zeroed")
+
+
 def _diag_sequential_order(torch, local, stream, dev):
     """Diagnostic leg: feeders whose lateral units are listed in a shuffled order
-    (the sequential-order plan, DESIGN 5.0e: the fast kernels' FULL variant) at
-    4096 scenarios (scenario major), beside the exact generic kernel -- until
+    (the sequential-order plan, DESIGN 5.0e: the fast kernels' FULL variant; one
+    with zeroed phases too) at 4096 scenarios (scenario major), beside the exact
+    generic kernel -- until
     round 5 the only kernel for such tables -- and the tree-ordered feeder's own
     fast solve of the same loads: launch times, identical iteration counts and
     status, max V relative difference."""
     from freedm_amd import PowerFlow, scenario_loads, synthetic_feeder
     out = {}
-    for name, n, seed in (("123bus_shuffled", 123, 1), ("2048bus_shuffled", 2048, 13)):
+    for name, n, seed in (("123bus_shuffled", 123, 1), ("123bus_shuffled_zeroed", 123, 1), ("2048bus_shuffled", 2048, 13)):
         f0 = synthetic_feeder(n, n)
+        if name.endswith("_zeroed"):
+            f0 = _zeroed_units(f0)
         f = _shuffled_units(f0, seed)
         B = 4096
         pq = scenario_loads(f, np.arange(B), seed=B + 11)
@@ -485,10 +504,13 @@ def _diag_sequential_order(torch, local, stream, dev):
         conv = oe["status"] == 0
         a = torch.complex(of["v_re"], of["v_im"])
         b = torch.complex(oe["v_re"], oe["v_im"])
-        r = torch.where(conv.view(-1, 1, 1), (a - b).abs() / b.abs(), torch.zeros_like(b.real))
+        # (zeroed phases: V exactly 0 in both)
+        r = torch.where(conv.view(-1, 1, 1) & (b.abs() > 0), (a - b).abs() / b.abs().clamp_min(1e-300),
+                        torch.zeros_like(b.real))
         vrel = float(r.max().item())
         del a, b, r, d
-        out[name] = {"workload": f"{nn}-bus synthetic feeder, lateral units shuffled (seed {seed}), {B} scenarios",
+        zz = ", phase c zeroed on every second leaf unit" if name.endswith("_zeroed") else ""
+        out[name] = {"workload": f"{nn}-bus synthetic feeder{zz}, lateral units shuffled (seed {seed}), {B} scenarios",
                      "kernel": _wave_kernel_name(nb) if kf == "wave" else kf, "variant": "full (sequential order)",
                      "kernel_ms": msf, "converged_scenarios_per_s": int(conv.sum().item()) / (msf / 1e3),
                      "mean_sweeps": float(of["iters"].double().mean().item()),

@@ -566,8 +566,10 @@ static void analyse_coop(const HostFeeder &h, WaveHost &w, int n, int C, int wps
 //     a segment's base is V at its F-parent (a block-offset chain of Ginc pairs, as
 //     the tree plan's blocks) or, at an F-root, V0 or V_prev of its source -- which
 //     the slot holding that source stores into LDS at the top of every sweep.
-// Zeroed phases are declined (the generic kernel runs those tables); the loss
-// then takes the reference's PQb / PQL form (the kernel's FULL variant).
+// Zeroed phases (on the wave kernel: up to 256 branches) as the tree plan's: V = 0
+// and IL = 0 on them; a live phase below a zeroed F-ancestor (restarting from 0
+// there) is declined; the loss takes the reference's PQb / PQL form (the kernel's
+// FULL variant).
 void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_why) {
     auto no = [&](const std::string &why) { w.ok = false; w.why = tree_why + "; sequential-order plan: " + why; };
     if (getenv("FPF_NO_WAVE_LAG")) return no("disabled (FPF_NO_WAVE_LAG)");
@@ -597,9 +599,13 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
         }
         for (int k = 1; k < nn; ++k)
             if (row_of[k] < 0) return no("node without a branch row");
-        for (int k = 1; k < nn; ++k)
-            if (h.fw[fw_of[k]].mask & 7) return no("zeroed phases");
     }
+    // zeroed phases (a line code without that phase, :180-192): V(k, p) = 0 on them
+    // and IL = 0 there; the wave-block kernel's sequential-order plan declines them
+    int has_mask = 0;
+    for (int k = 1; k < nn; ++k)
+        if (h.fw[fw_of[k]].mask & 7) has_mask = 1;
+    if (has_mask && wps) return no("zeroed phases past 256 branches (the generic kernel runs them)");
     // P-forest (backward) and F-forest (forward)
     std::vector<int> ppar(nn, -1), post(nn, -1), fpar(nn, -1), fsrc(nn, 0);   // fsrc: an F-root's source (0: V0)
     std::vector<int> chain(nn, -1);
@@ -685,6 +691,31 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
         if (fpar[hd] >= 0) needf(pos[fpar[hd]]);
         needf(bfirst[b] - 1);
     }
+    // a live phase below a zeroed node m on this sweep's forward path restarts from
+    // 0 there: V(k, p) = Vr(k) - Vr(m), Vr = the segment base - the path sum before
+    // the zeroing (the tree plan's rule on the F-forest: m the nearest zeroed
+    // F-ancestor; a source of the previous sweep brings its zeroed V along)
+    std::vector<std::array<int, 3>> mref(nn, {-1, -1, -1});
+    int has_rel = 0;
+    for (int k = 1; k < nn && has_mask; ++k)
+        for (int p = 0; p < 3; ++p) {
+            if ((h.fw[fw_of[k]].mask >> p) & 1) continue;
+            int guard = 0;
+            for (int a = fpar[k]; a >= 1 && guard <= nn; a = fpar[a], ++guard)
+                if ((h.fw[fw_of[a]].mask >> p) & 1) {
+                    mref[k][p] = a;
+                    has_rel = 1;
+                    break;
+                }
+        }
+    // (measured: V = Vr(k) - Vr(m), a difference of two ~1 p.u. values, missed the
+    // 1e-10 relative bar on the small V below the zeroed node -- 5.0e-10 on a
+    // shuffled 60-bus table, tests/test_gpu_lag.py -- so these tables keep the
+    // generic kernel, as the paired wave-block kernel's do)
+    if (has_rel) return no("a live phase below a zeroed one (the generic kernel runs it)");
+    for (int k = 1; k < nn; ++k)
+        for (int p = 0; p < 3; ++p)
+            if (mref[k][p] >= 1) needf(pos[mref[k][p]]);
     const bool off_in_x = false;
     const int ncomp = std::max(std::max(nb_c, nf_c), 1);
     if (ncomp > 510) return no("too many gathered positions");
@@ -727,8 +758,11 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
         const int k = at[q], c = q % C, lane = q / C, i = c * L + lane;
         w.row[i] = row_of[k];
         w.node[i] = k;
-        w.info[i] = (int32_t)((uint32_t)(8 | ((cb[q] + 1) << 4) | (cb[q + size[k] - 1] << 13) | ((cf[q] + 1) << 22)));
+        w.info[i] = (int32_t)((uint32_t)((h.fw[fw_of[k]].mask & 7) | 8 | ((cb[q] + 1) << 4) | (cb[q + size[k] - 1] << 13) |
+                                         ((cf[q] + 1) << 22)));
         w.blk[i] = blk[q];
+        for (int p = 0; p < 3; ++p)
+            if (mref[k][p] >= 1) w.mref[(p * C + c) * L + lane] = cf[pos[mref[k][p]]];
         int hi = ncomp, lo = ncomp;
         if (lo_t[k] >= 0) {
             hi = cb[hi_t[k]];
@@ -794,8 +828,8 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
     w.nblk = nblk;
     w.bdepth = bdepth;
     w.ncomp = ncomp;
-    w.has_rel = 0;
-    w.has_mask = 0;
+    w.has_rel = has_rel;
+    w.has_mask = has_mask;
     w.off_in_x = off_in_x ? 1 : 0;
     w.wps = wps;
     w.has_lag = 1;

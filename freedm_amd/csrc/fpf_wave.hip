@@ -152,6 +152,7 @@ WaveKernel pick_w(bool full, int gx) {
     // (the 1-scenario, 2-slot geometry -- FPF_WAVE_GEOM experiments only -- has no
     // zeroed-phase instantiation: the compiler's register allocator crashes on it)
     if constexpr (SPW == 1 && C == 2) return nullptr;
+    else if (gx == 3) return dpf_wave_kernel<SPW, C, true, WPB, 3>;   // sequential order with zeroed phases
     else return dpf_wave_kernel<SPW, C, true, WPB, 1>;
 }
 template <int SPW, int C>
@@ -176,8 +177,8 @@ hipError_t launch_wave(const WaveDev &w, int n_scen, const double *pq, const Out
     // loss of a feeder with zeroed phases (reference formula over PQL)
     const bool full = o.vpolar || o.pqb || o.pql || w.has_mask || w.has_lag;   // (the sequential-order plan: FULL only)
     // the general paths only where the plan has them (fpf_wave_body.h: GX): zeroed
-    // phases, or the sequential-order plan (which declines zeroed phases)
-    const int gen = w.has_lag ? 2 : (w.has_mask || w.has_rel ? 1 : 0);
+    // phases (bit 0), the sequential-order plan (bit 1)
+    const int gen = (w.has_lag ? 2 : 0) | (w.has_mask || w.has_rel ? 1 : 0);
     WaveKernel k = nullptr;
     int id = -1;
     if (w.spw == 4 && w.C == 1) { k = pick<4, 1>(full, gen, w.wpb); id = 0; }

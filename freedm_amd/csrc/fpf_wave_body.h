@@ -171,9 +171,9 @@ __device__ __attribute__((noinline)) void full_gen_reductions(const OutDev &o, i
 
 // FULL: the full-output variant (Vpolar / PQb / PQL); GX: the general paths
 // compiled into it -- bit 0 zeroed phases (has_mask / has_rel), bit 1 the
-// sequential-order plan (has_lag; never with zeroed phases).  One instantiation per
-// kind keeps each within the register file: all of them in one spilled ~150 VGPRs,
-// each alone 0-14 (tools/res_usage2.py)
+// sequential-order plan (has_lag); 3 both (a sequential-order table with zeroed
+// phases).  One instantiation per kind keeps each within the register file: all
+// of them in one spilled ~150 VGPRs, each alone 0-14 (tools/res_usage2.py)
 template <int SPW, int C, bool FULL, int WPB, int GX = FULL ? 1 : 0>
 __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, C>::template eff_minw<WPB>())) void dpf_wave_kernel(
     WaveDev f, int B, const double *__restrict__ pq, OutDev o) {

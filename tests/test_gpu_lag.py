@@ -6,12 +6,13 @@ the reference solves with its sequential semantics (DPF_return7.cpp:134-195).
 They used to run only on the exact generic kernel (~10x slower); fast mode now
 runs them on the wave kernel, checked against the oracle at the north-star bar:
 identical iteration counts and status, V within 1e-10 relative, PQb / PQL /
-Vpolar as tests/test_gpu_parity.py's fast-mode bar, loss 1e-8, Vmin/Vmax 1e-10."""
+Vpolar as tests/test_gpu_parity.py's fast-mode bar, loss 1e-8, Vmin/Vmax 1e-10;
+zeroed phases in such tables too (lag_tables.zeroed_cases)."""
 import numpy as np
 import pytest
 
 from freedm_amd import feeder as F
-from lag_tables import cases, wblk_cases
+from lag_tables import cases, restart_cases, wblk_cases, zeroed_cases
 from test_gpu_parity import _close, _fast_mode_outputs_match, _vrel
 
 pytestmark = pytest.mark.gpu
@@ -42,6 +43,54 @@ def test_sequential_order_tables_on_the_wave_kernel(name):
     assert e.kernel in ("generic", "tiled")
     re_ = e.solve(pq[:, :, :16])
     np.testing.assert_array_equal(re_["V_re"], c["V_re"][..., :16])
+
+
+@pytest.mark.parametrize("name", sorted(zeroed_cases()))
+def test_sequential_order_zeroed_phases_on_the_wave_kernel(name):
+    """Sequential-order tables with zeroed phases (V = 0 on them, IL = 0 there,
+    DPF_return7.cpp:180-192; one whose rows below a zeroed node read its
+    previous-sweep V) on the wave kernel's FULL variant with both general paths:
+    the same bar."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = zeroed_cases()[name]
+    B = 192
+    pq = F.scenario_loads(f, np.arange(B), pv_frac=0.0)
+    pf = PowerFlow(f)
+    assert pf.kernel == "wave", pf.info
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    np.testing.assert_array_equal(r["iters"], c["iters"])
+    np.testing.assert_array_equal(r["status"], c["status"])
+    conv = c["status"] == 0
+    assert conv.all()
+    assert (c["V_re"] == 0).any()   # some (node, phase) zeroed
+    assert _vrel(r["V_re"], r["V_im"], c["V_re"], c["V_im"]) <= 1e-10   # zeroed entries: exactly 0 in both
+    _fast_mode_outputs_match(r, c, conv)
+    _close(r["loss"], c["loss"], 1e-8)
+    np.testing.assert_allclose(r["vmin"], c["vmin"], rtol=1e-10)
+    np.testing.assert_allclose(r["vmax"], c["vmax"], rtol=1e-10)
+    e = PowerFlow(f, exact=1)
+    re_ = e.solve(pq[:, :, :16])
+    np.testing.assert_array_equal(re_["V_re"], c["V_re"][..., :16])
+
+
+@pytest.mark.parametrize("name", sorted(restart_cases()))
+def test_restart_below_zeroed_runs_generic(name):
+    """A live phase restarting below a zeroed node in sequential order: the plan
+    declines it and fast mode runs the generic kernel -- the oracle's V, iteration
+    counts and status."""
+    from freedm_amd import PowerFlow
+    from oracle import oracle as O
+    f = restart_cases()[name]
+    pq = F.scenario_loads(f, np.arange(48), pv_frac=0.0)
+    pf = PowerFlow(f)
+    assert pf.kernel == "generic", pf.info
+    r = pf.solve(pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=8)
+    np.testing.assert_array_equal(r["iters"], c["iters"])
+    np.testing.assert_array_equal(r["status"], c["status"])
+    assert _vrel(r["V_re"], r["V_im"], c["V_re"], c["V_im"]) <= 1e-10
 
 
 @pytest.mark.parametrize("name", sorted(wblk_cases()))

@@ -1,12 +1,13 @@
 """The wave kernel's sequential-order plan (fpf_api.cpp: analyse_wave_lag, no
 device): Dl tables whose rows do not follow the feeder tree -- which the tree
 plan declines and which used to run only on the exact generic kernel -- get a
-wave plan; zeroed phases keep the generic kernel."""
+wave plan, zeroed phases included up to 256 branches (past that the generic
+kernel runs them)."""
 import numpy as np
 import pytest
 
 from freedm_amd import feeder as F
-from lag_tables import cases, wblk_cases
+from lag_tables import cases, restart_cases, shuffled_blocks, wblk_cases, zeroed_cases
 from test_wave_plan import _plan
 
 
@@ -52,12 +53,27 @@ def _rows_chain(Dl):
     return False
 
 
-def test_zeroed_phases_stay_generic():
-    f = F.demo_feeder()
-    Z = np.vstack([f.Z, np.diag([0, 2.0 + 6.0j, 0])])
-    Dl = f.Dl[[0, 2, 1, 3, 4, 5, 6, 7, 8]].copy()
-    Dl[6, 3] = 3
-    assert _plan(F.Feeder(Dl, Z))["ok"] == 0
+@pytest.mark.parametrize("name", sorted(zeroed_cases()))
+def test_zeroed_phases_get_a_wave_plan(name):
+    """Sequential-order tables with zeroed phases (one with the rows below a
+    zeroed node reading its previous-sweep V): the wave kernel's plan."""
+    f = zeroed_cases()[name]
+    assert _rows_chain(f.Dl), name
+    p = _plan(f)
+    assert p["ok"] == 1 and p["spw"] >= 1 and p["lds"] <= 159 * 1024, (name, p)
+
+
+@pytest.mark.parametrize("name", sorted(restart_cases()))
+def test_restart_below_zeroed_stays_generic(name):
+    """A live phase below a zeroed node on this sweep's forward path (V there =
+    Vr(k) - Vr(m), short of the 1e-10 bar on the small result): declined."""
+    assert _plan(restart_cases()[name])["ok"] == 0
+
+
+def test_zeroed_phases_past_256_branches_stay_generic():
+    from lag_tables import zeroed
+    f = shuffled_blocks(zeroed(F.synthetic_feeder(700, 700)), 11)
+    assert _plan(f)["ok"] == 0
 
 
 def test_tree_tables_keep_the_tree_plan():

@@ -18,24 +18,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 from freedm_amd import Feeder, PowerFlow, scenario_loads, synthetic_feeder  # noqa: E402
-from lag_tables import shuffled_blocks  # noqa: E402
-
-
-def zeroed(f):
-    """Phase c zeroed on every second lateral unit that no other unit taps (a
-    two-phase line code on its rows, no phase-c load)."""
-    Dl = np.array(f.Dl, copy=True)
-    Z = np.vstack([f.Z, np.diag([f.Z[0, 0], f.Z[1, 1], 0])])
-    code = Z.shape[0] // 3
-    sep = [i for i in range(Dl.shape[0]) if Dl[i, 0] == 0] + [Dl.shape[0]]
-    taps = {int(Dl[i + 1, 1]) for i in sep[:-1] if i + 1 < Dl.shape[0]}
-    leaves = [u for u in range(len(sep) - 1)
-              if not any(int(Dl[r, 2]) in taps for r in range(sep[u] + 1, sep[u + 1]))]
-    for u in leaves[::2]:
-        for r in range(sep[u] + 1, sep[u + 1]):
-            Dl[r, 3] = code
-            Dl[r, 10:12] = 0.0
-    return Feeder(Dl, Z, name=f"{f.name}-zeroed")
+from lag_tables import shuffled_blocks, zeroed  # noqa: E402
 
 
 def leg(f, full, B=4096, reps=10):
