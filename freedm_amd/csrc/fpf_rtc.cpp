@@ -536,12 +536,13 @@ int rtc_build(int device, const RtcSpec &sp, RtcKernel *out, std::string *err) {
 // the static build with the plan's uniform values defined as constants, so the
 // arithmetic -- and every result -- is the static kernel's.  Measured -4 to -5 %
 // kernel time on the 123-bus feeder (profiles/r04sp, r04rtc).
-// build switches of the wave kernel's per-plan build (experiments): FPF_WAVE_RTC_DEFS
-// = comma-separated macro names of fpf_wave_body.h, each defined as 1
+// build switches of the wave and wave-block kernels' per-plan builds (experiments): FPF_WAVE_RTC_DEFS
+// = comma-separated FPF_WAVE_* macro names (fpf_wave_body.h, fpf_wblk_body.h), each defined as 1
 std::string wave_rtc_defs(const WaveDev &w) {
     std::string out;
     const char *e = getenv("FPF_WAVE_RTC_DEFS");
-    if (!e || w.wps) return out;
+    (void)w;
+    if (!e) return out;
     std::string s(e);
     size_t a = 0;
     while (a < s.size()) {

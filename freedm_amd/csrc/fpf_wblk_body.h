@@ -185,7 +185,9 @@ __global__ __launch_bounds__(W * 64, C >= 8 ? 1 : (C <= 2 ? 4 : 2)) void dpf_wbl
     // offsets were 28 % of a config-3 sweep with one block per thread, 3 phases each)
     // (the per-plan builds only: in the static build, with the plan's values at
     // run time, the second chain form spilled 118 VGPRs of the light variant)
-#if defined(FPF_WSPEC) || defined(FPF_WBLK_OFF3_STATIC)
+#if defined(FPF_WAVE_WBLK_NO_OFF3)
+    const bool off3 = false;   // (experiment: the per-plan build with one block per thread)
+#elif defined(FPF_WSPEC) || defined(FPF_WBLK_OFF3_STATIC)
     const bool off3 = chain_regs && 3 * nblk <= NT;
 #else
     // (the general full variants keep it -- zeroed phases 1.65 vs 1.78 ms, 2048-bus x
