@@ -245,3 +245,33 @@ def test_lane_two_streams(monkeypatch):
         np.testing.assert_array_equal(outs[k]["v_im"].cpu().numpy(), ref[k]["v_im"])
         np.testing.assert_array_equal(outs[k]["iters"].cpu().numpy(), ref[k]["iters"])
         np.testing.assert_array_equal(outs[k]["loss"].cpu().numpy(), ref[k]["loss"])
+
+
+@pytest.mark.parametrize("n,seed,lat", [(20, 7, None), (47, 3, 9), (77, 21, 4), (101, 5, 20), (128, 9, 12)])
+def test_lane_random_feeders(n, seed, lat, monkeypatch):
+    """Seeded synthetic feeders of every slot count (tests/test_lane_plan.py: FUZZ)
+    on the lane kernel against the oracle at the north-star bar."""
+    from freedm_amd import PowerFlow
+    monkeypatch.setenv("FPF_LANE", "1")
+    f = F.synthetic_feeder(n, seed, n_laterals=lat)
+    pq = F.scenario_loads(f, np.arange(130), seed=seed)
+    pf = PowerFlow(f)
+    n0 = _launches()
+    r = _solve_light(pf, pq)
+    assert _launches() == n0 + 1
+    _check_oracle(f, pq, r)
+
+
+def test_lane_nested_blocks(monkeypatch):
+    """Block chains six deep with ten one-node laterals (the plan's block table,
+    tests/test_lane_plan.py: the algebra on CPU) on the GPU."""
+    from freedm_amd import PowerFlow
+    from test_gpu_wave import nested_feeder
+    monkeypatch.setenv("FPF_LANE", "1")
+    f = nested_feeder(depth=6, extra=10)
+    pq = F.scenario_loads(f, np.arange(200))
+    n0 = _launches()
+    r = _solve_light(PowerFlow(f), pq)
+    assert _launches() == n0 + 1
+    _check_oracle(f, pq, r)
+

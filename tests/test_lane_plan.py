@@ -183,3 +183,23 @@ def test_lane_algebra_matches_oracle(name):
     Vc = c["V_re"] + 1j * c["V_im"]
     assert np.max(np.abs(r["V"] - Vc) / np.abs(Vc)) <= 1e-12
     np.testing.assert_allclose(r["loss"], c["loss"], rtol=1e-9)
+
+
+# seeded synthetic feeders of every slot count (NS 4 / 8 / 12 / 16), lateral
+# counts and lengths varied: the plan and its algebra against the oracle
+FUZZ = [(20, 7, None), (33, 11, 2), (47, 3, 9), (77, 21, 4), (101, 5, 20), (113, 17, 1), (128, 9, 12)]
+
+
+@pytest.mark.parametrize("n,seed,lat", FUZZ)
+def test_lane_algebra_random_feeders(n, seed, lat):
+    from oracle import oracle as O
+    f = F.synthetic_feeder(n, seed, n_laterals=lat)
+    p = _plan(f)
+    assert p["ok"] == 1, (n, seed, lat)
+    pq = F.scenario_loads(f, np.arange(12), seed=seed)
+    r = lane_emulate(f, p, pq)
+    c = O.dpf_batch(f.Dl, f.Z, pq, nthreads=4)
+    assert (r["iters"] == c["iters"]).all()
+    Vc = c["V_re"] + 1j * c["V_im"]
+    assert np.max(np.abs(r["V"] - Vc) / np.abs(Vc)) <= 1e-12
+
