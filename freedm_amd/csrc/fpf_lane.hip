@@ -26,8 +26,10 @@
 //     Four barriers per sweep: wave totals of E, published E, wave totals of G,
 //     published G.
 // The loads (P, Q) are read from the caller's scenario-fastest batch every sweep
-// (64 consecutive doubles per load instruction; the re-reads hit the Infinity
-// Cache).  A lane whose scenario has finished is frozen -- every update of a
+// (64 consecutive doubles per load instruction, one slot ahead; FPF_LANE_DMA=1:
+// through an LDS-DMA ring three slots ahead) -- 3.2x the algorithmic bytes beyond
+// L2 (profiles/r06_c4lane), the design's bound.  A lane whose
+// scenario has finished is frozen -- every update of a
 // sweep runs under a divergent !done branch -- so its registers keep the V of its
 // last sweep until the workgroup's last scenario is done; then every lane's V
 // leaves in whole 512-byte rows (stored in the sweep each scenario finished, the
@@ -64,11 +66,13 @@ namespace fpf {
 // diagnostic ablation builds (tools/runs: FPF_LANE_ABL bits; results are wrong
 // when set): 1 the loads come from a constant instead of memory, 2 the backward
 // gathers read the slot's own value instead of LDS, 4 every scenario takes
-// exactly 5 sweeps (so that the other bits compare at equal work)
+// exactly 5 sweeps (so that the other bits compare at equal work), 8 no
+// reciprocal in the load currents.  The other switches are the measured
+// alternatives of profiles/r06_lane (the defaults are the faster ones)
 #ifndef FPF_LANE_ABL
 #define FPF_LANE_ABL 0
 #endif
-// slots of loads in flight ahead of the load currents (registers: 12 per slot)
+// the carry loops' three reads issued together (measured slower: 1.151 vs 1.114 ms)
 #ifndef FPF_LANE_LD3
 #define FPF_LANE_LD3 0
 #endif
@@ -78,6 +82,8 @@ namespace fpf {
 #ifndef FPF_LANE_SB
 #define FPF_LANE_SB 1   // (bit 1: a scheduling barrier between the load currents' slots)
 #endif
+// slots of loads in flight ahead of the load currents (registers: 12 per slot;
+// 2 and 3 spill)
 #ifndef FPF_LANE_PF
 #define FPF_LANE_PF 1
 #endif

@@ -115,17 +115,17 @@ def test_sequential_order_tables_on_the_wave_block_kernel(name):
     np.testing.assert_allclose(r["vmax"], c["vmax"], rtol=1e-10)
 
 
-@pytest.mark.parametrize("name", ["123-shuffled1", "123-swapped", "700-shuffled-swapped"])
+@pytest.mark.parametrize("name", ["123-shuffled1", "123-swapped", "700-shuffled-swapped", "123-shuffled-zeroed"])
 def test_sequential_order_device_batches(name):
     """Device buffers, both layouts, a batch past the per-plan build's threshold
     (4096) and a ragged one: V and the scalars against the host-buffer solve's."""
     import torch
     from freedm_amd import PowerFlow
     from oracle import oracle as O
-    f = {**cases(), **wblk_cases()}[name]
+    f = {**cases(), **wblk_cases(), **zeroed_cases()}[name]
     dev = torch.device("cuda:0")
     for B in (4103, 77):
-        pq = F.scenario_loads(f, np.arange(B))
+        pq = F.scenario_loads(f, np.arange(B), pv_frac=0.0 if "zeroed" in name else 0.2)
         for layout in (0, 1):
             pf = PowerFlow(f, layout=layout)
             x = pq if layout == 0 else np.ascontiguousarray(pq.transpose(2, 0, 1))
