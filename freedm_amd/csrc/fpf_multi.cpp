@@ -394,7 +394,7 @@ extern "C" int fpf_multi_solve(fpf_multi *m, int n_scen, const double *pq, const
         hipStream_t st = m->stream[d];
         const size_t nd = (size_t)(hi[d] - lo[d]);
         scal_layout(nd);
-        if (nd == 0) {   // an empty shard still joins the all-reduce, with the identity
+        if (nd == 0) {   // an empty shard still joins the all-gather, with the identity
             MHIP(m, hipMemcpyAsync(m->d_agg[d], ident, sizeof(ident), hipMemcpyHostToDevice, st));
             continue;
         }

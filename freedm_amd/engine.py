@@ -444,7 +444,8 @@ class PowerFlow:
 class MultiPowerFlow:
     """One process, n GPUs (fpf_multi_*): the batch is sharded contiguously over
     devices 0..n-1, every device solves its shard, and the per-device
-    aggregates are combined by one RCCL all-reduce inside the library."""
+    aggregates are combined by one RCCL all-gather inside the library, folded in
+    device order (the same bits as dist.fold_aggregates)."""
 
     def __init__(self, feeder: Feeder, n_gpus: int = 1, kernel: str = "auto", **opts):
         L = _lib.load()

@@ -174,7 +174,8 @@ typedef struct fpf_outputs {
 } fpf_outputs;
 
 /* Batch aggregate (the hosting-study reduction).  Also the payload of the
- * cross-GPU all-reduce: fields 0 (sum) and 3..7 (sum), 1 (min), 2 (max). */
+ * cross-GPU combine (one all-gather, folded in rank / device order by
+ * fpf_aggregate_fold): fields 0 (sum) and 3..7 (sum), 1 (min), 2 (max). */
 typedef struct fpf_aggregate {
     double loss_sum;   /* over converged scenarios                     */
     double vmin;       /* min over converged scenarios                 */
@@ -245,7 +246,8 @@ int         fpf_feeder_check(fpf_feeder *feeder, void *stream);
  * (ncclCommInitAll; xGMI inside an MI355X node).  fpf_multi_solve cuts the
  * batch into contiguous shards (fpf_multi_shard), solves every shard on its
  * device concurrently (pinned, double-buffered chunks: fpf_multi_schedule) and combines the per-device batch aggregates with one
- * RCCL all-reduce (sum of the 8 fields, min of vmin, max of vmax) -- the only
+ * grouped RCCL all-gather of the 8-double rows, folded in device order
+ * (fpf_aggregate_fold: the same bits as dist.fold_aggregates) -- the only
  * exchange: per-scenario results go straight back to the caller's host arrays
  * at their global index.  pq / out / agg as fpf_solve_batch (host memory, the
  * whole batch's layout, either fpf_opts.layout).  Returns >= 0 (non-converged scenarios) or FPF_ERR_*.

@@ -1,7 +1,8 @@
 """Multi-process (world_size 2, gloo on CPU) coverage of the sharded study
 (freedm_amd/dist.py): shard assignment, shard invariance of the
-scenario inputs, and the one collective -- the all-reduce of the study
-aggregates -- against the single-process aggregate of the same scenarios.
+scenario inputs, and the one collective -- the all-gather of the study
+aggregates, folded in rank order -- against the single-process aggregate of the
+same scenarios.
 The per-shard solves use the CPU oracle here (test infrastructure, no GPU in
 this container); on the GPU box bench.py runs the same path over RCCL."""
 import os
