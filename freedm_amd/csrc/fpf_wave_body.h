@@ -326,15 +326,17 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             // the tile's chunk c (scenarios 0 .. SPW-1), shifted to this wave's columns
             const int nchw = wnw * 3 * nl, SUW = f.stage_uw;
             const int2 *tab = (const int2 *)f.stage_smaj;
-            // (a wave with no live scenario -- the tail of a partial last tile --
-            // reads the tile's first chunk, which is inside the batch, not past it)
-            const d2v *src = (const d2v *)(pq + (size_t)(s0 + (wnw > 0 ? wsc0 : 0)) * 6 * nl);
+            // only the wave's own chunks are read (a wave with no live scenario -- the
+            // tail of a partial last tile -- reads nothing, so nothing past the batch;
+            // basing idle waves on the tile instead measured config 4 +1.4 %,
+            // profiles/r06_ab_stage)
+            const d2v *src = (const d2v *)(pq + (size_t)(s0 + wsc0) * 6 * nl);
 #pragma unroll
             for (int u = 0; u < US; ++u) {
                 if (u < SUW) {
                     const int c = u * 64 + lane;
                     wtb[u] = tab[c];
-                    wr[u] = __builtin_nontemporal_load(src + (c < nchw ? c : 0));
+                    if (c < nchw) wr[u] = __builtin_nontemporal_load(src + c);
                 }
             }
         } else if (SU > 0 && (o.smaj || (FPF_WAVE_L0_TABLE && (B & 1) == 0))) {
