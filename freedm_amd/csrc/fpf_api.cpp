@@ -418,6 +418,12 @@ constexpr size_t WAVE_LDS_BUDGET = 159 * 1024;   // 160 KiB per CU minus the ker
 // build): config 2's 4 096-scenario batch on 4-wave workgroups with the per-plan
 // build 37.3 us against 38.9-39.2 on one 8-wave workgroup per CU, static (profiles/r05wio)
 constexpr int WAVE_SMALL_WPB_MIN_SCEN = 4096;
+// ... but only for the geometries whose small workgroups keep the registers of
+// the large ones (fpf_wave_body.h: WaveGeom::eff_minw): with C = 4 both run 2 waves
+// per SIMD at 256 VGPRs; the C <= 2 geometries' 4-wave workgroups would be launched
+// for 3 waves per SIMD at 168 VGPRs and spill (config 5's 36-bus area, <2,2,4>:
+// 37-41 us a launch against 22-27 us on 8-wave workgroups, profiles/r06s2_c5)
+static bool wave_small_wpb_regs_ok(int spw, int C) { return spw * C > 2 && C > 2; }
 
 struct WaveHost {
     bool ok = false;
@@ -866,7 +872,7 @@ void analyse_wave_lag(const HostFeeder &h, WaveHost &w, const std::string &tree_
     else if (lds_at(small) <= WAVE_LDS_BUDGET) wpb = small;
     else return no("per-scenario LDS above the budget");
     w.wpb = wpb;
-    w.wpb_big_batch = (spw * C > 2 && 2 * (lds_at(small) + 1024) <= 160 * 1024) ? small : wpb;
+    w.wpb_big_batch = (wave_small_wpb_regs_ok(spw, C) && 2 * (lds_at(small) + 1024) <= 160 * 1024) ? small : wpb;
     w.ok = true;
 }
 
@@ -1190,7 +1196,7 @@ void analyse_wave(const HostFeeder &h, WaveHost &w) {
     if (lds_at(big) <= WAVE_LDS_BUDGET) wpb = big;
     else if (lds_at(small) <= WAVE_LDS_BUDGET) wpb = small;
     else return no("per-scenario LDS above the budget");
-    wpb_big_batch = (spw * C > 2 && 2 * (lds_at(small) + 1024) <= 160 * 1024) ? small : wpb;
+    wpb_big_batch = (wave_small_wpb_regs_ok(spw, C) && 2 * (lds_at(small) + 1024) <= 160 * 1024) ? small : wpb;
     if (const char *e = getenv("FPF_WAVE_WPB")) {   // experiments
         const int x = atoi(e);
         if (wave_wpb_supported(spw, C, x) && lds_at(x) <= WAVE_LDS_BUDGET) wpb = wpb_big_batch = x;

@@ -87,6 +87,15 @@ constexpr int WAVE_STAGE_U = 16;   // chunks per thread the table-driven staging
 #define FPF_WAVE_SLD_PREF 0
 #endif
 constexpr int REGION_EXTRA = FPF_WAVE_IBO_LDS ? 3 : 0;
+// experiment (per-plan build, FPF_WAVE_RTC_DEFS=FPF_WAVE_DPRIO=m): issue priority
+// flipped per sweep phase -- m = 1: the LDS-chained phases (scans, gathers, the
+// convergence test, block offsets, V) at priority 2 and the VALU-dense ones (load
+// currents, branch drops) at 0; m = 2 the other way round
+#ifndef FPF_WAVE_DPRIO
+#define FPF_WAVE_DPRIO 0
+#endif
+#define WPRIO_CHAIN() do { if (FPF_WAVE_DPRIO) __builtin_amdgcn_s_setprio(FPF_WAVE_DPRIO == 1 ? 2 : 0); } while (0)
+#define WPRIO_DENSE() do { if (FPF_WAVE_DPRIO) __builtin_amdgcn_s_setprio(FPF_WAVE_DPRIO == 1 ? 0 : 2); } while (0)
 
 template <int SPW, int C>
 struct WaveGeom {
@@ -639,6 +648,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
             }
         }
         WSTAMP(4 + 8 * it);
+        WPRIO_DENSE();
         // ---- load currents (:106-130)
         cx il[C][3], ib[C][3];
 #ifndef FPF_WAVE_GROUP
@@ -696,6 +706,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         }
 #endif
 
+        WPRIO_CHAIN();
         // ---- backward sweep (:134-160): Ib = subtree sums via the prefix scan E of IL;
         // Einc is gathered at subtree ends only (leaves)
         cx tot[3], exl[3];
@@ -848,6 +859,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         }
         WSTAMP(7 + 8 * it);
 
+        WPRIO_DENSE();
         // ---- branch drops lng * (Ib . Zl) (:163-178), then the forward prefix scan.
         // Also Re(drop . conj(Ib)) per phase: on a feeder without zeroed phases
         // PQb(0).re - sum_k PQL(k).re = s3 sum_a Re(drop_a conj(Ib_a)) exactly
@@ -931,6 +943,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
                     lp[a] = fma(g[c][a].re, ib[c][a].re, fma(g[c][a].im, ib[c][a].im, lp[a]));
         }
         WSTAMP(8 + 8 * it);
+        WPRIO_CHAIN();
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             cx acc = g[0][p];
@@ -1113,6 +1126,7 @@ __global__ __launch_bounds__(WPB * 64, (FULL && SPW * C > 2 ? 2 : WaveGeom<SPW, 
         done = done || fin;
     }
     WSTAMP(120);
+    if (FPF_WAVE_DPRIO) __builtin_amdgcn_s_setprio(0);
     if (FG && live) {
         // (the full variant with the general paths) the loss and the extremes of the
         // scenario's last sweep from what it left in LDS, outside the sweep loop (a
