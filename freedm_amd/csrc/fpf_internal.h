@@ -397,6 +397,11 @@ int take_exchange_fault(fpf_feeder *f);
 // batches in FPF_LAYOUT_SCEN_FASTEST whatever the feeder's fpf_opts.layout)
 int solve_batch_host(fpf_feeder *f, int n_scen, const double *pq, const fpf_outputs *out, fpf_aggregate *agg,
                      int layout);
+// fpf_vvc.cpp: the step-size search; lazy > 1 solves the first `lazy` candidates
+// and the rest only if the stop rule has not fired (fpf_vvc_round)
+int vvc_line_search(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols, const double *g,
+                    const double *load_nodes, const int *n_loads, int ld, double c0, double alpha, int m_max,
+                    double ploss_orig, fpf_line_search *res, int lazy);
 // launchers (fpf_generic.hip, fpf_tiled.hip, fpf_rtc.cpp)
 hipError_t launch_generic(const FeederDev &f, int n_scen, const double *pq, double *scratch,
                           size_t ld, const OutDev &o, hipStream_t st);

@@ -433,6 +433,12 @@ extern "C" int fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, con
     return FPF_OK;
 }
 
+// the host-synchronous round's first batch of step sizes: the stop of the config-1
+// feeders' rounds falls at m = 0 (123-bus), 23 (Dl_new) and 28 (demo), and the
+// demo's candidates up to 31 converge in 5 sweeps where its last ones take 14-20
+// (one batch of all 101: 41 us of kernel, profiles/r06s2_vvc)
+constexpr int VVC_LAZY_FIRST = 32;
+
 extern "C" int fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols, const double *z, int z_rows,
                              int z_cols, double beta0, double alpha, int m_max, int ld, double *g, double *load_nodes,
                              int *n_loads, double *loss_fwd, double *loss_rev, double *dl_out, double *res) {
@@ -458,8 +464,10 @@ extern "C" int fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, 
         fpf_line_search ls;
         std::memset(&ls, 0, sizeof(ls));
         ls.loss = lossv;
-        rc = fpf_vvc_line_search(feeder, ctrl_dl, nl, ncols, g, load_nodes, n_loads, ld, c0, alpha, m_max, ploss_orig,
-                                 &ls);
+        // the first VVC_LAZY_FIRST step sizes as one batch, the rest only if the
+        // stop rule has not fired among them (fpf_vvc.cpp: vvc_line_search)
+        rc = fpf::vvc_line_search(feeder, ctrl_dl, nl, ncols, g, load_nodes, n_loads, ld, c0, alpha, m_max,
+                                  ploss_orig, &ls, VVC_LAZY_FIRST);
         if (rc < 0) return rc;
         // the reference solves candidates 0 .. stop + 1 (two per step) and throws
         // at the first that does not converge

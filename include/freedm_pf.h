@@ -476,9 +476,12 @@ int         fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl, in
                                    double *stats, signed char *gstatus);
 
 /* One whole VVC round of vvc_main (VoltVarCtrl.cpp:1141-1762): the gradient,
- * the step-size search as one batch (fpf_vvc_line_search), and the reversed
- * search when the reference reverses.  loss_fwd / loss_rev [m_max + 1] (loss_rev
- * may be NULL), dl_out (nl x ncols): the control after the round (the kept
+ * the step-size search batched (fpf_vvc_line_search's candidates: the first 32
+ * step sizes as one batch, the rest as a second only when the stop rule has not
+ * fired among the first), and the reversed search when the reference reverses.
+ * loss_fwd / loss_rev [m_max + 1] (loss_rev may be NULL; NaN for the step sizes
+ * past the stop that were not solved -- the reference never solves a candidate
+ * past stop + 1), dl_out (nl x ncols): the control after the round (the kept
  * candidate, Dl = Dl_osize, :1486/1707; else ctrl_dl).  res[13] = Ploss_orig,
  * Vmin_orig, Vmax_orig, c0, stop_fwd, stop_rev, reversed, sent (the S2
  * set-points go to the slaves, :1495/1716), Ploss_after, gmin, gmax,
