@@ -80,3 +80,23 @@ def test_load_nodes_follow_the_reference_scan():
     for x in range(3):
         want = [f.Dl[i, 2] for i in range(f.nl) if int(f.Dl[i, 6 + 2 * x]) != 0]
         assert list(nodes[x]) == want[:len(nodes[x])]
+
+
+@pytest.mark.parametrize("which", ["demo", "dl_new", "123bus"])
+def test_round_staged_search_equals_one_batch(which):
+    """fpf_vvc_round solves the first 32 step sizes as one batch and the rest only
+    when the stop rule has not fired among them (fpf_vvc.cpp: vvc_line_search):
+    its decisions and its losses up to the stop equal the one-batch search's
+    (fpf_vvc_line_search, every candidate) bit for bit -- a scenario's result does
+    not depend on the batch it is solved in -- and the step sizes it did not
+    solve read NaN."""
+    from freedm_amd import PowerFlow
+    f = {"demo": F.demo_feeder, "dl_new": F.dl_new_feeder, "123bus": lambda: F.synthetic_feeder(123, 123)}[which]()
+    pf = PowerFlow(f)
+    r = pf.vvc_round(f.Dl)
+    full = pf.vvc_line_search(f.Dl, r["g"], r["load_nodes"], r["c0"], 1.1, 100, r["ploss_orig"])
+    stop = r["stop_fwd"]
+    assert stop == full["stop"] and r["reversed"] == full["reverse"]
+    solved = 101 if stop < 0 or stop + 1 >= 32 else 32
+    np.testing.assert_array_equal(r["loss_fwd"][:solved], full["loss"][:solved])
+    assert np.isnan(r["loss_fwd"][solved:]).all()
