@@ -1056,7 +1056,7 @@ def main():
             if (n_vis > 1 and os.environ.get("FPF_BENCH_MULTI") != "0") or os.environ.get("FPF_BENCH_MULTI") == "1":
                 # in a child process with a time limit: the bench line does not depend on it
                 res["multi_gpu_inproc"] = _multi_leg_child(n_vis)
-            c1["note"] =("fpf_vvc_round (gradient + 101 step sizes in one batch + reversal), host-synchronous, "
+            c1["note"] =("fpf_vvc_round (gradient + the step sizes batched (the first 32, the rest only without a stop) + reversal), host-synchronous, "
                           "per config-1 feeder")
             res["config1_vvc_round"] = c1
             if not args.no_cpu_baseline:
