@@ -102,6 +102,8 @@ struct fpf_feeder {
     // the guard's local mode inside the wave kernel (solves without an aggregate):
     // the exact op lists as a device-side FeederDev
     FeederDev *d_fixdev = nullptr;
+    // the VVC batch paths' cached scratch (fpf::feeder_buf): [slot] = (pointer, bytes)
+    std::vector<std::pair<void *, size_t>> bufs_dev, bufs_host;
 };
 
 // The guard band of the fast kernels' convergence test (fpf_opts.no_guard).
@@ -119,6 +121,27 @@ static int fail(fpf_ctx *ctx, int code, const std::string &msg) {
     return code;
 }
 int fpf::feeder_fail(fpf_feeder *f, int code, const std::string &msg) { return fail(f ? f->ctx : nullptr, code, msg); }
+
+void *fpf::feeder_buf(fpf_feeder *f, int slot, size_t bytes, bool host) {
+    if (!f || slot < 0) return nullptr;
+    auto &v = host ? f->bufs_host : f->bufs_dev;
+    if ((size_t)slot >= v.size()) v.resize((size_t)slot + 1, {nullptr, 0});
+    auto &b = v[(size_t)slot];
+    bytes = std::max<size_t>(bytes, 256);
+    if (b.first && b.second >= bytes) return b.first;
+    if (b.first) (void)(host ? hipHostFree(b.first) : hipFree(b.first));
+    b = {nullptr, 0};
+    // (a little headroom: the next batch of a study is often slightly larger)
+    const size_t want = bytes + bytes / 8;
+    const hipError_t e = host ? hipHostMalloc(&b.first, want) : hipMalloc(&b.first, want);
+    if (e != hipSuccess) {
+        b = {nullptr, 0};
+        fail(f->ctx, FPF_ERR_HIP, std::string("scratch allocation: ") + hipGetErrorString(e));
+        return nullptr;
+    }
+    b.second = want;
+    return b.first;
+}
 
 #define HIPCHK(ctx, expr)                                                                      \
     do {                                                                                       \
@@ -2221,6 +2244,8 @@ extern "C" void fpf_feeder_destroy(fpf_feeder *f) {
     (void)hipFree(f->d_fix_scratch);
     (void)hipFree(f->d_fixdev);
     if (f->agg_event) (void)hipEventDestroy(f->agg_event);
+    for (auto &b : f->bufs_dev) (void)hipFree(b.first);
+    for (auto &b : f->bufs_host) (void)hipHostFree(b.first);
     if (f->rtc) rtc_release(f->rtc_kernel);
     if (f->rtc_ib) rtc_release(f->rtc_kernel_ib);
     delete f;

@@ -390,6 +390,11 @@ int fixup_batch_device(fpf_feeder *f, int n_scen, const double *d_pq, const fpf_
                        void *stream, int layout);
 // record msg as the feeder's context's last error (fpf_last_error) and return code
 int feeder_fail(fpf_feeder *f, int code, const std::string &msg);
+// Scratch of the VVC batch paths (fpf_vvc_grad.cpp), cached on the feeder by slot
+// across calls: device memory (or pinned host memory, host = true) of at least
+// `bytes`, grown on demand (the only hipMalloc / hipFree of a repeated call),
+// freed with the feeder.  nullptr on failure (the feeder's context has the error).
+void *feeder_buf(fpf_feeder *f, int slot, size_t bytes, bool host = false);
 // FPF_ERR_EXCHANGE (with the message) if the feeder's paired-kernel fault word is
 // set, clearing it; FPF_OK otherwise (fpf_api.cpp)
 int take_exchange_fault(fpf_feeder *f);

@@ -508,25 +508,28 @@ extern "C" int fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, 
 // on the host once per batch, from the first converged scenario.
 
 namespace {
-template <class T>
-struct DevArr {   // a device copy of a host vector
-    T *p = nullptr;
-    ~DevArr() { (void)hipFree(p); }
-    hipError_t up(const std::vector<T> &v) {
-        hipError_t e = hipMalloc(&p, sizeof(T) * std::max<size_t>(v.size(), 1));
-        if (e == hipSuccess && !v.empty()) e = hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice);
-        return e;
-    }
+// the cached scratch slots of the batch paths (fpf::feeder_buf): reused call after
+// call, so a repeated call allocates nothing and uploads its plan in one copy per
+// phase -- the per-array hipMalloc / hipMemcpy / hipFree of the first version cost
+// more than the whole device work on the small feeders (profiles/r06s2_vvcb)
+enum : int {
+    SB_PQ = 0,      // the batch's loads [6][Nl][B] (fpf_vvc_round_batch reads them again)
+    SB_VP,          // Vpolar of the base solves
+    SB_RES,         // iters | status | loss | vmin | vmax of the base solves
+    SB_FLAGS,       // gstatus | singular flags of the three phases
+    SB_G,           // g [B][3][ld]
+    SB_PLAN0,       // + x: phase x's plan arrays (device)
+    SB_A0 = SB_PLAN0 + 3,   // + x: phase x's J^T chunk
+    SB_RHS0 = SB_A0 + 3,    // + x: its right-hand sides
+    SB_RB_G = SB_RHS0 + 3,  // fpf_vvc_round_batch: g, the Q-update triples, the pass lists
+    SB_RB_TRI,
+    SB_RB_TODO,
+    SB_RB_CAND,
+    SB_RB_OUT,      // candidates' loss | status
+    SB_HOST_PLAN0 = 0,      // pinned host slots: + x, phase x's plan arrays
+    SB_HOST_RES = 3,        // the base solves' scalars, the flags
 };
-struct PhaseBufs {
-    DevArr<int32_t> vrow, bs, br, inc_ptr, inc_br, y_ptr, y_col, ld_ptr, ld_ia;
-    DevArr<int8_t> vmask, inc_role;
-    DevArr<double> yre_sr, y_re, y_im, ydiag_re, ydiag_im;
-};
-struct DevBuf {
-    void *p = nullptr;
-    ~DevBuf() { (void)hipFree(p); }
-};
+constexpr size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
 }  // namespace
 
 extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols, const double *z,
@@ -564,37 +567,40 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
         if (e_ != hipSuccess)                                                                           \
             return fpf::feeder_fail(feeder, FPF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
+#define BUF(var, slot, bytes, host)                                         \
+    void *var = fpf::feeder_buf(feeder, (slot), (bytes), (host));           \
+    if (!var) return FPF_ERR_HIP
     // ---- the base solves (VoltVarCtrl.cpp:1141), scenario fastest
-    DevBuf d_pq, d_vp, d_it, d_stt, d_loss, d_vmin, d_vmax, d_gst;
-    GCHK(hipMalloc(&d_pq.p, sizeof(double) * 6 * nl * b));
-    GCHK(hipMalloc(&d_vp.p, sizeof(double) * 6 * nn * b));
-    GCHK(hipMalloc(&d_it.p, sizeof(int32_t) * b));
-    GCHK(hipMalloc(&d_stt.p, b));
-    GCHK(hipMalloc(&d_loss.p, sizeof(double) * b));
-    GCHK(hipMalloc(&d_vmin.p, sizeof(double) * b));
-    GCHK(hipMalloc(&d_vmax.p, sizeof(double) * b));
-    GCHK(hipMalloc(&d_gst.p, b));
-    GCHK(hipMemcpy(d_pq.p, pq, sizeof(double) * 6 * nl * b, hipMemcpyHostToDevice));
+    // results region: iters | status | loss | vmin | vmax (one copy back)
+    const size_t o_it = 0, o_st = al256(4 * b), o_loss = o_st + al256(b), o_vmin = o_loss + al256(8 * b),
+                 o_vmax = o_vmin + al256(8 * b), res_bytes = o_vmax + al256(8 * b);
+    // flags region: gstatus | singular of phase 0 | 1 | 2
+    const size_t o_sing = al256(b), flags_bytes = o_sing + 3 * al256(b);
+    BUF(d_pq, SB_PQ, sizeof(double) * 6 * nl * b, false);
+    BUF(d_vp, SB_VP, sizeof(double) * 6 * nn * b, false);
+    BUF(d_res, SB_RES, res_bytes, false);
+    BUF(d_fl, SB_FLAGS, flags_bytes, false);
+    BUF(h_res, SB_HOST_RES, std::max(res_bytes, flags_bytes), true);
+    char *const dr = (char *)d_res, *const hr = (char *)h_res, *const dfl = (char *)d_fl;
+    int8_t *const d_gst = (int8_t *)dfl;
+    GCHK(hipMemcpy(d_pq, pq, sizeof(double) * 6 * nl * b, hipMemcpyHostToDevice));
     fpf_outputs o;
     std::memset(&o, 0, sizeof(o));
-    o.vpolar = (double *)d_vp.p;
-    o.iters = (int *)d_it.p;
-    o.status = (signed char *)d_stt.p;
-    o.loss = (double *)d_loss.p;
-    o.vmin = (double *)d_vmin.p;
-    o.vmax = (double *)d_vmax.p;
-    int rc = fpf::solve_batch_device_ex(feeder, B, (const double *)d_pq.p, &o, nullptr, (void *)st, nullptr, nullptr,
+    o.vpolar = (double *)d_vp;
+    o.iters = (int *)(dr + o_it);
+    o.status = (signed char *)(dr + o_st);
+    o.loss = (double *)(dr + o_loss);
+    o.vmin = (double *)(dr + o_vmin);
+    o.vmax = (double *)(dr + o_vmax);
+    int rc = fpf::solve_batch_device_ex(feeder, B, (const double *)d_pq, &o, nullptr, (void *)st, nullptr, nullptr,
                                         FPF_LAYOUT_SCEN_FASTEST);
     if (rc < 0) return rc;
-    std::vector<int8_t> h_st(b);
-    std::vector<int32_t> h_it(b);
-    std::vector<double> h_loss(b), h_vmin(b), h_vmax(b);
-    GCHK(hipMemcpy(h_st.data(), d_stt.p, b, hipMemcpyDeviceToHost));
-    GCHK(hipMemcpy(h_it.data(), d_it.p, sizeof(int32_t) * b, hipMemcpyDeviceToHost));
-    GCHK(hipMemcpy(h_loss.data(), d_loss.p, sizeof(double) * b, hipMemcpyDeviceToHost));
-    GCHK(hipMemcpy(h_vmin.data(), d_vmin.p, sizeof(double) * b, hipMemcpyDeviceToHost));
-    GCHK(hipMemcpy(h_vmax.data(), d_vmax.p, sizeof(double) * b, hipMemcpyDeviceToHost));
-    rc = fpf::take_exchange_fault(feeder);   // (the copies above synchronised the device)
+    GCHK(hipMemcpy(hr, dr, res_bytes, hipMemcpyDeviceToHost));
+    const int8_t *const h_st = (const int8_t *)(hr + o_st);
+    const int32_t *const h_it = (const int32_t *)(hr + o_it);
+    const double *const h_loss = (const double *)(hr + o_loss), *const h_vmin = (const double *)(hr + o_vmin),
+                        *const h_vmax = (const double *)(hr + o_vmax);
+    rc = fpf::take_exchange_fault(feeder);   // (the copy above synchronised the device)
     if (rc) return rc;
     int s0 = -1;
     for (int s = 0; s < B && s0 < 0; ++s)
@@ -614,7 +620,7 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
     }
     // ---- the plan, from the first converged scenario's Vpolar (nn x 6 column-major)
     std::vector<double> vp0((size_t)6 * nn);
-    GCHK(hipMemcpy2D(vp0.data(), sizeof(double), (const double *)d_vp.p + s0, sizeof(double) * b, sizeof(double),
+    GCHK(hipMemcpy2D(vp0.data(), sizeof(double), (const double *)d_vp + s0, sizeof(double) * b, sizeof(double),
                      (size_t)6 * nn, hipMemcpyDeviceToHost));
     GradPlan plan;
     std::string err;
@@ -626,10 +632,10 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
                                     "fpf_vvc_gradient_batch: phase " + std::to_string(x) + " has " +
                                         std::to_string(plan.ph[x].lnum) +
                                         " load nodes; the device LU holds at most 3200 (fpf_vvc_gradient runs it)");
-    GCHK(hipMemcpy(d_gst.p, h_gst.data(), b, hipMemcpyHostToDevice));
-    DevBuf d_g;
-    GCHK(hipMalloc(&d_g.p, sizeof(double) * b * 3 * ld));
-    GCHK(hipMemset(d_g.p, 0, sizeof(double) * b * 3 * ld));
+    GCHK(hipMemcpy(d_gst, h_gst.data(), b, hipMemcpyHostToDevice));
+    GCHK(hipMemset(dfl + o_sing, 0, 3 * al256(b)));
+    BUF(d_g, SB_G, sizeof(double) * b * 3 * ld, false);
+    GCHK(hipMemset(d_g, 0, sizeof(double) * b * 3 * ld));
     // the three phases' set-up / LU / g on three streams: independent matrices (one
     // workgroup each), so their launches overlap; their buffers live until the end.
     // The streams are the device's, created once (creating three per call cost
@@ -651,12 +657,6 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
         }
         for (int x = 0; x < 3; ++x) ps.s[x] = it->second[x];
     }
-    struct PhaseWork {
-        PhaseBufs pb;
-        DevBuf A, rhs, sing;
-        bool used = false;
-    };
-    PhaseWork work[3];
     for (int x = 0; x < 3; ++x) {
         const PhaseNet &P = plan.ph[x];
         const int L = P.lnum, n = L + 1, m1 = n - 1, nf = 2 * m1;
@@ -702,23 +702,33 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
                 if (P.node[ia + 1] == plan.loads[x][j]) ld_ia.push_back(ia);
             ld_ptr.push_back((int32_t)ld_ia.size());
         }
-        PhaseBufs &pb = work[x].pb;
-        GCHK(pb.vrow.up(P.vrow));
-        GCHK(pb.vmask.up(vmask));
-        GCHK(pb.bs.up(P.s));
-        GCHK(pb.br.up(P.r));
-        GCHK(pb.yre_sr.up(yre_sr));
-        GCHK(pb.inc_ptr.up(inc_ptr));
-        GCHK(pb.inc_br.up(inc_br));
-        GCHK(pb.inc_role.up(inc_role));
-        GCHK(pb.y_ptr.up(y_ptr));
-        GCHK(pb.y_col.up(y_col));
-        GCHK(pb.y_re.up(y_re));
-        GCHK(pb.y_im.up(y_im));
-        GCHK(pb.ydiag_re.up(yd_re));
-        GCHK(pb.ydiag_im.up(yd_im));
-        GCHK(pb.ld_ptr.up(ld_ptr));
-        GCHK(pb.ld_ia.up(ld_ia));
+        // the sixteen arrays packed into the phase's pinned slot, one copy up
+        struct Arr {
+            const void *p;
+            size_t bytes;
+            size_t off;
+        };
+        Arr arrs[16] = {{P.vrow.data(), 4 * P.vrow.size(), 0},  {vmask.data(), vmask.size(), 0},
+                        {P.s.data(), 4 * P.s.size(), 0},        {P.r.data(), 4 * P.r.size(), 0},
+                        {yre_sr.data(), 8 * yre_sr.size(), 0},  {inc_ptr.data(), 4 * inc_ptr.size(), 0},
+                        {inc_br.data(), 4 * inc_br.size(), 0},  {inc_role.data(), inc_role.size(), 0},
+                        {y_ptr.data(), 4 * y_ptr.size(), 0},    {y_col.data(), 4 * y_col.size(), 0},
+                        {y_re.data(), 8 * y_re.size(), 0},      {y_im.data(), 8 * y_im.size(), 0},
+                        {yd_re.data(), 8 * yd_re.size(), 0},    {yd_im.data(), 8 * yd_im.size(), 0},
+                        {ld_ptr.data(), 4 * ld_ptr.size(), 0},  {ld_ia.data(), 4 * ld_ia.size(), 0}};
+        static_assert(sizeof(P.vrow[0]) == 4 && sizeof(P.s[0]) == 4 && sizeof(P.r[0]) == 4, "int32 plan arrays");
+        size_t tot = 0;
+        for (Arr &a : arrs) {
+            a.off = tot;
+            tot += al256(std::max<size_t>(a.bytes, 1));
+        }
+        BUF(h_plan, SB_HOST_PLAN0 + x, tot, true);
+        BUF(d_plan, SB_PLAN0 + x, tot, false);
+        for (const Arr &a : arrs)
+            if (a.bytes) std::memcpy((char *)h_plan + a.off, a.p, a.bytes);
+        const hipStream_t sx = ps.s[x];
+        GCHK(hipMemcpyAsync(d_plan, h_plan, tot, hipMemcpyHostToDevice, sx));
+        auto dp = [&](int i) { return (void *)((char *)d_plan + arrs[i].off); };
         fpf::GradPhaseDev D;
         D.x = x;
         D.L = L;
@@ -726,52 +736,48 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
         D.nn = nn;
         D.scan_end = P.scan_end;
         D.n_loads = nld;
-        D.vrow = pb.vrow.p;
-        D.vmask = pb.vmask.p;
-        D.bs = pb.bs.p;
-        D.br = pb.br.p;
-        D.yre_sr = pb.yre_sr.p;
-        D.inc_ptr = pb.inc_ptr.p;
-        D.inc_br = pb.inc_br.p;
-        D.inc_role = pb.inc_role.p;
-        D.y_ptr = pb.y_ptr.p;
-        D.y_col = pb.y_col.p;
-        D.y_re = pb.y_re.p;
-        D.y_im = pb.y_im.p;
-        D.ydiag_re = pb.ydiag_re.p;
-        D.ydiag_im = pb.ydiag_im.p;
-        D.ld_ptr = pb.ld_ptr.p;
-        D.ld_ia = pb.ld_ia.p;
+        D.vrow = (int32_t *)dp(0);
+        D.vmask = (int8_t *)dp(1);
+        D.bs = (int32_t *)dp(2);
+        D.br = (int32_t *)dp(3);
+        D.yre_sr = (double *)dp(4);
+        D.inc_ptr = (int32_t *)dp(5);
+        D.inc_br = (int32_t *)dp(6);
+        D.inc_role = (int8_t *)dp(7);
+        D.y_ptr = (int32_t *)dp(8);
+        D.y_col = (int32_t *)dp(9);
+        D.y_re = (double *)dp(10);
+        D.y_im = (double *)dp(11);
+        D.ydiag_re = (double *)dp(12);
+        D.ydiag_im = (double *)dp(13);
+        D.ld_ptr = (int32_t *)dp(14);
+        D.ld_ia = (int32_t *)dp(15);
         // the dense J^T of a chunk of scenarios at a time (nf^2 doubles each, within ~2 GB)
         const size_t per = (size_t)nf * nf * sizeof(double);
         const int chunk = (int)std::max<size_t>(1, std::min<size_t>(b, ((size_t)2 << 30) / per));
-        PhaseWork &w = work[x];
-        GCHK(hipMalloc(&w.A.p, per * chunk));
-        GCHK(hipMalloc(&w.rhs.p, sizeof(double) * nf * chunk));
-        GCHK(hipMalloc(&w.sing.p, b));
-        w.used = true;
-        const hipStream_t sx = ps.s[x];
+        BUF(d_A, SB_A0 + x, per * chunk, false);
+        BUF(d_rhs, SB_RHS0 + x, sizeof(double) * nf * chunk, false);
+        int8_t *const d_sing = (int8_t *)(dfl + o_sing + x * al256(b));
         for (int c0 = 0; c0 < B; c0 += chunk) {
             const int nb = std::min(chunk, B - c0);
-            double *A = (double *)w.A.p, *rhs = (double *)w.rhs.p;
-            GCHK(fpf::launch_gradb_setup(D, B, c0, nb, (const double *)d_vp.p, A, rhs, (int8_t *)d_gst.p, sx));
+            double *A = (double *)d_A, *rhs = (double *)d_rhs;
+            GCHK(fpf::launch_gradb_setup(D, B, c0, nb, (const double *)d_vp, A, rhs, d_gst, sx));
             // lambda = -inv(J^T) Fx: one LU with partial pivoting and one solve per matrix
-            GCHK(fpf::launch_gradb_lu(nf, nb, A, rhs, (int8_t *)w.sing.p + c0, sx));
-            GCHK(fpf::launch_gradb_g(D, c0, nb, rhs, ld, (double *)d_g.p, sx));
+            GCHK(fpf::launch_gradb_lu(nf, nb, A, rhs, d_sing + c0, sx));
+            GCHK(fpf::launch_gradb_g(D, c0, nb, rhs, ld, (double *)d_g, sx));
         }
     }
-    std::vector<int8_t> sing(b);
+    for (int x = 0; x < 3; ++x) GCHK(hipStreamSynchronize(ps.s[x]));
+    // per-scenario results: the device's pattern flags and the singular matrices
+    // merged with the host's, one copy back
+    GCHK(hipMemcpy(hr, dfl, flags_bytes, hipMemcpyDeviceToHost));
+    const int8_t *const d_flags = (const int8_t *)hr;
     for (int x = 0; x < 3; ++x) {
-        GCHK(hipStreamSynchronize(ps.s[x]));
-        if (!work[x].used) continue;
-        GCHK(hipMemcpy(sing.data(), work[x].sing.p, b, hipMemcpyDeviceToHost));
+        const int8_t *sing = (const int8_t *)(hr + o_sing + x * al256(b));
         for (int s = 0; s < B; ++s)
             if (sing[s] != 0 && h_gst[s] == fpf::FPF_GRAD_OK) h_gst[s] = fpf::FPF_GRAD_SINGULAR;
     }
-    // per-scenario results: the device's pattern flags merged with the host's
-    std::vector<int8_t> d_flags(b);
-    GCHK(hipMemcpy(d_flags.data(), d_gst.p, b, hipMemcpyDeviceToHost));
-    GCHK(hipMemcpy(g, d_g.p, sizeof(double) * b * 3 * ld, hipMemcpyDeviceToHost));
+    GCHK(hipMemcpy(g, d_g, sizeof(double) * b * 3 * ld, hipMemcpyDeviceToHost));
     int bad = 0;
     for (int s = 0; s < B; ++s) {
         int8_t gs = h_gst[s];
@@ -803,6 +809,7 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
     }
     return bad;
 #undef GCHK
+#undef BUF
 }
 
 // ---------------------------------------------------------------------------
@@ -883,20 +890,22 @@ extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, in
             for (int r : rows[x][i]) tri.insert(tri.end(), {x, i, r});
     const int T = (int)(tri.size() / 3);
     const size_t Bmax = (size_t)todo.size() * M;
-    DevBuf d_pq, d_g, d_tri, d_todo, d_cst, d_cand, d_loss, d_stat;
+    // the cached scratch (fpf::feeder_buf); the loads are still in SB_PQ, where
+    // fpf_vvc_gradient_batch put them above
+    void *d_pq = nullptr, *d_g = nullptr, *d_tri = nullptr, *d_todo = nullptr, *d_cand = nullptr, *d_out = nullptr;
+    const size_t o_cst = al256(sizeof(int32_t) * b), o_stat = al256(sizeof(double) * Bmax);
     if (!todo.empty()) {
-        RCHK(hipMalloc(&d_pq.p, sizeof(double) * 6 * nlz * b));
-        RCHK(hipMalloc(&d_g.p, sizeof(double) * b * 3 * ld));
-        RCHK(hipMalloc(&d_tri.p, sizeof(int32_t) * std::max<size_t>(tri.size(), 1)));
-        RCHK(hipMalloc(&d_todo.p, sizeof(int32_t) * b));
-        RCHK(hipMalloc(&d_cst.p, sizeof(double) * b));
-        RCHK(hipMalloc(&d_cand.p, sizeof(double) * 6 * nlz * Bmax));
-        RCHK(hipMalloc(&d_loss.p, sizeof(double) * Bmax));
-        RCHK(hipMalloc(&d_stat.p, Bmax));
-        RCHK(hipMemcpy(d_pq.p, pq, sizeof(double) * 6 * nlz * b, hipMemcpyHostToDevice));
-        RCHK(hipMemcpy(d_g.p, g, sizeof(double) * b * 3 * ld, hipMemcpyHostToDevice));
-        if (!tri.empty()) RCHK(hipMemcpy(d_tri.p, tri.data(), sizeof(int32_t) * tri.size(), hipMemcpyHostToDevice));
+        d_pq = fpf::feeder_buf(feeder, SB_PQ, sizeof(double) * 6 * nlz * b);
+        d_g = fpf::feeder_buf(feeder, SB_RB_G, sizeof(double) * b * 3 * ld);
+        d_tri = fpf::feeder_buf(feeder, SB_RB_TRI, sizeof(int32_t) * std::max<size_t>(tri.size(), 1));
+        d_todo = fpf::feeder_buf(feeder, SB_RB_TODO, o_cst + sizeof(double) * b);   // todo | cstart
+        d_cand = fpf::feeder_buf(feeder, SB_RB_CAND, sizeof(double) * 6 * nlz * Bmax);
+        d_out = fpf::feeder_buf(feeder, SB_RB_OUT, o_stat + Bmax);                  // loss | status
+        if (!d_pq || !d_g || !d_tri || !d_todo || !d_cand || !d_out) return FPF_ERR_HIP;
+        RCHK(hipMemcpy(d_g, g, sizeof(double) * b * 3 * ld, hipMemcpyHostToDevice));
+        if (!tri.empty()) RCHK(hipMemcpy(d_tri, tri.data(), sizeof(int32_t) * tri.size(), hipMemcpyHostToDevice));
     }
+    std::vector<char> h_out;
     for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
         const int K = (int)todo.size();
         const size_t Bc = (size_t)K * M;
@@ -908,22 +917,26 @@ extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, in
             const double *st8 = &stats[(size_t)todo[k] * 8];
             cstart[k] = pass == 0 ? st8[3] : -beta0 / (bkva / 3) / st8[2];
         }
-        RCHK(hipMemcpy(d_todo.p, todo.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice));
-        RCHK(hipMemcpy(d_cst.p, cstart.data(), sizeof(double) * K, hipMemcpyHostToDevice));
-        RCHK(fpf::launch_vvc_candidates((const double *)d_pq.p, nl, B, (const int32_t *)d_todo.p, K, M,
-                                        (const int32_t *)d_tri.p, T, (const double *)d_g.p, ld, scale, alpha,
-                                        (const double *)d_cst.p, (double *)d_cand.p, nullptr));
+        // the pass's scenario list and first step sizes, one copy up
+        std::vector<char> up(o_cst + sizeof(double) * K);
+        std::memcpy(up.data(), todo.data(), sizeof(int32_t) * K);
+        std::memcpy(up.data() + o_cst, cstart.data(), sizeof(double) * K);
+        RCHK(hipMemcpy(d_todo, up.data(), up.size(), hipMemcpyHostToDevice));
+        RCHK(fpf::launch_vvc_candidates((const double *)d_pq, nl, B, (const int32_t *)d_todo, K, M,
+                                        (const int32_t *)d_tri, T, (const double *)d_g, ld, scale, alpha,
+                                        (const double *)((char *)d_todo + o_cst), (double *)d_cand, nullptr));
         fpf_outputs out;
         std::memset(&out, 0, sizeof(out));
-        out.loss = (double *)d_loss.p;
-        out.status = (signed char *)d_stat.p;
-        rc = fpf::solve_batch_device_ex(feeder, (int)Bc, (const double *)d_cand.p, &out, nullptr, nullptr, nullptr,
+        out.loss = (double *)d_out;
+        out.status = (signed char *)((char *)d_out + o_stat);
+        rc = fpf::solve_batch_device_ex(feeder, (int)Bc, (const double *)d_cand, &out, nullptr, nullptr, nullptr,
                                         nullptr, FPF_LAYOUT_SCEN_FASTEST);
         if (rc < 0) return rc;
-        std::vector<double> loss(Bc);
-        std::vector<signed char> status(Bc);
-        RCHK(hipMemcpy(loss.data(), d_loss.p, sizeof(double) * Bc, hipMemcpyDeviceToHost));
-        RCHK(hipMemcpy(status.data(), d_stat.p, Bc, hipMemcpyDeviceToHost));
+        // loss | status back in one copy
+        h_out.resize(o_stat + Bc);
+        RCHK(hipMemcpy(h_out.data(), d_out, o_stat + Bc, hipMemcpyDeviceToHost));
+        const double *const loss = (const double *)h_out.data();
+        const signed char *const status = (const signed char *)(h_out.data() + o_stat);
         rc = fpf::take_exchange_fault(feeder);   // (the copies above synchronised the device)
         if (rc) return rc;
         std::vector<int> next;
