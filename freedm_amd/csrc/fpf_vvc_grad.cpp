@@ -814,9 +814,10 @@ extern "C" int fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl,
 
 // ---------------------------------------------------------------------------
 // A whole VVC round per load scenario (VoltVarCtrl.cpp:1141-1762 for B scenarios
-// of one control table): the batched gradient, then every scenario's m_max + 1
-// step sizes as ONE device batch (B x (m_max + 1) solves), the reference's stop
-// rule per scenario, and one more batch for the scenarios whose search reverses.
+// of one control table): the batched gradient, then every scenario's step sizes
+// as device batches (the first VVC_LAZY_FIRST of every search as one, the rest of
+// the searches without a stop as a second), the reference's stop rule per
+// scenario, and the same for the scenarios whose search reverses.
 
 namespace {
 // the reference's stop rule over one search (VoltVarCtrl.cpp:1330-1540, as
@@ -906,39 +907,72 @@ extern "C" int fpf_vvc_round_batch(fpf_feeder *feeder, const double *ctrl_dl, in
         if (!tri.empty()) RCHK(hipMemcpy(d_tri, tri.data(), sizeof(int32_t) * tri.size(), hipMemcpyHostToDevice));
     }
     std::vector<char> h_out;
+    std::vector<double> lossv;
+    std::vector<signed char> statv;
     for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
         const int K = (int)todo.size();
-        const size_t Bc = (size_t)K * M;
-        // candidate (k, m) = column k M + m: scenario todo[k]'s loads with its Q
-        // set-points moved by -g (bkva/3) c_m, c_0 = c0 (:1323) or the reversed
-        // start -beta0/(bkva/3)/gabs_min (:1546), c_{m+1} = alpha c_m (:1420-1422)
+        // candidate (k, m): scenario todo[k]'s loads with its Q set-points moved by
+        // -g (bkva/3) c_m, c_0 = c0 (:1323) or the reversed start
+        // -beta0/(bkva/3)/gabs_min (:1546), c_{m+1} = alpha c_m (:1420-1422)
         std::vector<double> cstart(K);
         for (int k = 0; k < K; ++k) {
             const double *st8 = &stats[(size_t)todo[k] * 8];
             cstart[k] = pass == 0 ? st8[3] : -beta0 / (bkva / 3) / st8[2];
         }
-        // the pass's scenario list and first step sizes, one copy up
-        std::vector<char> up(o_cst + sizeof(double) * K);
-        std::memcpy(up.data(), todo.data(), sizeof(int32_t) * K);
-        std::memcpy(up.data() + o_cst, cstart.data(), sizeof(double) * K);
-        RCHK(hipMemcpy(d_todo, up.data(), up.size(), hipMemcpyHostToDevice));
-        RCHK(fpf::launch_vvc_candidates((const double *)d_pq, nl, B, (const int32_t *)d_todo, K, M,
-                                        (const int32_t *)d_tri, T, (const double *)d_g, ld, scale, alpha,
-                                        (const double *)((char *)d_todo + o_cst), (double *)d_cand, nullptr));
-        fpf_outputs out;
-        std::memset(&out, 0, sizeof(out));
-        out.loss = (double *)d_out;
-        out.status = (signed char *)((char *)d_out + o_stat);
-        rc = fpf::solve_batch_device_ex(feeder, (int)Bc, (const double *)d_cand, &out, nullptr, nullptr, nullptr,
-                                        nullptr, FPF_LAYOUT_SCEN_FASTEST);
-        if (rc < 0) return rc;
-        // loss | status back in one copy
-        h_out.resize(o_stat + Bc);
-        RCHK(hipMemcpy(h_out.data(), d_out, o_stat + Bc, hipMemcpyDeviceToHost));
-        const double *const loss = (const double *)h_out.data();
-        const signed char *const status = (const signed char *)(h_out.data() + o_stat);
-        rc = fpf::take_exchange_fault(feeder);   // (the copies above synchronised the device)
-        if (rc) return rc;
+        // the step sizes in two stages, as fpf_vvc_round: the first VVC_LAZY_FIRST of
+        // every search, then the rest of the searches whose stop rule has not fired
+        // (the reference never solves past stop + 1; the large steps are the slow
+        // ones).  Unsolved candidates: NaN loss, status "converged" (not looked at)
+        lossv.assign((size_t)K * M, NAN);
+        statv.assign((size_t)K * M, (signed char)FPF_CONVERGED);
+        std::vector<int> ks(K);
+        for (int k = 0; k < K; ++k) ks[k] = k;
+        std::vector<double> cst = cstart;   // c_{m0} of each search, by the same products
+        int m0 = 0;
+        while (m0 < M && !ks.empty()) {
+            const int m1 = m0 == 0 ? std::min(M, VVC_LAZY_FIRST) : M, Mk = m1 - m0, Ks = (int)ks.size();
+            const size_t Bc = (size_t)Ks * Mk;
+            // this stage's scenario list and first step sizes, one copy up
+            std::vector<char> up(o_cst + sizeof(double) * Ks);
+            for (int j = 0; j < Ks; ++j) {
+                const int32_t sid = todo[ks[j]];
+                std::memcpy(up.data() + sizeof(int32_t) * j, &sid, sizeof(int32_t));
+                std::memcpy(up.data() + o_cst + sizeof(double) * j, &cst[ks[j]], sizeof(double));
+            }
+            RCHK(hipMemcpy(d_todo, up.data(), up.size(), hipMemcpyHostToDevice));
+            RCHK(fpf::launch_vvc_candidates((const double *)d_pq, nl, B, (const int32_t *)d_todo, Ks, Mk,
+                                            (const int32_t *)d_tri, T, (const double *)d_g, ld, scale, alpha,
+                                            (const double *)((char *)d_todo + o_cst), (double *)d_cand, nullptr));
+            fpf_outputs out;
+            std::memset(&out, 0, sizeof(out));
+            out.loss = (double *)d_out;
+            out.status = (signed char *)((char *)d_out + o_stat);
+            rc = fpf::solve_batch_device_ex(feeder, (int)Bc, (const double *)d_cand, &out, nullptr, nullptr, nullptr,
+                                            nullptr, FPF_LAYOUT_SCEN_FASTEST);
+            if (rc < 0) return rc;
+            // loss | status back in one copy
+            h_out.resize(o_stat + Bc);
+            RCHK(hipMemcpy(h_out.data(), d_out, o_stat + Bc, hipMemcpyDeviceToHost));
+            rc = fpf::take_exchange_fault(feeder);   // (the copy above synchronised the device)
+            if (rc) return rc;
+            const double *const ls = (const double *)h_out.data();
+            const signed char *const ss = (const signed char *)(h_out.data() + o_stat);
+            std::vector<int> open;
+            for (int j = 0; j < Ks; ++j) {
+                const int k = ks[j];
+                std::memcpy(&lossv[(size_t)k * M + m0], ls + (size_t)j * Mk, sizeof(double) * Mk);
+                std::memcpy(&statv[(size_t)k * M + m0], ss + (size_t)j * Mk, Mk);
+                for (int m = 0; m < Mk; ++m) cst[k] = alpha * cst[k];   // c_{m1}
+                int stop, reverse, first_nonconv;
+                stop_rule(&lossv[(size_t)k * M], &statv[(size_t)k * M], m_max, stats[(size_t)todo[k] * 8 + 4], &stop,
+                          &reverse, &first_nonconv);
+                if (stop < 0) open.push_back(k);
+            }
+            ks.swap(open);
+            m0 = m1;
+        }
+        const double *const loss = lossv.data();
+        const signed char *const status = statv.data();
         std::vector<int> next;
         for (int k = 0; k < K; ++k) {
             const int s = todo[k];

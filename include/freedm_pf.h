@@ -496,11 +496,13 @@ int         fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, int
  * Monte Carlo): scenario s is ctrl_dl with its load columns 6..11 replaced by
  * pq[.][.][s] (host, [6][Nl][n_scen]).  The gradients as fpf_vvc_gradient_batch
  * (same arguments and rules: every scenario's (int) load tests must be the
- * control's); then every scenario's m_max + 1 step sizes as ONE device batch,
- * the reference's stop rule per scenario, and one more batch for the scenarios
- * whose search reverses (:1544-1762).  Per scenario: loss_fwd / loss_rev
- * [n_scen][m_max + 1] (may be NULL; rows of scenarios that do not reverse are
- * left as they are), pq_out [6][Nl][n_scen] the scenario's loads after the round
+ * control's); then every scenario's step sizes as device batches (the first 32
+ * of every search as one, the rest of the searches whose stop rule has not
+ * fired as a second), the reference's stop rule per scenario, and the same for
+ * the scenarios whose search reverses (:1544-1762).  Per scenario: loss_fwd /
+ * loss_rev [n_scen][m_max + 1] (may be NULL; rows of scenarios that do not
+ * reverse are left as they are; NaN for step sizes not solved, past the stop),
+ * pq_out [6][Nl][n_scen] the scenario's loads after the round
  * (the kept candidate's Q set-points, Dl = Dl_osize), res [n_scen][13] as
  * fpf_vvc_round's, rstatus [n_scen] the gradient's gstatus (0: the round ran).
  * Returns the number of scenarios with rstatus != 0 or a non-converged candidate
