@@ -21,7 +21,10 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <complex>
 #include <cstring>
 #include <map>
@@ -395,13 +398,20 @@ extern "C" int fpf_vvc_gradient(fpf_feeder *feeder, const double *ctrl_dl, int n
     o.loss = &loss;
     o.vmin = &vmin;
     o.vmax = &vmax;
+    static const bool trace = getenv("FPF_VVC_TRACE") && atoi(getenv("FPF_VVC_TRACE")) != 0;   // (diagnostics)
+    const auto t0 = std::chrono::steady_clock::now();
     const int rc = fpf_solve_batch(feeder, 1, ctrl_dl + (size_t)6 * nl, &o, nullptr);
     if (rc < 0) return rc;
     if (status != FPF_CONVERGED) return FPF_ERR_UNSUPPORTED;   // the reference throws (DPF_return7.cpp:242)
+    const auto t1 = std::chrono::steady_clock::now();
     std::string err;
     double st[4] = {0, 0, 0, 0};
     const int gr = gradient(Table{ctrl_dl, nl}, ncols, z, z_rows, vpolar.data(), nn, fpf_feeder_bkva(feeder),
                             fpf_feeder_bkv(feeder), beta0, ld, g, load_nodes, n_loads, st, &err);
+    if (trace)
+        fprintf(stderr, "vvc_gradient: base solve %.1f us, host gradient %.1f us\n",
+                std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count());
     if (gr != FPF_OK) return gr;
     if (stats) {
         stats[0] = st[0];
@@ -466,9 +476,14 @@ extern "C" int fpf_vvc_round(fpf_feeder *feeder, const double *ctrl_dl, int nl, 
         ls.loss = lossv;
         // the first VVC_LAZY_FIRST step sizes as one batch, the rest only if the
         // stop rule has not fired among them (fpf_vvc.cpp: vvc_line_search)
+        static const bool trace = getenv("FPF_VVC_TRACE") && atoi(getenv("FPF_VVC_TRACE")) != 0;   // (diagnostics)
+        const auto t0 = std::chrono::steady_clock::now();
         rc = fpf::vvc_line_search(feeder, ctrl_dl, nl, ncols, g, load_nodes, n_loads, ld, c0, alpha, m_max,
                                   ploss_orig, &ls, VVC_LAZY_FIRST);
         if (rc < 0) return rc;
+        if (trace)
+            fprintf(stderr, "vvc_round: search pass %d %.1f us (stop %d)\n", pass,
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(), ls.stop);
         // the reference solves candidates 0 .. stop + 1 (two per step) and throws
         // at the first that does not converge
         const int last = ls.stop >= 0 ? ls.stop + 1 : m_max;
