@@ -469,7 +469,11 @@ int         fpf_vvc_gradient_at(const double *ctrl_dl, int nl, int ncols, const 
  * converged scenario's (g and stats[0..3] are 0 unless 0).  Returns the number
  * of scenarios with gstatus != 0, or FPF_ERR_* (FPF_ERR_UNSUPPORTED: a phase
  * with more than 3200 load nodes -- fpf_vvc_gradient solves those on the host;
- * FPF_ERR_EXCHANGE: a paired-kernel base solve's exchange gave up). */
+ * FPF_ERR_EXCHANGE: a paired-kernel base solve's exchange gave up).  Its device
+ * scratch (the batch's loads and base-solve outputs, the plan, the dense J^T of a
+ * chunk of scenarios per phase -- up to 2 GB a phase on large feeders) and a few
+ * pinned host buffers stay with the feeder for the next call (and for
+ * fpf_vvc_round_batch) until fpf_feeder_destroy. */
 int         fpf_vvc_gradient_batch(fpf_feeder *feeder, const double *ctrl_dl, int nl, int ncols,
                                    const double *z, int z_rows, int z_cols, int n_scen, const double *pq,
                                    double beta0, int ld, double *g, double *load_nodes, int *n_loads,
