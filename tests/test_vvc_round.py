@@ -268,3 +268,30 @@ def test_vvc_round_batch_against_oracle(which):
             np.testing.assert_allclose(vvc.s2_setpoints(Da), vvc.s2_setpoints(o["Dl"]), rtol=1e-9, atol=1e-12)
     assert r["n_bad"] == n_throw
     print(f"{which}: {n_rev} of {B} rounds reverse, {n_throw} would throw")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["demo", "dlnew"])
+def test_vvc_round_batch_scratch_reuse(which):
+    """The batch paths keep their scratch on the feeder across calls
+    (fpf::feeder_buf, grown on demand): batches of 8, 64 and 8 rounds on one
+    feeder give exactly what each gives on a fresh feeder -- a grown slot, a
+    reused larger slot and the loads fpf_vvc_round_batch reads back from the
+    gradient's slot all hold the call's own data."""
+    from freedm_amd import PowerFlow
+    f = {"demo": F.demo_feeder, "dlnew": F.dl_new_feeder}[which]()
+    pq8, pq64 = _round_scenarios(f, 8, 21), _round_scenarios(f, 64, 22)
+    keys = ("stop_fwd", "stop_rev", "reversed", "sent", "ploss_orig", "c0", "ploss_after")
+
+    def run(pf, pq):
+        r = pf.vvc_round_batch(f.Dl, pq)
+        return {k: np.asarray(r[k]).copy() for k in keys}, [np.concatenate(x) for x in r["g"]], r["pq"].copy()
+
+    fresh8, fresh64 = run(PowerFlow(f), pq8), run(PowerFlow(f), pq64)
+    pf = PowerFlow(f)
+    for got, want in ((run(pf, pq8), fresh8), (run(pf, pq64), fresh64), (run(pf, pq8), fresh8)):
+        for k in keys:
+            np.testing.assert_array_equal(got[0][k], want[0][k], err_msg=k)
+        for a, b in zip(got[1], want[1]):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(got[2], want[2])
